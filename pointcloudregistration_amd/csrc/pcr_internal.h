@@ -1,0 +1,53 @@
+// Internal helpers shared by the libpcr HIP translation units.
+// gfx950 (MI355X) only: wave64, 160 KiB LDS/CU, 256 CUs in 8 XCDs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/pcr_api.h"
+
+namespace pcr {
+
+// thread-local last-error string, surfaced through pcr_last_error()
+void set_error(const char *fmt, ...);
+void clear_error();
+
+// Per-device scratch owned by the library.  Grows on demand; superseded buffers
+// stay allocated until process exit so kernels still in flight on another
+// stream never see their scratch freed.  Mutex-guarded.
+void *workspace(int slot, size_t bytes);
+
+inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+constexpr int kCUs = 256;
+
+}  // namespace pcr
+
+#define PCR_HIP_CHECK(expr)                                                            \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            pcr::set_error("%s failed at %s:%d: %s", #expr, __FILE__, __LINE__,       \
+                           hipGetErrorString(e_));                                     \
+            return PCR_ERR_HIP;                                                        \
+        }                                                                              \
+    } while (0)
+
+#define PCR_REQUIRE(cond, code, ...)                                                   \
+    do {                                                                               \
+        if (!(cond)) {                                                                 \
+            pcr::set_error(__VA_ARGS__);                                               \
+            return (code);                                                             \
+        }                                                                              \
+    } while (0)
+
+#define PCR_LAUNCH_CHECK()                                                             \
+    do {                                                                               \
+        hipError_t e_ = hipGetLastError();                                             \
+        if (e_ != hipSuccess) {                                                        \
+            pcr::set_error("kernel launch failed at %s:%d: %s", __FILE__, __LINE__,    \
+                           hipGetErrorString(e_));                                     \
+            return PCR_ERR_HIP;                                                        \
+        }                                                                              \
+    } while (0)
