@@ -2,11 +2,14 @@
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--points NPTS]
 
-Workload (BASELINE.json configs[3]): P synthetic TOF/PC-style
-cloud pairs of NPTS points per GPU rank (weak scaling: pair ids are
-rank*P .. rank*P+P-1), inputs resident in HBM.  One step = one pass of the hot
-path over the batch.  Multi-GPU: one process per GPU (torchrun), no data-path
-collective, barrier + synchronize around the timed loop, max over ranks.
+Workload = BASELINE.json configs[3]: P synthetic TOF/PC-style
+cloud pairs of NPTS points with D=32 descriptors per GPU rank (weak scaling: rank
+r owns pairs r*P .. r*P+P-1, generated locally), inputs resident in HBM.
+One step = the whole pair pipeline over the batch (pointcloudregistration_amd/
+pipeline.py): exact mutual feature NN -> RANSAC (RANSAC.py parameters) -> ICP
+-> nnd Chamfer quality, then the RCCL all-gather of the per-pair records.
+Multi-GPU: one process per GPU (torchrun), barrier + synchronize around the timed
+loop, max over ranks; value = all pairs processed / that time.
 """
 from __future__ import annotations
 
@@ -22,17 +25,20 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MI355X_PEAK_FP32_TFLOPS = 157.3   # vector & f32-MFMA peak (MI355X_MICROARCH.md)
-MI355X_PEAK_HBM_GBS = 8000.0
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak
+PEAK_HBM_GBS = 8000.0
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=256)
     ap.add_argument("--points", type=int, default=8192)
+    ap.add_argument("--dim", type=int, default=32)
+    ap.add_argument("--feat-noise", type=float, default=1.0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -63,89 +69,100 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def make_clouds(pairs, npts, rank):
-    """Synthetic pair batch generated on the GPU (seeded per rank)."""
-    g = torch.Generator(device="cuda").manual_seed(1000 + rank)
-    src = torch.rand(pairs, npts, 3, device="cuda", generator=g) * 2 - 1
-    tgt = torch.rand(pairs, npts, 3, device="cuda", generator=g) * 2 - 1
-    return src, tgt
-
-
-def cpu_baseline_nnd(npts, budget_s=12.0):
-    """Reference CPU nndistance (oracle/_ref, compiled from the reference's
-    my_lib.cpp) on a bounded sample of the same workload, single thread."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle", "_ref"))
-    try:
-        import torch_nndistance_ref as ref
-        kind = "reference"
-        fwd = ref.nnd_forward
-    except ImportError:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        kind = "port"
-
-        def fwd(a, b, d1, d2, i1, i2):
-            r = oracle.nnd_forward(a.numpy(), b.numpy())
-            d1.copy_(torch.from_numpy(r[0]))
-            return 1
-    torch.set_num_threads(1)
-    rng = np.random.default_rng(0)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or done == 0:
-        a = torch.from_numpy(rng.random((1, npts, 3), dtype=np.float32) * 2 - 1)
-        b = torch.from_numpy(rng.random((1, npts, 3), dtype=np.float32) * 2 - 1)
-        d1, d2 = torch.zeros(1, npts), torch.zeros(1, npts)
-        i1 = torch.zeros(1, npts, dtype=torch.int32)
-        i2 = torch.zeros(1, npts, dtype=torch.int32)
-        fwd(a, b, d1, d2, i1, i2)
+def cpu_baseline(batch, params, budget_s):
+    """The oracle's C restatement of the same per-pair pipeline (oracle/pcr_oracle.c:
+    featnn both ways -> mutual corres -> sequential RANSAC -> ICP -> nnd Chamfer) on
+    the first pairs of this rank's workload, for ~budget_s seconds.  featnn uses
+    OpenMP (OMP_NUM_THREADS threads); the rest is single-threaded like the reference."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    rp, ip = params.ransac, params.icp
+    done, t0, Ts = 0, time.perf_counter(), []
+    while (time.perf_counter() - t0 < budget_s or done == 0) and done < batch.src.shape[0]:
+        p = done
+        nn12 = oracle.featnn(batch.src_feat[p], batch.tgt_feat[p])
+        nn21 = oracle.featnn(batch.tgt_feat[p], batch.src_feat[p])
+        co = oracle.corres(nn12, nn21, rp.mutual_filter, rp.ransac_n)
+        r = oracle.ransac(batch.src[p], batch.tgt[p], co, rp.max_correspondence_distance,
+                          rp.ransac_n, rp.edge_length_ratio, None, rp.max_iteration,
+                          rp.confidence, rp.seed, p)
+        ic = oracle.icp(batch.src[p], batch.tgt[p], ip.max_correspondence_distance, init=r["T"])
+        T = ic["T"]
+        aligned = (batch.src[p].astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+        oracle.nnd_forward(aligned[None], batch.tgt[p][None])
+        Ts.append((r["T"], T))
         done += 1
     el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "pairs/s", "cores": 1, "kind": kind,
-            "sample": f"{done} pairs x {npts} pts nndistance forward (both directions), "
-                      f"single thread, {el:.1f}s"}
+    return ({"value": done / el, "unit": "pairs/s", "cores": threads, "kind": "port",
+             "sample": f"{done} of the workload's pairs ({batch.src.shape[1]} pts, D="
+                       f"{batch.src_feat.shape[2]}) through the oracle pipeline in {el:.1f}s; "
+                       f"feature-NN on {threads} OpenMP threads, RANSAC/ICP/Chamfer 1 thread"},
+            Ts)
 
 
 def main():
     args = parse()
     rank, world, local = dist_setup()
-    from pointcloudregistration_amd import nndistance as nd
+    from pointcloudregistration_amd import _lib, synth
+    from pointcloudregistration_amd.multigpu import gather_records, weak_shard
+    from pointcloudregistration_amd.pipeline import PairPipeline, default_params
 
-    P, N = args.pairs, args.points
-    src, tgt = make_clouds(P, N, rank)
-    d1 = torch.empty(P, N, device="cuda")
-    d2 = torch.empty(P, N, device="cuda")
-    i1 = torch.empty(P, N, dtype=torch.int32, device="cuda")
-    i2 = torch.empty(P, N, dtype=torch.int32, device="cuda")
+    first, P = weak_shard(args.pairs, rank)
+    N, D = args.points, args.dim
+    batch = synth.make_batch(P, n=N, m=N, d=D, base_seed=1000, first_pair=first,
+                             feat_noise=args.feat_noise)
+    params = default_params(seed=0)
+    pipe = PairPipeline(batch.src, batch.tgt, batch.src_feat, batch.tgt_feat, params,
+                        pair_ids=np.arange(first, first + P, dtype=np.int32))
 
     def step():
-        nd.nnd_forward_cuda(src, tgt, d1, d2, i1, i2)
+        pipe.run()
+        return gather_records(pipe.records(), world)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    _lib.profile_enable(True)
+    for pid in range(5):
+        _lib.profile_read(pid, reset=True)
     barrier(world)
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
     for _ in range(args.steps):
-        step()
-    ev1.record()
+        rec = step()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    wall = max_over_ranks(wall, world)
-    kern_ms = ev0.elapsed_time(ev1) / args.steps   # nnd kernel(s) per step, same stream
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    prof = {name: _lib.profile_read(pid) for name, pid in
+            (("feature_screen", _lib.PROF_FEAT_SCREEN), ("nnd_fwd", _lib.PROF_NND_FWD),
+             ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
+             ("icp", _lib.PROF_ICP))}
+    _lib.profile_enable(False)
+
+    # stage split of one extra (untimed) step
+    pipe.run(time_stages=True)
+    torch.cuda.synchronize()
+    stages = dict(zip(("feature_match", "corres+ransac", "icp", "transform", "chamfer"),
+                      pipe.stage_ms()))
+
+    # dominant kernel: the f32-MFMA feature-distance screen (one launch = one
+    # direction for all P pairs: P*N*M*D MACs = 2*P*N*M*D flops)
+    ms_tot, launches = prof["feature_screen"]
+    per_launch_ms = ms_tot / max(launches, 1)
+    flops_launch = 2.0 * P * N * N * D
+    achieved = flops_launch / (per_launch_ms * 1e-3) / 1e12
+
+    recs = rec.cpu().numpy()
+    mine = recs[rank * P:(rank + 1) * P]
+    T_icp = mine[:, 16:32].reshape(P, 4, 4)
+    rre, rte = synth.rre_rte(T_icp[:, :3, :3], T_icp[:, :3, 3], batch.R, batch.t)
 
     total_pairs = P * world * args.steps
-    value = total_pairs / wall
-    # roofline of the dominant kernel (nnd sweep): 2*N*M pair evals x 8 flops per pair
-    flops = 2.0 * N * N * 8 * P
-    achieved = flops / (kern_ms * 1e-3) / 1e12
     out = {
         "metric": "TOF/PC pairs/sec (8192 pts)",
-        "value": value,
+        "value": total_pairs / wall,
         "unit": "pairs/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -154,17 +171,39 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (uniform clouds generated on device, seeded per rank)",
-        "config": {"workload": "c4_chamfer_leg", "pairs_per_gpu": P, "points": N,
-                   "parallelism": f"pair-sharded x{world}"},
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": MI355X_PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / MI355X_PEAK_FP32_TFLOPS,
-                     "traffic": None, "kernel": "nnd_fwd_kernel",
-                     "kernel_ms": kern_ms},
+        "dtype": "f32 xyz/features; f64 RANSAC/ICP; f32-in MFMA screen + f64 exact re-rank",
+        "data": f"synthetic: procedural surface pairs, ROPNet-style augmentation, D={D} "
+                f"descriptors (noise {args.feat_noise}), generated per rank (seeds 1000+pair)",
+        "config": {"workload": "C4: batch of augmented TOF/PC pairs (featNN+RANSAC+ICP+Chamfer)",
+                   "pairs_per_gpu": P, "points": N, "feature_dim": D,
+                   "ransac": "d=0.04 mutual n=3 edge0.9 dist0.04 (100000,0.999)",
+                   "icp": "d=0.02 (1e-6,1e-6,30)", "parallelism": f"pair-sharded x{world}"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_F32_MFMA_TFLOPS,
+                     "traffic": None, "kernel": "featnn_screen (v_mfma_f32_32x32x2_f32)",
+                     "kernel_ms_per_launch": per_launch_ms, "launches": launches,
+                     "flops_per_launch": flops_launch},
+        "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+        "stages_ms": stages,
+        "accuracy": {"rre_deg_median": float(np.median(rre)), "rre_deg_max": float(np.max(rre)),
+                     "rte_median": float(np.median(rte)), "rte_max": float(np.max(rte)),
+                     "ransac_iters_mean": float(mine[:, 37].mean()),
+                     "mutual_corres_mean": float(mine[:, 39].mean())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_nnd(N)
+        cb, Ts = cpu_baseline(batch, params, args.cpu_budget)
+        out["cpu_baseline"] = cb
+        k = len(Ts)
+        T_r = mine[:k, 0:16].reshape(k, 4, 4)
+        same_r = all(np.array_equal(T_r[i], Ts[i][0]) for i in range(k))
+        same_i = all(np.array_equal(T_icp[i], Ts[i][1]) for i in range(k))
+        d_rre, d_rte = synth.rre_rte(T_icp[:k, :3, :3], T_icp[:k, :3, 3],
+                                     np.stack([t[1][:3, :3] for t in Ts]),
+                                     np.stack([t[1][:3, 3] for t in Ts]))
+        out["accuracy"]["vs_cpu_ref"] = {"pairs": k, "T_ransac_bitexact": bool(same_r),
+                                         "T_icp_bitexact": bool(same_i),
+                                         "rre_deg_max": float(np.max(d_rre)),
+                                         "rte_max": float(np.max(d_rte))}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

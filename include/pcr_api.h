@@ -32,6 +32,13 @@ typedef void *pcr_stream_t; /* hipStream_t */
 const char *pcr_last_error(void);
 int pcr_version(void);
 
+/* Optional per-kernel timing with HIP events recorded on the launch stream
+ * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,
+ * 3 ICP, 4 RANSAC hypotheses).  pcr_profile_read synchronizes the pending
+ * events and returns the accumulated milliseconds and launch count. */
+void pcr_profile_enable(int32_t on);
+int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset);
+
 /* ---------------------------------------------------------------------------
  * a1 -- brute-force bidirectional 1-NN ("nnd" / Chamfer building block).
  * Replaces nnd_forward_cuda (dip/torch-nndistance/src/my_lib_cuda.cpp:25-41)
@@ -59,6 +66,117 @@ int pcr_nnd_backward(const float *xyz1, const float *xyz2, const float *graddist
                      const float *graddist2, const int32_t *idx1, const int32_t *idx2,
                      int32_t b, int32_t n, int32_t m, float *gradxyz1, float *gradxyz2,
                      pcr_stream_t stream);
+
+
+/* ===========================================================================
+ * Registration path (batched over P cloud pairs).  Layout: pair p's source
+ * points are src_xyz[p*Nmax*3 .. +n_src[p]*3) (f32, AoS), features
+ * src_feat[p*Nmax*D ..] (f32, row-major); likewise tgt with Mmax.  n_src /
+ * n_tgt may be NULL (= all Nmax / Mmax points valid).
+ * ======================================================================== */
+
+/* ---------------------------------------------------------------------------
+ * a5 -- exact feature-space 1-NN, both directions.  Replaces the KD-tree
+ * SearchKNN(k=1) loops inside Open3D registration_ransac_based_on_feature_matching
+ * (called at DataPreparation/RANSAC.py:43, dip/demo.py:43,
+ * c2p-net/ngenet/utils/o3d.py:174) and vote.get_coor_points
+ * (c2p-net/ngenet/models/vote.py:6-9).  nn12 (P,Nmax): argmin_j |f_i-g_j|^2,
+ * nn21 (P,Mmax): argmin_i; distances in f64, lowest index on ties.  1 <= D <= 128.
+ * ------------------------------------------------------------------------- */
+int pcr_feature_match(const float *src_feat, const float *tgt_feat, int32_t P, int32_t Nmax,
+                      int32_t Mmax, int32_t D, const int32_t *n_src, const int32_t *n_tgt,
+                      int32_t *nn12, int32_t *nn21, pcr_stream_t stream);
+
+/* mutual filter + ordered compaction: corres (P,Nmax,2) = (i, nn12[i]) for i with
+ * nn21[nn12[i]] == i in increasing i, or all (i, nn12[i]) when fewer than
+ * 3*ransac_n survive or mutual_filter == 0 (Open3D 0.13 semantics). */
+int pcr_correspondences(const int32_t *nn12, const int32_t *nn21, int32_t P, int32_t Nmax,
+                        int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt,
+                        int32_t mutual_filter, int32_t ransac_n, int32_t *corres,
+                        int32_t *n_corres, pcr_stream_t stream);
+
+/* RANSAC parameters (Open3D names; RANSAC.py:43-52). */
+typedef struct pcr_ransac_params {
+    double max_correspondence_distance; /* verification radius d                         */
+    double edge_length_ratio;           /* CorrespondenceCheckerBasedOnEdgeLength; <=0 off */
+    double distance_check;              /* CorrespondenceCheckerBasedOnDistance;   <=0 off */
+    double confidence;                  /* RANSACConvergenceCriteria.confidence            */
+    int32_t max_iteration;              /* RANSACConvergenceCriteria.max_iteration          */
+    int32_t ransac_n;                   /* 3..8                                            */
+    int32_t mutual_filter;              /* used by pcr_register_feature_ransac             */
+    int32_t reserved;
+    uint64_t seed;                      /* Philox key; hypothesis = f(seed, pair_id, itr)  */
+} pcr_ransac_params;
+
+/* ---------------------------------------------------------------------------
+ * a6/a7 -- RANSAC hypothesize-and-verify on given correspondences.
+ * Replaces Open3D RegistrationRANSACBasedOnCorrespondence.  corres (P,Kmax,2)
+ * with n_corres[p] valid rows; pair_ids (P) optional (default p) keys the
+ * hypothesis stream.  Outputs: T (P,16) f64 row-major 4x4, fitness_rmse (P,2),
+ * stats (P,5) = {iterations, validated, best_itr, status(1 ok/0 none/-1 bad
+ * input), n_correspondences}, corr_tgt (P,Nmax) target index per source point
+ * or -1 (optional), inlier_mask (P, ceil(Nmax/32)) bitset (optional).
+ * Blocks the host between hypothesis waves (one 4-byte readback per wave).
+ * ------------------------------------------------------------------------- */
+int pcr_ransac_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t Nmax,
+                     int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt,
+                     const int32_t *corres, const int32_t *n_corres, int32_t Kmax,
+                     const uint32_t *pair_ids, const pcr_ransac_params *params, double *T,
+                     double *fitness_rmse, int32_t *stats, int32_t *corr_tgt,
+                     uint32_t *inlier_mask, pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * a5+a6+a7 composite: feature matching -> (mutual) correspondences -> RANSAC.
+ * Replaces registration_ransac_based_on_feature_matching (RANSAC.py:43-52) for
+ * P pairs at once; outputs as pcr_ransac_batch.  `scratch` sizing is internal.
+ * ------------------------------------------------------------------------- */
+int pcr_register_feature_ransac(const float *src_xyz, const float *tgt_xyz,
+                                const float *src_feat, const float *tgt_feat, int32_t P,
+                                int32_t Nmax, int32_t Mmax, int32_t D, const int32_t *n_src,
+                                const int32_t *n_tgt, const uint32_t *pair_ids,
+                                const pcr_ransac_params *params, double *T,
+                                double *fitness_rmse, int32_t *stats, int32_t *corr_tgt,
+                                uint32_t *inlier_mask, pcr_stream_t stream);
+
+/* ICP parameters (Open3D ICPConvergenceCriteria defaults 1e-6, 1e-6, 30). */
+typedef struct pcr_icp_params {
+    double max_correspondence_distance;
+    double relative_fitness;
+    double relative_rmse;
+    int32_t max_iteration;
+    int32_t reserved;
+} pcr_icp_params;
+
+/* ---------------------------------------------------------------------------
+ * a8 -- point-to-point ICP.  Replaces Open3D registration_icp
+ * (DataPreparation/RANSAC.py:61-63).  init (P,16) f64; outputs T (P,16),
+ * fitness_rmse (P,2), stats (P,2) = {iterations, n_correspondences}, corr_tgt
+ * (P,Nmax) optional: target index of each source point in the final
+ * correspondence set (Open3D result.correspondence_set) or -1.
+ * ------------------------------------------------------------------------- */
+int pcr_icp_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t Nmax,
+                  int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt, const double *init,
+                  const pcr_icp_params *params, double *T, double *fitness_rmse, int32_t *stats,
+                  int32_t *corr_tgt, pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * radius-limited 1-NN (Open3D KDTreeFlann::SearchHybrid(r, max_nn=1), used by
+ * RANSAC verification / ICP): for each f64 query (P,Qmax,3) the nearest target
+ * point with d^2 < float(r*r), lowest index on ties; idx -1 if none, d2 optional.
+ * ------------------------------------------------------------------------- */
+int pcr_radius_nn(const float *tgt_xyz, int32_t P, int32_t Mmax, const int32_t *n_tgt,
+                  const double *queries, int32_t Qmax, const int32_t *n_q, double r,
+                  int32_t *idx, double *d2, pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * a9 -- batched weighted Procrustes (B items of N points).  Replaces the
+ * torch.svd Kabsch of ROPNet weighted_icp (model_utils.py:105-139; abs_weights=0,
+ * eps=1e-8) and NDP rigid_fit (deformationpyramid/model/geometry.py:8-34;
+ * abs_weights=1, eps=1e-4).  T (B,12) f64 = [R | t] row-major, tgt ~ R src + t.
+ * ------------------------------------------------------------------------- */
+int pcr_procrustes_batch(const float *src, const float *tgt, const float *weights, int32_t B,
+                         int32_t N, int32_t abs_weights, double eps, double *T,
+                         pcr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -63,3 +63,132 @@ def nnd_backward(xyz1, xyz2, gd1, gd2, idx1, idx2):
     lib().oracle_nnd_backward(_p(xyz1), _p(xyz2), _p(gd1), _p(gd2), _p(idx1), _p(idx2),
                               b, n, m, _p(g1), _p(g2))
     return g1, g2
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _setup_sigs():
+    L = lib()
+    c = ctypes
+    L.oracle_det_log.restype = c.c_double
+    L.oracle_det_log.argtypes = [c.c_double]
+    L.oracle_est_k.restype = c.c_double
+    L.oracle_est_k.argtypes = [c.c_double, c.c_int, c.c_double]
+    L.oracle_radius_thr.restype = c.c_double
+    L.oracle_radius_thr.argtypes = [c.c_double]
+    L.oracle_procrustes_batch.argtypes = [c.c_void_p] * 3 + [c.c_int, c.c_int, c.c_int, c.c_double, c.c_void_p]
+    L.oracle_ransac.restype = c.c_int
+    L.oracle_ransac.argtypes = ([c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_int,
+                                 c.c_double, c.c_int, c.c_double, c.c_double, c.c_int, c.c_double,
+                                 c.c_uint64, c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p])
+    L.oracle_icp.restype = c.c_int
+    L.oracle_icp.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_double,
+                             c.c_int, c.c_double, c.c_double, c.c_void_p, c.c_void_p, c.c_void_p]
+    L.oracle_radius_nn.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_double, c.c_int,
+                                   c.c_void_p, c.c_void_p]
+    L.oracle_featnn.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
+    L.oracle_corres.restype = c.c_int
+    L.oracle_corres.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
+    L.oracle_philox.argtypes = [c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
+    L.oracle_horn_rotation.argtypes = [c.c_void_p, c.c_void_p]
+    return L
+
+
+_sigs = None
+
+
+def L():
+    global _sigs
+    if _sigs is None:
+        _sigs = _setup_sigs()
+    return _sigs
+
+
+def det_log(x):
+    return L().oracle_det_log(float(x))
+
+
+def est_k(w, n, conf):
+    return L().oracle_est_k(float(w), int(n), float(conf))
+
+
+def philox(seed, pair, itr, block=0):
+    out = np.zeros(4, np.uint32)
+    L().oracle_philox(seed, pair, itr, block, _p(out))
+    return out
+
+
+def horn_rotation(S):
+    S = _f64(S).reshape(9)
+    R = np.zeros(9, np.float64)
+    L().oracle_horn_rotation(_p(S), _p(R))
+    return R.reshape(3, 3)
+
+
+def procrustes_batch(src, tgt, w, absw, eps):
+    """(B,N,3),(B,N,3),(B,N) -> T (B,3,4) f64 (weighted_icp: absw=0,eps=1e-8;
+    rigid_fit: absw=1, eps=1e-4)."""
+    src, tgt, w = _f32(src), _f32(tgt), _f32(w)
+    b, n = src.shape[0], src.shape[1]
+    T = np.zeros((b, 3, 4), np.float64)
+    L().oracle_procrustes_batch(_p(src), _p(tgt), _p(w), b, n, int(absw), float(eps), _p(T))
+    return T
+
+
+def featnn(F, G):
+    F, G = _f32(F), _f32(G)
+    nn = np.zeros(F.shape[0], np.int32)
+    L().oracle_featnn(_p(F), _p(G), F.shape[0], G.shape[0], F.shape[1], _p(nn))
+    return nn
+
+
+def corres(nn12, nn21, mutual=True, ransac_n=3):
+    nn12, nn21 = _i32(nn12), _i32(nn21)
+    out = np.zeros((nn12.shape[0], 2), np.int32)
+    k = L().oracle_corres(_p(nn12), _p(nn21), nn12.shape[0], int(mutual), int(ransac_n), _p(out))
+    return out[:k].copy()
+
+
+def radius_nn(tgt, queries, r, use_grid=True):
+    tgt, q = _f64(tgt), _f64(queries)
+    idx = np.zeros(q.shape[0], np.int32)
+    d2 = np.zeros(q.shape[0], np.float64)
+    L().oracle_radius_nn(_p(tgt), tgt.shape[0], _p(q), q.shape[0], float(r), int(use_grid),
+                         _p(idx), _p(d2))
+    return idx, d2
+
+
+def ransac(src, tgt, corr, max_corr_dist, ransac_n=3, edge_ratio=0.9, dist_check=None,
+           max_iteration=100000, confidence=0.999, seed=0, pair_id=0):
+    """Returns dict(T (4,4), fitness, inlier_rmse, correspondence_set (K,2), iters,
+    validated, best_itr, found)."""
+    src, tgt, corr = _f32(src), _f32(tgt), _i32(corr).reshape(-1, 2)
+    if dist_check is None:
+        dist_check = max_corr_dist
+    T = np.zeros(16, np.float64)
+    fr = np.zeros(2, np.float64)
+    co = np.zeros((src.shape[0], 2), np.int32)
+    st = np.zeros(4, np.int32)
+    nc = L().oracle_ransac(_p(src), src.shape[0], _p(tgt), tgt.shape[0], _p(corr), corr.shape[0],
+                           float(max_corr_dist), int(ransac_n), float(edge_ratio), float(dist_check),
+                           int(max_iteration), float(confidence), int(seed), int(pair_id),
+                           _p(T), _p(fr), _p(co), _p(st))
+    return dict(T=T.reshape(4, 4), fitness=fr[0], inlier_rmse=fr[1],
+                correspondence_set=co[:nc].copy(), iters=int(st[0]), validated=int(st[1]),
+                best_itr=int(st[2]), found=int(st[3]))
+
+
+def icp(src, tgt, max_corr_dist, init=None, max_iteration=30, relative_fitness=1e-6,
+        relative_rmse=1e-6):
+    src, tgt = _f32(src), _f32(tgt)
+    init = np.eye(4) if init is None else init
+    init = _f64(init).reshape(16)
+    T = np.zeros(16, np.float64)
+    fr = np.zeros(2, np.float64)
+    it = np.zeros(1, np.int32)
+    nc = L().oracle_icp(_p(src), src.shape[0], _p(tgt), tgt.shape[0], _p(init),
+                        float(max_corr_dist), int(max_iteration), float(relative_fitness),
+                        float(relative_rmse), _p(T), _p(fr), _p(it))
+    return dict(T=T.reshape(4, 4), fitness=fr[0], inlier_rmse=fr[1], n_corr=nc, iters=int(it[0]))

@@ -32,10 +32,37 @@ _f32 = ctypes.c_float
 _f64 = ctypes.c_double
 _u64 = ctypes.c_uint64
 
+
+
+class RansacParams(ctypes.Structure):
+    """pcr_ransac_params (include/pcr_api.h)."""
+    _fields_ = [("max_correspondence_distance", _f64), ("edge_length_ratio", _f64),
+                ("distance_check", _f64), ("confidence", _f64), ("max_iteration", _i32),
+                ("ransac_n", _i32), ("mutual_filter", _i32), ("reserved", _i32), ("seed", _u64)]
+
+
+class IcpParams(ctypes.Structure):
+    """pcr_icp_params (include/pcr_api.h)."""
+    _fields_ = [("max_correspondence_distance", _f64), ("relative_fitness", _f64),
+                ("relative_rmse", _f64), ("max_iteration", _i32), ("reserved", _i32)]
+
+
+_rp = ctypes.POINTER(RansacParams)
+_ip = ctypes.POINTER(IcpParams)
+
 # name -> argtypes (restype is always c_int); keep in sync with include/pcr_api.h
 SIGNATURES = {
     "pcr_nnd_forward": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p],
     "pcr_nnd_backward": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p],
+    "pcr_feature_match": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p],
+    "pcr_correspondences": [_p, _p, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p],
+    "pcr_ransac_batch": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _rp, _p, _p, _p,
+                         _p, _p, _p],
+    "pcr_register_feature_ransac": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _rp,
+                                    _p, _p, _p, _p, _p, _p],
+    "pcr_icp_batch": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _ip, _p, _p, _p, _p, _p],
+    "pcr_radius_nn": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _p, _p, _p],
+    "pcr_procrustes_batch": [_p, _p, _p, _i32, _i32, _i32, _f64, _p, _p],
 }
 
 
@@ -59,6 +86,10 @@ def load():
         lib.pcr_last_error.restype = ctypes.c_char_p
         lib.pcr_last_error.argtypes = []
         lib.pcr_version.restype = ctypes.c_int
+        lib.pcr_profile_enable.restype = None
+        lib.pcr_profile_enable.argtypes = [_i32]
+        lib.pcr_profile_read.restype = ctypes.c_int
+        lib.pcr_profile_read.argtypes = [_i32, ctypes.POINTER(_f64), ctypes.POINTER(_i64), _i32]
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
@@ -68,7 +99,23 @@ def load():
 
 
 def exported_symbols():
-    return ["pcr_last_error", "pcr_version"] + list(SIGNATURES)
+    return ["pcr_last_error", "pcr_version", "pcr_profile_enable", "pcr_profile_read"] + list(SIGNATURES)
+
+
+PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
+
+
+def profile_enable(on=True):
+    load().pcr_profile_enable(1 if on else 0)
+
+
+def profile_read(pid, reset=True):
+    """(total_ms, launches) of kernel slot `pid` since the last reset."""
+    ms, cnt = _f64(0.0), _i64(0)
+    rc = load().pcr_profile_read(pid, ctypes.byref(ms), ctypes.byref(cnt), 1 if reset else 0)
+    if rc != PCR_OK:
+        raise PcrError(load().pcr_last_error().decode())
+    return ms.value, cnt.value
 
 
 def call(name, *args):

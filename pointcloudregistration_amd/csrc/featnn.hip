@@ -1,0 +1,324 @@
+// a5: exact feature-space 1-NN for batches of cloud pairs + mutual filter.
+//
+// Reference semantics: Open3D KDTreeFlann SearchKNN(k=1) over Feature.data
+// inside registration_ransac_based_on_feature_matching (call sites
+// DataPreparation/RANSAC.py:43-52, dip/demo.py:43-52, ngenet/utils/o3d.py:174-180)
+// and torch.cdist + min in c2p-net/ngenet/models/vote.py:6-9.  Contract
+// (oracle_featnn): argmin_j D_ij, D_ij = sum_k ((double)f_ik - (double)g_jk)^2
+// summed sequentially in f64, lowest index on ties.
+//
+// MI355X design:
+//  1. pack: features -> MFMA operand layout [tile][k-pair s][lane], lane l holds
+//     row 32t+(l&31), dim 2s+(l>>5) (both A and B of v_mfma_f32_32x32x2_f32 use
+//     this map), zero-padded to a multiple of 16 dims; squared norms.
+//  2. screen: each wave owns 32 query rows (A = -2*q kept in VGPRs) and sweeps
+//     every 32-candidate tile: C is seeded with |g_j|^2, 8*KCH f32-in MFMAs give
+//     s_ij = |g_j|^2 - 2 q_i.g_j as an exact k-ordered fmaf chain; a running
+//     top-2 per row (v_med3 + v_min + cndmask) is kept per lane and merged
+//     across lanes once at the end.
+//  3. certify: |s^ - s| <= (K+1) 2^-24 (|q_i| + max_j |g_j|)^2.  If the top-2 gap
+//     exceeds 2x that bound (x2 safety), the winner is the exact f64 argmin; else
+//     the row is queued for an exact f64 rescan (4. rescan, one wave per row).
+//  The screen is the MFMA-bound kernel (4.3 GFLOP per 8192^2 x 32 direction).
+#include "pcr_internal.h"
+#include "scan.h"
+
+namespace pcr {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int count_of(const int32_t *n, int p, int Nmax) {
+    return n ? min(max(n[p], 0), Nmax) : Nmax;
+}
+
+// X (P, Nmax, D) -> Xp (P, ntiles, S2, 64); cn/nrm (P, ntiles*32); gmax (P) float bits
+__global__ __launch_bounds__(64) void feat_pack(const float *X, const int32_t *n, int Nmax, int D,
+                                                int S2, int ntiles, float *Xp, float *cn,
+                                                float *nrm, unsigned *gmax) {
+    const int p = blockIdx.y, t = blockIdx.x, l = threadIdx.x;
+    const int cnt = count_of(n, p, Nmax);
+    const int row = t * 32 + (l & 31), h = l >> 5;
+    const bool valid = row < cnt;
+    const float *x = X + ((size_t)p * Nmax + (valid ? row : 0)) * D;
+    float *dst = Xp + (((size_t)p * ntiles + t) * S2) * 64 + l;
+    for (int s = 0; s < S2; ++s) {
+        const int k = 2 * s + h;
+        dst[(size_t)s * 64] = (valid && k < D) ? x[k] : 0.0f;
+    }
+    if (h == 0) {
+        float c = __builtin_inff(), r = 0.0f;
+        if (valid) {
+            double acc = 0.0;
+            for (int k = 0; k < D; ++k) acc = acc + (double)x[k] * (double)x[k];
+            c = (float)acc;
+            r = (float)__builtin_sqrt(acc);
+            atomicMax(gmax + p, __float_as_uint(r));
+        }
+        cn[(size_t)p * ntiles * 32 + row] = c;
+        nrm[(size_t)p * ntiles * 32 + row] = r;
+    }
+}
+
+struct ScreenArgs {
+    const float *Qp, *Cp;   // packed queries / candidates
+    const float *ccn;       // candidate |g|^2 (+inf on padding)
+    const float *qnrm;      // query |q|
+    const unsigned *cgmax;  // max candidate |g| (float bits) per pair
+    const int32_t *nq, *nc; // valid counts (may be null)
+    int Nqmax, Ncmax, ntq, ntc, S2;
+    int32_t *nn;            // (P, Nqmax)
+    int *list;              // ambiguous rows: p*Nqmax + row
+    int *list_count;
+};
+
+template <int KCH>
+__global__ __launch_bounds__(256) void featnn_screen(ScreenArgs a) {
+    constexpr int S2 = 8 * KCH;
+    const int p = blockIdx.y;
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int qt = blockIdx.x * 4 + wid;
+    const int nq = count_of(a.nq, p, a.Nqmax);
+    if (qt * 32 >= nq) return;  // wave-uniform
+    const int nc = count_of(a.nc, p, a.Ncmax);
+    const int ntc = (nc + 31) >> 5;
+
+    float A[S2];
+    const float *qp = a.Qp + (((size_t)p * a.ntq + qt) * S2) * 64 + l;
+#pragma unroll
+    for (int s = 0; s < S2; ++s) A[s] = -2.0f * qp[(size_t)s * 64];
+
+    float b1[16], b2[16];
+    int i1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); i1[r] = 0; }
+
+    const float *cbase = a.Cp + ((size_t)p * a.ntc * S2) * 64 + l;
+    const float *cnb = a.ccn + (size_t)p * a.ntc * 32 + (l & 31);
+    for (int ct = 0; ct < ntc; ++ct) {
+        const float *cp = cbase + (size_t)ct * S2 * 64;
+        float B[S2];
+#pragma unroll
+        for (int s = 0; s < S2; ++s) B[s] = cp[(size_t)s * 64];
+        const float c0 = cnb[ct * 32];
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = c0;
+#pragma unroll
+        for (int s = 0; s < S2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], B[s], acc, 0, 0, 0);
+        const int j = ct * 32 + (l & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float v = acc[r];
+            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], v);
+            const bool c = v < b1[r];
+            b1[r] = c ? v : b1[r];
+            i1[r] = c ? j : i1[r];
+        }
+    }
+    // merge the 32 lanes of each half (same rows, disjoint candidate classes)
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float ob1 = __shfl_xor(b1[r], o, 64);
+            const float ob2 = __shfl_xor(b2[r], o, 64);
+            const int oi1 = __shfl_xor(i1[r], o, 64);
+            const bool take = (ob1 < b1[r]) || (ob1 == b1[r] && oi1 < i1[r]);
+            const float nb2 = fminf(fmaxf(b1[r], ob1), fminf(b2[r], ob2));
+            b1[r] = take ? ob1 : b1[r];
+            i1[r] = take ? oi1 : i1[r];
+            b2[r] = nb2;
+        }
+    }
+    const int h = l >> 5, lr = l & 31;
+    if (lr >= 16) return;
+    float mb1 = 0.f, mb2 = 0.f;
+    int mi1 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+    if (row >= nq) return;
+    a.nn[(size_t)p * a.Nqmax + row] = mi1;
+    const double G = (double)__uint_as_float(a.cgmax[p]);
+    const double qn = (double)a.qnrm[(size_t)p * a.ntq * 32 + row];
+    const double K = 2.0 * S2;
+    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (qn + G) * (qn + G);
+    if (!((double)mb2 - (double)mb1 > bound)) {
+        const int e = atomicAdd(a.list_count, 1);
+        a.list[e] = p * a.Nqmax + row;
+    }
+}
+
+// exact f64 rescan of ambiguous rows: one wave per row, grid-stride over the list
+__global__ __launch_bounds__(256) void featnn_rescan(const float *Q, const float *C, int Nqmax,
+                                                     int Ncmax, int D, const int32_t *ncnt,
+                                                     const int *list, const int *list_count,
+                                                     int32_t *nn) {
+    const int l = threadIdx.x & 63;
+    const int nwaves = gridDim.x * 4;
+    const int count = *list_count;
+    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < count; e += nwaves) {
+        const int code = list[e];
+        const int p = code / Nqmax, row = code - p * Nqmax;
+        const int nc = count_of(ncnt, p, Ncmax);
+        const float *q = Q + ((size_t)p * Nqmax + row) * D;
+        const float *cb = C + (size_t)p * Ncmax * D;
+        double best = __builtin_inf();
+        int bj = 0x7fffffff;
+        for (int j = l; j < nc; j += 64) {
+            const float *c = cb + (size_t)j * D;
+            double acc = 0.0;
+            for (int k = 0; k < D; ++k) {
+                const double df = (double)q[k] - (double)c[k];
+                acc = acc + df * df;
+            }
+            if (acc < best) { best = acc; bj = j; }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double ob = __shfl_xor(best, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+        }
+        if (l == 0) nn[(size_t)p * Nqmax + row] = (bj == 0x7fffffff) ? 0 : bj;
+    }
+}
+
+// mutual filter + ordered compaction (one block per pair)
+__global__ __launch_bounds__(1024) void corres_build(const int32_t *nn12, const int32_t *nn21,
+                                                     const int32_t *n_src, const int32_t *n_tgt,
+                                                     int Nmax, int Mmax, int mutual, int ransac_n,
+                                                     int *scratch, int32_t *corres,
+                                                     int32_t *n_corres) {
+    const int p = blockIdx.x;
+    const int n = count_of(n_src, p, Nmax);
+    const int m = count_of(n_tgt, p, Mmax);
+    const int32_t *a12 = nn12 + (size_t)p * Nmax;
+    const int32_t *a21 = nn21 + (size_t)p * Mmax;
+    int *f = scratch + (size_t)p * (Nmax + 1);
+    int32_t *co = corres + (size_t)p * Nmax * 2;
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const int j = a12[i];
+        f[i] = (mutual && j >= 0 && j < m && a21[j] == i) ? 1 : 0;
+    }
+    __syncthreads();
+    block_exclusive_scan_1024(f, f, n, false);
+    const int total = f[n];
+    const bool use_mutual = mutual && total >= 3 * ransac_n;
+    if (use_mutual) {
+        for (int i = threadIdx.x; i < n; i += 1024) {
+            const int pos = f[i];
+            if (f[i + 1] != pos) { co[2 * pos] = i; co[2 * pos + 1] = a12[i]; }
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += 1024) { co[2 * i] = i; co[2 * i + 1] = a12[i]; }
+    }
+    if (threadIdx.x == 0) n_corres[p] = use_mutual ? total : n;
+}
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+// direction-agnostic exact 1-NN of Q rows among C rows, both packed already
+static int screen_and_rescan(const float *Q, const float *C, const float *Qp, const float *Cp,
+                             const float *ccn, const float *qnrm, const unsigned *cgmax,
+                             const int32_t *nq, const int32_t *nc, int P, int Nqmax, int Ncmax,
+                             int D, int KCH, int32_t *nn, int *list, int *list_count,
+                             hipStream_t s) {
+    ScreenArgs a;
+    a.Qp = Qp; a.Cp = Cp; a.ccn = ccn; a.qnrm = qnrm; a.cgmax = cgmax; a.nq = nq; a.nc = nc;
+    a.Nqmax = Nqmax; a.Ncmax = Ncmax; a.ntq = cdiv(Nqmax, 32); a.ntc = cdiv(Ncmax, 32);
+    a.S2 = 8 * KCH; a.nn = nn; a.list = list; a.list_count = list_count;
+    PCR_HIP_CHECK(hipMemsetAsync(list_count, 0, sizeof(int), s));
+    const dim3 g(cdiv(a.ntq, 4), P);
+    prof_begin(s, kProfFeatScreen);
+    switch (KCH) {
+#define PCR_CASE(K) \
+    case K: hipLaunchKernelGGL(featnn_screen<K>, g, dim3(256), 0, s, a); break;
+        PCR_CASE(1) PCR_CASE(2) PCR_CASE(3) PCR_CASE(4) PCR_CASE(5) PCR_CASE(6) PCR_CASE(7) PCR_CASE(8)
+#undef PCR_CASE
+        default: set_error("feature dim too large"); return PCR_ERR_ARG;
+    }
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatScreen);
+    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, Q, C, Nqmax, Ncmax, D, nc, list,
+                       list_count, nn);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                       const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12, int32_t *nn21,
+                       hipStream_t s) {
+    const int KCH = cdiv(D, 16);
+    PCR_REQUIRE(D >= 1 && KCH <= 8, PCR_ERR_ARG, "feature_match: D=%d unsupported (1..128)", D);
+    const int S2 = 8 * KCH;
+    const int ntn = cdiv(Nmax, 32), ntm = cdiv(Mmax, 32);
+    const size_t fp_n = (size_t)P * ntn * S2 * 64, fp_m = (size_t)P * ntm * S2 * 64;
+    const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
+    const size_t bytes = 4 * (fp_n + fp_m + 2 * nn_n + 2 * nn_m + P + 2 + (size_t)P * (Nmax + Mmax));
+    char *ws = (char *)workspace(2, bytes + 256);
+    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
+    float *Fp = (float *)ws;
+    float *Gp = Fp + fp_n;
+    float *fcn = Gp + fp_m;
+    float *fnr = fcn + nn_n;
+    float *gcn = fnr + nn_n;
+    float *gnr = gcn + nn_m;
+    unsigned *gmax = (unsigned *)(gnr + nn_m);  // [0..P): max|g| ; [P..2P): max|f|
+    int *list_count = (int *)(gmax + 2 * P);
+    int *list = list_count + 2;
+    PCR_HIP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned) * 2 * P, s));
+    hipLaunchKernelGGL(feat_pack, dim3(ntn, P), dim3(64), 0, s, F, n_src, Nmax, D, S2, ntn, Fp, fcn,
+                       fnr, gmax + P);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(feat_pack, dim3(ntm, P), dim3(64), 0, s, G, n_tgt, Mmax, D, S2, ntm, Gp, gcn,
+                       gnr, gmax);
+    PCR_LAUNCH_CHECK();
+    int rc = screen_and_rescan(F, G, Fp, Gp, gcn, fnr, gmax, n_src, n_tgt, P, Nmax, Mmax, D, KCH,
+                               nn12, list, list_count, s);
+    if (rc != PCR_OK) return rc;
+    return screen_and_rescan(G, F, Gp, Fp, fcn, gnr, gmax + P, n_tgt, n_src, P, Mmax, Nmax, D, KCH,
+                             nn21, list, list_count + 1, s);
+}
+
+int corres_impl(const int32_t *nn12, const int32_t *nn21, const int32_t *n_src,
+                const int32_t *n_tgt, int P, int Nmax, int Mmax, int mutual, int ransac_n,
+                int32_t *corres, int32_t *n_corres, hipStream_t s) {
+    int *scratch = (int *)workspace(3, sizeof(int) * (size_t)P * (Nmax + 1));
+    PCR_REQUIRE(scratch, PCR_ERR_NOMEM, "corres: %s", pcr_last_error());
+    hipLaunchKernelGGL(corres_build, dim3(P), dim3(1024), 0, s, nn12, nn21, n_src, n_tgt, Nmax, Mmax,
+                       mutual, ransac_n, scratch, corres, n_corres);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+}  // namespace pcr
+
+extern "C" int pcr_feature_match(const float *src_feat, const float *tgt_feat, int32_t P,
+                                 int32_t Nmax, int32_t Mmax, int32_t D, const int32_t *n_src,
+                                 const int32_t *n_tgt, int32_t *nn12, int32_t *nn21,
+                                 pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(P >= 0 && Nmax >= 0 && Mmax >= 0, PCR_ERR_ARG, "feature_match: negative size");
+    if (P == 0 || Nmax == 0 || Mmax == 0) return PCR_OK;
+    PCR_REQUIRE(src_feat && tgt_feat && nn12 && nn21, PCR_ERR_ARG, "feature_match: null pointer");
+    PCR_REQUIRE(P <= 65535, PCR_ERR_ARG, "feature_match: P=%d > 65535", P);
+    return pcr::feature_match_impl(src_feat, tgt_feat, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21,
+                                   pcr::as_stream(stream));
+}
+
+extern "C" int pcr_correspondences(const int32_t *nn12, const int32_t *nn21, int32_t P,
+                                   int32_t Nmax, int32_t Mmax, const int32_t *n_src,
+                                   const int32_t *n_tgt, int32_t mutual_filter, int32_t ransac_n,
+                                   int32_t *corres, int32_t *n_corres, pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(P >= 0 && Nmax >= 0 && Mmax >= 0, PCR_ERR_ARG, "correspondences: negative size");
+    if (P == 0) return PCR_OK;
+    PCR_REQUIRE(nn12 && nn21 && corres && n_corres, PCR_ERR_ARG, "correspondences: null pointer");
+    return pcr::corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, Mmax, mutual_filter, ransac_n,
+                            corres, n_corres, pcr::as_stream(stream));
+}

@@ -1,0 +1,124 @@
+// Batched hashed-grid construction over target clouds (one launch per stage
+// for all P pairs).  See grid.h for the layout and query semantics.
+#include "pcr_internal.h"
+#include "grid.h"
+#include "scan.h"
+
+namespace pcr {
+namespace {
+
+struct BuildArgs {
+    const float *tgt;
+    const int32_t *n_tgt;
+    int Mmax, S;
+    double cell;
+    int *cnt;      // P*S
+    int *start;    // P*(S+1)
+    float4 *pts;   // P*Mmax
+};
+
+__device__ __forceinline__ int count_of(const int32_t *n, int p, int Mmax) {
+    return n ? min(max(n[p], 0), Mmax) : Mmax;
+}
+
+__global__ void grid_count(BuildArgs a) {
+    const int p = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count_of(a.n_tgt, p, a.Mmax)) return;
+    const float *q = a.tgt + ((size_t)p * a.Mmax + j) * 3;
+    const unsigned h = cell_hash(cell_coord((double)q[0], a.cell), cell_coord((double)q[1], a.cell),
+                                 cell_coord((double)q[2], a.cell), a.S);
+    atomicAdd(a.cnt + (size_t)p * a.S + h, 1);
+}
+
+__global__ __launch_bounds__(1024) void grid_scan(BuildArgs a) {
+    const int p = blockIdx.x;
+    block_exclusive_scan_1024(a.cnt + (size_t)p * a.S, a.start + (size_t)p * (a.S + 1), a.S, true);
+}
+
+__global__ void grid_scatter(BuildArgs a) {
+    const int p = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count_of(a.n_tgt, p, a.Mmax)) return;
+    const float *q = a.tgt + ((size_t)p * a.Mmax + j) * 3;
+    const unsigned h = cell_hash(cell_coord((double)q[0], a.cell), cell_coord((double)q[1], a.cell),
+                                 cell_coord((double)q[2], a.cell), a.S);
+    const int pos = a.start[(size_t)p * (a.S + 1) + h] + atomicAdd(a.cnt + (size_t)p * a.S + h, 1);
+    a.pts[(size_t)p * a.Mmax + pos] = make_float4(q[0], q[1], q[2], __int_as_float(j));
+}
+
+}  // namespace
+
+int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r, hipStream_t s,
+                int ws_slot, GridBatch &out) {
+    int S = 256;
+    while (S < Mmax) S <<= 1;
+    const size_t cnt_b = sizeof(int) * (size_t)P * S;
+    const size_t start_b = sizeof(int) * (size_t)P * (S + 1);
+    const size_t pts_b = sizeof(float4) * (size_t)P * (Mmax > 0 ? Mmax : 1);
+    char *ws = (char *)workspace(ws_slot, cnt_b + start_b + pts_b + 64);
+    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "grid workspace: %s", pcr_last_error());
+    BuildArgs a;
+    a.tgt = tgt;
+    a.n_tgt = n_tgt;
+    a.Mmax = Mmax;
+    a.S = S;
+    a.cell = 2.01 * r;
+    a.cnt = (int *)ws;
+    a.start = (int *)(ws + cnt_b);
+    size_t off = (cnt_b + start_b + 15) & ~size_t(15);
+    a.pts = (float4 *)(ws + off);
+    PCR_HIP_CHECK(hipMemsetAsync(a.cnt, 0, cnt_b, s));
+    const dim3 g((Mmax + 255) / 256 > 0 ? (Mmax + 255) / 256 : 1, P);
+    hipLaunchKernelGGL(grid_count, g, dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(grid_scan, dim3(P), dim3(1024), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(grid_scatter, g, dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    out.pts = a.pts;
+    out.start = a.start;
+    out.S = S;
+    out.mstride = Mmax;
+    out.cell = a.cell;
+    return PCR_OK;
+}
+
+namespace {
+__global__ void radius_nn_kernel(GridBatch g, const double *q, const int32_t *n_q, int Qmax,
+                                 double r, double thr, int32_t *idx, double *d2o) {
+    const int p = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Qmax) return;
+    const int nq = n_q ? min(max(n_q[p], 0), Qmax) : Qmax;
+    int j = -1;
+    double d2 = __builtin_inf();
+    if (i < nq) {
+        const double *x = q + ((size_t)p * Qmax + i) * 3;
+        j = grid_query(g.view(p), r, thr, x[0], x[1], x[2], d2);
+    }
+    idx[(size_t)p * Qmax + i] = j;
+    if (d2o) d2o[(size_t)p * Qmax + i] = d2;
+}
+}  // namespace
+
+}  // namespace pcr
+
+extern "C" int pcr_radius_nn(const float *tgt_xyz, int32_t P, int32_t Mmax, const int32_t *n_tgt,
+                             const double *queries, int32_t Qmax, const int32_t *n_q, double r,
+                             int32_t *idx, double *d2, pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(P >= 0 && Mmax >= 0 && Qmax >= 0, PCR_ERR_ARG, "radius_nn: negative size");
+    if (P == 0 || Qmax == 0) return PCR_OK;
+    PCR_REQUIRE(tgt_xyz && queries && idx, PCR_ERR_ARG, "radius_nn: null pointer");
+    PCR_REQUIRE(r > 0.0, PCR_ERR_ARG, "radius_nn: r must be > 0");
+    PCR_REQUIRE(P <= 65535, PCR_ERR_ARG, "radius_nn: P=%d > 65535", P);
+    hipStream_t s = pcr::as_stream(stream);
+    pcr::GridBatch g;
+    int rc = pcr::build_grids(tgt_xyz, n_tgt, P, Mmax, r, s, 10, g);
+    if (rc != PCR_OK) return rc;
+    hipLaunchKernelGGL(pcr::radius_nn_kernel, dim3((Qmax + 255) / 256, P), dim3(256), 0, s, g,
+                       queries, n_q, Qmax, r, pcr::radius_thr(r), idx, d2);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}

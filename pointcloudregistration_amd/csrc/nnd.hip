@@ -363,8 +363,10 @@ extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, 
         PCR_HIP_CHECK(hipMemsetAsync(keys, 0xff,
                                      sizeof(unsigned long long) * ((size_t)b * n + (size_t)b * m), s));
     }
+    pcr::prof_begin(s, pcr::kProfNndFwd);
     hipLaunchKernelGGL(nnd_fwd_kernel<Q>, dim3(qtiles, ys, 2 * b), dim3(kThreads), 0, s, a);
     PCR_LAUNCH_CHECK();
+    pcr::prof_end(s, pcr::kProfNndFwd);
     if (a.split) {
         hipLaunchKernelGGL(nnd_finalize_kernel, dim3(cdiv(nmax, kThreads), 1, 2 * b),
                            dim3(kThreads), 0, s, a);

@@ -19,6 +19,12 @@ void *workspace(int slot, size_t bytes);
 
 inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)
+enum ProfId { kProfFeatScreen = 0, kProfNndFwd = 1, kProfRansacValidate = 2, kProfIcp = 3,
+              kProfRansacHyp = 4, kProfSlots = 8 };
+void prof_begin(hipStream_t s, int id);
+void prof_end(hipStream_t s, int id);
+
 constexpr int kWave = 64;
 constexpr int kCUs = 256;
 

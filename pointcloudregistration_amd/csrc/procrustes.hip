@@ -1,0 +1,89 @@
+// a9: batched weighted 3x3 Procrustes / Kabsch, the kernel behind the drop-ins
+// for ROPNet weighted_icp (ROPNet/src/models/model_utils.py:105-139) and NDP
+// rigid_fit (c2p-net/deformationpyramid/model/geometry.py:8-34).
+// Contract: oracle_procrustes (pcr_oracle.c):
+//   W = sum(w') + eps, w' = |w| (rigid_fit) or w (weighted_icp)
+//   mu_s = sum src*(w/W), mu_t = sum tgt*(w/W)
+//   S_ab = sum ((src_a - mu_s_a)*(w/W)) * (tgt_b - mu_t_b)
+//   R = Horn(S) (= SVD + det fix optimum), t = mu_t - R mu_s
+// All sums use the deterministic 256-lane order; one 256-thread block per item.
+#include "pcr_internal.h"
+#include "geom.h"
+
+namespace pcr {
+namespace {
+
+__device__ inline void tree256x(double (*red)[9], int nv) {
+    for (int s = 128; s >= 1; s >>= 1) {
+        if ((int)threadIdx.x < s)
+            for (int v = 0; v < nv; ++v) red[threadIdx.x][v] = red[threadIdx.x][v] + red[threadIdx.x + s][v];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void procrustes_kernel(const float *src, const float *tgt,
+                                                         const float *w, int N, int absw, double eps,
+                                                         double *T) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const float *S = src + (size_t)b * N * 3;
+    const float *G = tgt + (size_t)b * N * 3;
+    const float *Wt = w + (size_t)b * N;
+    __shared__ double red[256][9];
+    double v = 0.0;
+    for (int i = t; i < N; i += 256) {
+        const double wi = (double)Wt[i];
+        v = v + (absw ? __builtin_fabs(wi) : wi);
+    }
+    red[t][0] = v;
+    __syncthreads();
+    tree256x(red, 1);
+    const double W = red[0][0] + eps;
+    __syncthreads();
+    double m[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = t; i < N; i += 256) {
+        const double wn = (double)Wt[i] / W;
+        for (int c = 0; c < 3; ++c) {
+            m[c] = m[c] + (double)S[3 * i + c] * wn;
+            m[3 + c] = m[3 + c] + (double)G[3 * i + c] * wn;
+        }
+    }
+    for (int k = 0; k < 6; ++k) red[t][k] = m[k];
+    __syncthreads();
+    tree256x(red, 6);
+    const double ms[3] = {red[0][0], red[0][1], red[0][2]};
+    const double mt[3] = {red[0][3], red[0][4], red[0][5]};
+    __syncthreads();
+    double q[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = t; i < N; i += 256) {
+        const double wn = (double)Wt[i] / W;
+        for (int x = 0; x < 3; ++x) {
+            const double sx = ((double)S[3 * i + x] - ms[x]) * wn;
+            for (int y = 0; y < 3; ++y) q[3 * x + y] = q[3 * x + y] + sx * ((double)G[3 * i + y] - mt[y]);
+        }
+    }
+    for (int k = 0; k < 9; ++k) red[t][k] = q[k];
+    __syncthreads();
+    tree256x(red, 9);
+    if (t == 0) {
+        double Sm[9], R[9];
+        for (int k = 0; k < 9; ++k) Sm[k] = red[0][k];
+        horn_rotation(Sm, R);
+        compose_rt(R, ms, mt, T + (size_t)b * 12);
+    }
+}
+
+}  // namespace
+}  // namespace pcr
+
+extern "C" int pcr_procrustes_batch(const float *src, const float *tgt, const float *weights,
+                                    int32_t B, int32_t N, int32_t abs_weights, double eps,
+                                    double *T, pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(B >= 0 && N >= 0, PCR_ERR_ARG, "procrustes: negative size");
+    if (B == 0) return PCR_OK;
+    PCR_REQUIRE(src && tgt && weights && T, PCR_ERR_ARG, "procrustes: null pointer");
+    hipLaunchKernelGGL(pcr::procrustes_kernel, dim3(B), dim3(256), 0, pcr::as_stream(stream), src,
+                       tgt, weights, N, abs_weights, eps, T);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}

@@ -56,7 +56,75 @@ void *workspace(int slot, size_t bytes) {
     return p;
 }
 
+// ---- optional per-kernel HIP-event timing (pcr_profile_*) -----------------
+namespace {
+struct ProfRec {
+    hipEvent_t b, e;
+    int id;
+};
+std::mutex g_pmu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_pending;
+std::vector<hipEvent_t> g_free;
+double g_total_ms[kProfSlots] = {0};
+long g_count[kProfSlots] = {0};
+
+hipEvent_t take_event() {
+    if (!g_free.empty()) {
+        hipEvent_t e = g_free.back();
+        g_free.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+thread_local hipEvent_t t_begin[kProfSlots];
+}  // namespace
+
+void prof_begin(hipStream_t s, int id) {
+    if (!g_prof_on || id < 0 || id >= kProfSlots) return;
+    std::lock_guard<std::mutex> lk(g_pmu);
+    hipEvent_t e = take_event();
+    if (e && hipEventRecord(e, s) == hipSuccess) t_begin[id] = e;
+    else t_begin[id] = nullptr;
+}
+
+void prof_end(hipStream_t s, int id) {
+    if (!g_prof_on || id < 0 || id >= kProfSlots || !t_begin[id]) return;
+    std::lock_guard<std::mutex> lk(g_pmu);
+    hipEvent_t e = take_event();
+    if (e && hipEventRecord(e, s) == hipSuccess) g_pending.push_back({t_begin[id], e, id});
+    t_begin[id] = nullptr;
+}
+
 }  // namespace pcr
+
+extern "C" void pcr_profile_enable(int32_t on) {
+    std::lock_guard<std::mutex> lk(pcr::g_pmu);
+    pcr::g_prof_on = on != 0;
+}
+
+extern "C" int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset) {
+    if (id < 0 || id >= pcr::kProfSlots) return PCR_ERR_ARG;
+    std::lock_guard<std::mutex> lk(pcr::g_pmu);
+    for (auto &r : pcr::g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.e) != hipSuccess || hipEventElapsedTime(&ms, r.b, r.e) != hipSuccess) {
+            pcr::set_error("profile: event query failed");
+            return PCR_ERR_HIP;
+        }
+        pcr::g_total_ms[r.id] += ms;
+        pcr::g_count[r.id] += 1;
+        pcr::g_free.push_back(r.b);
+        pcr::g_free.push_back(r.e);
+    }
+    pcr::g_pending.clear();
+    if (total_ms) *total_ms = pcr::g_total_ms[id];
+    if (count) *count = pcr::g_count[id];
+    if (reset) { pcr::g_total_ms[id] = 0.0; pcr::g_count[id] = 0; }
+    return PCR_OK;
+}
 
 extern "C" const char *pcr_last_error(void) { return pcr::g_err; }
 extern "C" int pcr_version(void) { return 1; }
