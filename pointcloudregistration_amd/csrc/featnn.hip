@@ -22,6 +22,7 @@
 //  The screen is the MFMA-bound kernel (4.3 GFLOP per 8192^2 x 32 direction).
 #include "pcr_internal.h"
 #include "scan.h"
+#include <stdlib.h>
 
 namespace pcr {
 namespace {
@@ -218,9 +219,198 @@ __global__ __launch_bounds__(1024) void corres_build(const int32_t *nn12, const 
     if (threadIdx.x == 0) n_corres[p] = use_mutual ? total : n;
 }
 
+
+// ---------------------------------------------------------------------------
+// v2: ONE pass for both directions.  t_ij = -2 f_i.g_j (exact fmaf chain from
+// C = 0); row value t + |g_j|^2, column value t + |f_i|^2 (one more rounding:
+// the (K+2) factor of the bound covers it).  Workgroup = 8 waves x 32 rows =
+// 256 rows; every wave sweeps all candidate tiles in groups of G tiles (G
+// independent accumulator chains).  Row top-2 stays in registers (as v1);
+// column top-2 over the wave's 32 rows is merged across the 8 waves through
+// LDS once per group and written as one partial per 256-row block; a final
+// kernel merges the partials and certifies each column.
+// ---------------------------------------------------------------------------
+struct DualArgs {
+    const float *Fp, *Gp;         // packed rows (src) / columns (tgt)
+    const float *fcn, *gcn;       // |f|^2, |g|^2 (+inf padding), (P, tiles*32)
+    const float *fnr, *gnr;       // |f|, |g|
+    const unsigned *fmax, *gmax;  // per-pair max norms (float bits)
+    const int32_t *n_src, *n_tgt;
+    int Nmax, Mmax, ntn, ntm, nrb;
+    int32_t *nn12;
+    int *list12, *count12;
+    float *cp1, *cp2;             // (P, nrb, ntm*32) column partials
+    int *cpi;
+};
+
+__device__ __forceinline__ void top2_merge(float &b1, int &i1, float &b2, float o1, int oi, float o2) {
+    const bool take = (o1 < b1) || (o1 == b1 && oi < i1);
+    const float n2 = fminf(fmaxf(b1, o1), fminf(b2, o2));
+    b1 = take ? o1 : b1;
+    i1 = take ? oi : i1;
+    b2 = n2;
+}
+
+template <int KCH, int G>
+__global__ __launch_bounds__(512) void featnn_dual(DualArgs a) {
+    constexpr int S2 = 8 * KCH;
+    __shared__ float l_c1[2][G][8][32], l_c2[2][G][8][32];
+    __shared__ int l_ci[2][G][8][32];
+    const int p = blockIdx.y, rb = blockIdx.x;
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    const int qt = rb * 8 + wid;
+    const bool active = qt * 32 < n;  // wave-uniform; inactive waves still hit barriers
+    const int ntc = (m + 31) >> 5;
+
+    float A[S2];
+    const float *qp = a.Fp + (((size_t)p * a.ntn + (active ? qt : 0)) * S2) * 64 + l;
+#pragma unroll
+    for (int s = 0; s < S2; ++s) A[s] = active ? -2.0f * qp[(size_t)s * 64] : 0.0f;
+    float rn[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        rn[r] = active ? a.fcn[(size_t)p * a.ntn * 32 + row] : __builtin_inff();
+    }
+    float b1[16], b2[16];
+    int i1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); i1[r] = 0; }
+
+    const float *gbase = a.Gp + ((size_t)p * a.ntm * S2) * 64 + l;
+    const float *gcn = a.gcn + (size_t)p * a.ntm * 32;
+    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
+    int buf = 0;
+    for (int ct0 = 0; ct0 < ntc; ct0 += G, buf ^= 1) {
+        float B[G][S2];
+        f32x16 acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int ct = min(ct0 + g, ntc - 1);
+            const float *cp = gbase + (size_t)ct * S2 * 64;
+#pragma unroll
+            for (int s = 0; s < S2; ++s) B[g][s] = cp[(size_t)s * 64];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+        }
+#pragma unroll
+        for (int s = 0; s < S2; ++s)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], B[g][s], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int ct = ct0 + g;
+            const bool tile_ok = ct < ntc;  // uniform
+            const int j = ct * 32 + (l & 31);
+            const float gn = tile_ok ? gcn[j] : __builtin_inff();
+            float c1 = __builtin_inff(), c2 = __builtin_inff();
+            int ci = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float t = acc[g][r];
+                const float v = t + gn;  // row direction
+                b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], v);
+                const bool c = v < b1[r];
+                b1[r] = c ? v : b1[r];
+                i1[r] = c ? j : i1[r];
+                const float w = t + rn[r];  // column direction (rows increase with r)
+                c2 = __builtin_amdgcn_fmed3f(c1, c2, w);
+                const bool cc = w < c1;
+                c1 = cc ? w : c1;
+                ci = cc ? (qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) : ci;
+            }
+            const float o1 = __shfl_xor(c1, 32, 64), o2 = __shfl_xor(c2, 32, 64);
+            const int oi = __shfl_xor(ci, 32, 64);
+            top2_merge(c1, ci, c2, o1, oi, o2);
+            if (h == 0) {
+                l_c1[buf][g][wid][l] = c1;
+                l_c2[buf][g][wid][l] = c2;
+                l_ci[buf][g][wid][l] = ci;
+            }
+        }
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < G * 32) {
+            const int g = t >> 5, col = t & 31, ct = ct0 + g;
+            if (ct < ntc) {
+                float m1 = l_c1[buf][g][0][col], m2 = l_c2[buf][g][0][col];
+                int mi = l_ci[buf][g][0][col];
+#pragma unroll
+                for (int w = 1; w < 8; ++w)
+                    top2_merge(m1, mi, m2, l_c1[buf][g][w][col], l_ci[buf][g][w][col],
+                               l_c2[buf][g][w][col]);
+                const size_t o = cpoff + (size_t)ct * 32 + col;
+                a.cp1[o] = m1;
+                a.cp2[o] = m2;
+                a.cpi[o] = mi;
+            }
+        }
+    }
+    if (!active) return;
+    // rows: merge the 32 lanes of each half, certify, write
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float ob1 = __shfl_xor(b1[r], o, 64);
+            const float ob2 = __shfl_xor(b2[r], o, 64);
+            const int oi1 = __shfl_xor(i1[r], o, 64);
+            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+        }
+    }
+    const int lr = l & 31;
+    if (lr >= 16) return;
+    float mb1 = 0.f, mb2 = 0.f;
+    int mi1 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+    if (row >= n) return;
+    a.nn12[(size_t)p * a.Nmax + row] = mi1;
+    const double Gm = (double)__uint_as_float(a.gmax[p]);
+    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
+    const double K = 2.0 * S2;
+    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (qn + Gm) * (qn + Gm);
+    if (!((double)mb2 - (double)mb1 > bound)) a.list12[atomicAdd(a.count12, 1)] = p * a.Nmax + row;
+}
+
+// merge the per-256-row-block column partials in block order; certify columns
+__global__ void featnn_colmerge(DualArgs a, int32_t *nn21, int *list21, int *count21, int S2) {
+    const int p = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = count_of(a.n_tgt, p, a.Mmax);
+    if (j >= m) return;
+    const int n = count_of(a.n_src, p, a.Nmax);
+    const int nrb_used = (((n + 31) >> 5) + 7) >> 3;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = 0;
+    for (int rb = 0; rb < nrb_used; ++rb) {
+        const size_t o = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32 + j;
+        top2_merge(b1, i1, b2, a.cp1[o], a.cpi[o], a.cp2[o]);
+    }
+    nn21[(size_t)p * a.Mmax + j] = i1;
+    const double F = (double)__uint_as_float(a.fmax[p]);
+    const double gn = (double)a.gnr[(size_t)p * a.ntm * 32 + j];
+    const double K = 2.0 * S2;
+    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (gn + F) * (gn + F);
+    if (!((double)b2 - (double)b1 > bound)) list21[atomicAdd(count21, 1)] = p * a.Mmax + j;
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
+
+static bool featnn_twopass() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PCR_FEATNN_TWOPASS");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
 
 // direction-agnostic exact 1-NN of Q rows among C rows, both packed already
 static int screen_and_rescan(const float *Q, const float *C, const float *Qp, const float *Cp,
@@ -259,7 +449,7 @@ int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax
     const int ntn = cdiv(Nmax, 32), ntm = cdiv(Mmax, 32);
     const size_t fp_n = (size_t)P * ntn * S2 * 64, fp_m = (size_t)P * ntm * S2 * 64;
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
-    const size_t bytes = 4 * (fp_n + fp_m + 2 * nn_n + 2 * nn_m + P + 2 + (size_t)P * (Nmax + Mmax));
+    const size_t bytes = 4 * (fp_n + fp_m + 2 * nn_n + 2 * nn_m + 2 * (size_t)P + 2 + (size_t)P * (Nmax + Mmax));
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     float *Fp = (float *)ws;
@@ -278,11 +468,50 @@ int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax
     hipLaunchKernelGGL(feat_pack, dim3(ntm, P), dim3(64), 0, s, G, n_tgt, Mmax, D, S2, ntm, Gp, gcn,
                        gnr, gmax);
     PCR_LAUNCH_CHECK();
-    int rc = screen_and_rescan(F, G, Fp, Gp, gcn, fnr, gmax, n_src, n_tgt, P, Nmax, Mmax, D, KCH,
-                               nn12, list, list_count, s);
-    if (rc != PCR_OK) return rc;
-    return screen_and_rescan(G, F, Gp, Fp, fcn, gnr, gmax + P, n_tgt, n_src, P, Mmax, Nmax, D, KCH,
-                             nn21, list, list_count + 1, s);
+    if (featnn_twopass()) {
+        int rc = screen_and_rescan(F, G, Fp, Gp, gcn, fnr, gmax, n_src, n_tgt, P, Nmax, Mmax, D,
+                                   KCH, nn12, list, list_count, s);
+        if (rc != PCR_OK) return rc;
+        return screen_and_rescan(G, F, Gp, Fp, fcn, gnr, gmax + P, n_tgt, n_src, P, Mmax, Nmax, D,
+                                 KCH, nn21, list, list_count + 1, s);
+    }
+    // one pass, both directions
+    DualArgs d;
+    d.Fp = Fp; d.Gp = Gp; d.fcn = fcn; d.gcn = gcn; d.fnr = fnr; d.gnr = gnr;
+    d.fmax = gmax + P; d.gmax = gmax; d.n_src = n_src; d.n_tgt = n_tgt;
+    d.Nmax = Nmax; d.Mmax = Mmax; d.ntn = ntn; d.ntm = ntm; d.nrb = cdiv(ntn, 8);
+    d.nn12 = nn12;
+    int *list21 = list + (size_t)P * Nmax;
+    d.list12 = list; d.count12 = list_count;
+    const size_t cpn = (size_t)P * d.nrb * ntm * 32;
+    char *cw = (char *)workspace(11, cpn * 12 + 64);
+    PCR_REQUIRE(cw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
+    d.cp1 = (float *)cw;
+    d.cp2 = d.cp1 + cpn;
+    d.cpi = (int *)(d.cp2 + cpn);
+    PCR_HIP_CHECK(hipMemsetAsync(list_count, 0, 2 * sizeof(int), s));
+    const dim3 g(d.nrb, P);
+    prof_begin(s, kProfFeatScreen);
+    switch (KCH) {
+#define PCR_DCASE(K, GG) \
+    case K: hipLaunchKernelGGL((featnn_dual<K, GG>), g, dim3(512), 0, s, d); break;
+        PCR_DCASE(1, 4) PCR_DCASE(2, 3) PCR_DCASE(3, 2) PCR_DCASE(4, 2)
+        PCR_DCASE(5, 1) PCR_DCASE(6, 1) PCR_DCASE(7, 1) PCR_DCASE(8, 1)
+#undef PCR_DCASE
+        default: set_error("feature dim too large"); return PCR_ERR_ARG;
+    }
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatScreen);
+    hipLaunchKernelGGL(featnn_colmerge, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, list21,
+                       list_count + 1, S2);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, F, G, Nmax, Mmax, D, n_tgt, list,
+                       list_count, nn12);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, G, F, Mmax, Nmax, D, n_src,
+                       list21, list_count + 1, nn21);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
 }
 
 int corres_impl(const int32_t *nn12, const int32_t *nn21, const int32_t *n_src,
