@@ -95,50 +95,67 @@ __device__ inline void horn_rotation(const double S[9], double R[9]) {
     A[3][3] = (Szz - Sxx) - Syy;
     A[1][0] = A[0][1]; A[2][0] = A[0][2]; A[3][0] = A[0][3];
     A[2][1] = A[1][2]; A[3][1] = A[1][3]; A[3][2] = A[2][3];
+#pragma unroll
     for (int a = 0; a < 4; ++a)
+#pragma unroll
         for (int b = 0; b < 4; ++b) V[a][b] = (a == b) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 16; ++sweep) {
         double off = 0.0;
+#pragma unroll
         for (int p = 0; p < 3; ++p)
+#pragma unroll
             for (int r = p + 1; r < 4; ++r) off = off + A[p][r] * A[p][r];
         if (off == 0.0) break;
+#pragma unroll
         for (int p = 0; p < 3; ++p) {
+#pragma unroll
             for (int r = p + 1; r < 4; ++r) {
                 const double apr = A[p][r];
-                if (apr == 0.0) continue;
-                const double theta = (A[r][r] - A[p][p]) / (2.0 * apr);
-                double t = 1.0 / (__builtin_fabs(theta) + __builtin_sqrt(theta * theta + 1.0));
-                if (theta < 0.0) t = -t;
-                const double c = 1.0 / __builtin_sqrt(t * t + 1.0);
-                const double s = t * c;
-                A[p][p] = A[p][p] - t * apr;
-                A[r][r] = A[r][r] + t * apr;
-                A[p][r] = 0.0;
-                A[r][p] = 0.0;
-                for (int k = 0; k < 4; ++k) {
-                    if (k == p || k == r) continue;
-                    const double akp = A[k][p], akr = A[k][r];
-                    A[k][p] = c * akp - s * akr;
-                    A[p][k] = A[k][p];
-                    A[k][r] = s * akp + c * akr;
-                    A[r][k] = A[k][r];
-                }
-                for (int k = 0; k < 4; ++k) {
-                    const double vkp = V[k][p], vkr = V[k][r];
-                    V[k][p] = c * vkp - s * vkr;
-                    V[k][r] = s * vkp + c * vkr;
+                if (apr != 0.0) {
+                    const double theta = (A[r][r] - A[p][p]) / (2.0 * apr);
+                    double t = 1.0 / (__builtin_fabs(theta) + __builtin_sqrt(theta * theta + 1.0));
+                    if (theta < 0.0) t = -t;
+                    const double c = 1.0 / __builtin_sqrt(t * t + 1.0);
+                    const double s = t * c;
+                    A[p][p] = A[p][p] - t * apr;
+                    A[r][r] = A[r][r] + t * apr;
+                    A[p][r] = 0.0;
+                    A[r][p] = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (k == p || k == r) continue;
+                        const double akp = A[k][p], akr = A[k][r];
+                        A[k][p] = c * akp - s * akr;
+                        A[p][k] = A[k][p];
+                        A[k][r] = s * akp + c * akr;
+                        A[r][k] = A[k][r];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const double vkp = V[k][p], vkr = V[k][r];
+                        V[k][p] = c * vkp - s * vkr;
+                        V[k][r] = s * vkp + c * vkr;
+                    }
                 }
             }
         }
     }
-    int best = 0;
-    for (int k = 1; k < 4; ++k)
-        if (A[k][k] > A[best][best]) best = k;
-    double q[4];
+    // argmax of the diagonal, first index on ties (static register selects)
+    double bd = A[0][0];
+    double q[4] = {V[0][0], V[1][0], V[2][0], V[3][0]};
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const bool t = A[k][k] > bd;
+        bd = t ? A[k][k] : bd;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = t ? V[e][k] : q[e];
+    }
     double nrm = 0.0;
-    for (int k = 0; k < 4; ++k) nrm = nrm + V[k][best] * V[k][best];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nrm = nrm + q[k] * q[k];
     nrm = __builtin_sqrt(nrm);
-    for (int k = 0; k < 4; ++k) q[k] = V[k][best] / nrm;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = q[k] / nrm;
     const double w = q[0], x = q[1], y = q[2], z = q[3];
     R[0] = ((w * w + x * x) - y * y) - z * z;
     R[1] = 2.0 * (x * y - w * z);

@@ -14,7 +14,8 @@ struct BuildArgs {
     double cell;
     int *cnt;      // P*S
     int *start;    // P*(S+1)
-    float4 *pts;   // P*Mmax
+    float *x, *y, *z;
+    uint32_t *idx; // P*Mmax each
 };
 
 __device__ __forceinline__ int count_of(const int32_t *n, int p, int Mmax) {
@@ -44,7 +45,11 @@ __global__ void grid_scatter(BuildArgs a) {
     const unsigned h = cell_hash(cell_coord((double)q[0], a.cell), cell_coord((double)q[1], a.cell),
                                  cell_coord((double)q[2], a.cell), a.S);
     const int pos = a.start[(size_t)p * (a.S + 1) + h] + atomicAdd(a.cnt + (size_t)p * a.S + h, 1);
-    a.pts[(size_t)p * a.Mmax + pos] = make_float4(q[0], q[1], q[2], __int_as_float(j));
+    const size_t o = (size_t)p * a.Mmax + pos;
+    a.x[o] = q[0];
+    a.y[o] = q[1];
+    a.z[o] = q[2];
+    a.idx[o] = (uint32_t)j;
 }
 
 }  // namespace
@@ -55,7 +60,7 @@ int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double 
     while (S < Mmax) S <<= 1;
     const size_t cnt_b = sizeof(int) * (size_t)P * S;
     const size_t start_b = sizeof(int) * (size_t)P * (S + 1);
-    const size_t pts_b = sizeof(float4) * (size_t)P * (Mmax > 0 ? Mmax : 1);
+    const size_t pts_b = 16 * (size_t)P * (Mmax > 0 ? Mmax : 1);
     char *ws = (char *)workspace(ws_slot, cnt_b + start_b + pts_b + 64);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "grid workspace: %s", pcr_last_error());
     BuildArgs a;
@@ -67,7 +72,11 @@ int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double 
     a.cnt = (int *)ws;
     a.start = (int *)(ws + cnt_b);
     size_t off = (cnt_b + start_b + 15) & ~size_t(15);
-    a.pts = (float4 *)(ws + off);
+    const size_t pm = (size_t)P * (Mmax > 0 ? Mmax : 1);
+    a.x = (float *)(ws + off);
+    a.y = a.x + pm;
+    a.z = a.y + pm;
+    a.idx = (uint32_t *)(a.z + pm);
     PCR_HIP_CHECK(hipMemsetAsync(a.cnt, 0, cnt_b, s));
     const dim3 g((Mmax + 255) / 256 > 0 ? (Mmax + 255) / 256 : 1, P);
     hipLaunchKernelGGL(grid_count, g, dim3(256), 0, s, a);
@@ -76,8 +85,11 @@ int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double 
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(grid_scatter, g, dim3(256), 0, s, a);
     PCR_LAUNCH_CHECK();
-    out.pts = a.pts;
-    out.start = a.start;
+    out.x = a.x;
+    out.y = a.y;
+    out.z = a.z;
+    out.idx = a.idx;
+    out.start = (uint32_t *)a.start;
     out.S = S;
     out.mstride = Mmax;
     out.cell = a.cell;

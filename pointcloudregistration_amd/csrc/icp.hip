@@ -43,16 +43,24 @@ __device__ inline void tree256(double (*red)[9], int nv) {
     }
 }
 
+struct IShared {  // LDS header; the grid copy (if any) follows
+    double red[256][9];
+    double T[16], U[12];
+    unsigned long long s_acc[16];
+    int s_cnt[16];
+    double s_fit, s_rmse;
+    int s_count;
+};
+
+template <bool kLds>
 __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    IShared &sh = *reinterpret_cast<IShared *>(dsm);
+    double (*red)[9] = sh.red;
+    double *T = sh.T, *U = sh.U;
     const int p = blockIdx.x;
     const int n = cnt_of(a.n_src, p, a.Nmax);
     const int m = cnt_of(a.n_tgt, p, a.Mmax);
-    __shared__ double T[16], U[12];
-    __shared__ double red[256][9];
-    __shared__ unsigned long long s_acc[16];
-    __shared__ int s_cnt[16];
-    __shared__ double s_fit, s_rmse;
-    __shared__ int s_count, s_stop;
     const int tid = threadIdx.x;
     double *P3 = a.P3 + (size_t)p * a.Nmax * 3;
     int *cj = a.cj + (size_t)p * a.Nmax;
@@ -72,15 +80,22 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
         }
         P3[3 * i] = x; P3[3 * i + 1] = y; P3[3 * i + 2] = z;
     }
+    GridT<uint16_t> gl{};
+    GridView gg{};
+    if (valid) {
+        if constexpr (kLds) gl = grid_to_lds(a.grid, p, m, dsm + ((sizeof(IShared) + 15) & ~size_t(15)));
+        else gg = a.grid.view(p);
+    }
     __syncthreads();
-    const GridView g = a.grid.view(p);
     const double scale = fx_scale(a.thr);
     auto evaluate = [&]() {
         unsigned long long acc = 0;
         int cnt = 0;
         for (int i = tid; i < n; i += 1024) {
             double d2;
-            const int j = grid_query(g, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
+            int j;
+            if constexpr (kLds) j = grid_query(gl, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
+            else j = grid_query(gg, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
             cj[i] = j;
             if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
         }
@@ -89,19 +104,19 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
             acc += __shfl_xor(acc, o, 64);
             cnt += __shfl_xor(cnt, o, 64);
         }
-        if ((tid & 63) == 0) { s_acc[tid >> 6] = acc; s_cnt[tid >> 6] = cnt; }
+        if ((tid & 63) == 0) { sh.s_acc[tid >> 6] = acc; sh.s_cnt[tid >> 6] = cnt; }
         __syncthreads();
         if (tid == 0) {
             unsigned long long A = 0;
             int C = 0;
-            for (int w = 0; w < 16; ++w) { A += s_acc[w]; C += s_cnt[w]; }
-            s_count = C;
+            for (int w = 0; w < 16; ++w) { A += sh.s_acc[w]; C += sh.s_cnt[w]; }
+            sh.s_count = C;
             if (C > 0) {
-                s_fit = (double)C / (double)n;
-                s_rmse = __builtin_sqrt(((double)A / scale) / (double)C);
+                sh.s_fit = (double)C / (double)n;
+                sh.s_rmse = __builtin_sqrt(((double)A / scale) / (double)C);
             } else {
-                s_fit = 0.0;
-                s_rmse = 0.0;
+                sh.s_fit = 0.0;
+                sh.s_rmse = 0.0;
             }
         }
         __syncthreads();
@@ -110,7 +125,7 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
     if (valid) {
         evaluate();
         for (it = 0; it < a.max_iter;) {
-            if (s_count == 0) break;
+            if (sh.s_count == 0) break;
             // --- Umeyama over correspondences: means
             if (tid < 256) {
                 double v[6] = {0, 0, 0, 0, 0, 0};
@@ -128,7 +143,7 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
             }
             __syncthreads();
             tree256(red, 6);
-            const double inv = 1.0 / (double)s_count;
+            const double inv = 1.0 / (double)sh.s_count;
             const double ms0 = red[0][0] * inv, ms1 = red[0][1] * inv, ms2 = red[0][2] * inv;
             const double mt0 = red[0][3] * inv, mt1 = red[0][4] * inv, mt2 = red[0][5] * inv;
             __syncthreads();
@@ -171,11 +186,11 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
                 P3[3 * i] = ox; P3[3 * i + 1] = oy; P3[3 * i + 2] = oz;
             }
             __syncthreads();
-            const double pf = s_fit, pr = s_rmse;
+            const double pf = sh.s_fit, pr = sh.s_rmse;
             __syncthreads();
             evaluate();
             ++it;
-            if (__builtin_fabs(pf - s_fit) < a.rel_fit && __builtin_fabs(pr - s_rmse) < a.rel_rmse) break;
+            if (__builtin_fabs(pf - sh.s_fit) < a.rel_fit && __builtin_fabs(pr - sh.s_rmse) < a.rel_rmse) break;
         }
     }
     if (a.corr_tgt)
@@ -183,10 +198,10 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
             a.corr_tgt[(size_t)p * a.Nmax + i] = (valid && i < n) ? cj[i] : -1;
     if (tid == 0) {
         for (int k = 0; k < 16; ++k) a.T_out[(size_t)p * 16 + k] = T[k];
-        a.fit_out[2 * p] = valid ? s_fit : 0.0;
-        a.fit_out[2 * p + 1] = valid ? s_rmse : 0.0;
+        a.fit_out[2 * p] = valid ? sh.s_fit : 0.0;
+        a.fit_out[2 * p + 1] = valid ? sh.s_rmse : 0.0;
         a.stats[2 * p] = it;
-        a.stats[2 * p + 1] = valid ? s_count : 0;
+        a.stats[2 * p + 1] = valid ? sh.s_count : 0;
     }
 }
 
@@ -207,15 +222,27 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
         if (rc != PCR_OK) return rc;
     } else {
-        a.grid = GridBatch{nullptr, nullptr, 1, 0, 1.0};
+        a.grid = GridBatch{};
+        a.grid.S = 1;
+        a.grid.cell = 1.0;
     }
     char *ws = (char *)workspace(8, (sizeof(double) * 3 + sizeof(int)) * (size_t)P * (Nmax ? Nmax : 1) + 64);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
     a.P3 = (double *)ws;
     a.cj = (int *)(ws + sizeof(double) * 3 * (size_t)P * (Nmax ? Nmax : 1));
     a.T_out = T_out; a.fit_out = fit_out; a.stats = stats; a.corr_tgt = corr_tgt;
+    const size_t hdr = (sizeof(IShared) + 15) & ~size_t(15);
+    const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds_bytes(Mmax, a.grid.S, 160 * 1024 - hdr) : 0;
     prof_begin(s, kProfIcp);
-    hipLaunchKernelGGL(icp_kernel, dim3(P), dim3(1024), 0, s, a);
+    if (gbytes > 0) {
+        PCR_HIP_CHECK(hipFuncSetAttribute((const void *)icp_kernel<true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)(hdr + gbytes)));
+        hipLaunchKernelGGL(icp_kernel<true>, dim3(P), dim3(1024), hdr + gbytes, s, a);
+    } else {
+        PCR_HIP_CHECK(hipFuncSetAttribute((const void *)icp_kernel<false>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)hdr));
+        hipLaunchKernelGGL(icp_kernel<false>, dim3(P), dim3(1024), hdr, s, a);
+    }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfIcp);
     return PCR_OK;
