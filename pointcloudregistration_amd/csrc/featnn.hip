@@ -243,9 +243,13 @@ struct DualArgs {
     int *cpi;
 };
 
+// merge two top-2 states; lowest index wins equal minima.  Branch-free: the
+// screen's values are finite or +inf (never NaN), so plain selects are exact.
 __device__ __forceinline__ void top2_merge(float &b1, int &i1, float &b2, float o1, int oi, float o2) {
-    const bool take = (o1 < b1) || (o1 == b1 && oi < i1);
-    const float n2 = fminf(fmaxf(b1, o1), fminf(b2, o2));
+    const bool take = (o1 < b1) | ((o1 == b1) & (oi < i1));
+    const float mx = (b1 < o1) ? o1 : b1;
+    const float m2 = (o2 < b2) ? o2 : b2;
+    const float n2 = (m2 < mx) ? m2 : mx;
     b1 = take ? o1 : b1;
     i1 = take ? oi : i1;
     b2 = n2;
@@ -518,8 +522,12 @@ __global__ __launch_bounds__(512) void featnn_dual3(DualArgs3 a) {
         for (int g = 0; g < G; ++g) {
             const int ct = grp * G + g;
             const int j = ct * 32 + (l & 31);
-            float c1 = __builtin_inff(), c2 = __builtin_inff();
-            int ci = 0;
+            // column direction: 4 independent chains (q = r & 3, rows increasing
+            // along each), merged with the index tie-break
+            float c1[4], c2[4];
+            int ci[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { c1[q] = __builtin_inff(); c2[q] = __builtin_inff(); ci[q] = 0; }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float v = acc[g][r];
@@ -527,19 +535,25 @@ __global__ __launch_bounds__(512) void featnn_dual3(DualArgs3 a) {
                 const bool c = v < b1[r];
                 b1[r] = c ? v : b1[r];
                 i1[r] = c ? j : i1[r];
-                c2 = __builtin_amdgcn_fmed3f(c1, c2, v);
-                const bool cc = v < c1;
-                c1 = cc ? v : c1;
-                ci = cc ? (qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) : ci;
+                const int q = r & 3;
+                c2[q] = __builtin_amdgcn_fmed3f(c1[q], c2[q], v);
+                const bool cc = v < c1[q];
+                c1[q] = cc ? v : c1[q];
+                ci[q] = cc ? (qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) : ci[q];
             }
-            const float o1 = __shfl_xor(c1, 32, 64), o2 = __shfl_xor(c2, 32, 64);
-            const int oi = __shfl_xor(ci, 32, 64);
-            top2_merge(c1, ci, c2, o1, oi, o2);
+            top2_merge(c1[0], ci[0], c2[0], c1[1], ci[1], c2[1]);
+            top2_merge(c1[2], ci[2], c2[2], c1[3], ci[3], c2[3]);
+            top2_merge(c1[0], ci[0], c2[0], c1[2], ci[2], c2[2]);
+            float cc1 = c1[0], cc2 = c2[0];
+            int cci = ci[0];
+            const float o1 = __shfl_xor(cc1, 32, 64), o2 = __shfl_xor(cc2, 32, 64);
+            const int oi = __shfl_xor(cci, 32, 64);
+            top2_merge(cc1, cci, cc2, o1, oi, o2);
             if (h == 0) {
                 const int e = (buf * G + g) * 256 + wid * 32 + l;
-                Pc1[e] = c1;
-                Pc2[e] = c2;
-                Pci[e] = ci;
+                Pc1[e] = cc1;
+                Pc2[e] = cc2;
+                Pci[e] = cci;
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
