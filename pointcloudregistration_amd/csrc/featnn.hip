@@ -603,6 +603,173 @@ __global__ __launch_bounds__(512) void featnn_dual3(DualArgs3 a) {
     if (!((double)mb2 - (double)mb1 > bound)) a.list12[atomicAdd(a.count12, 1)] = p * a.Nmax + row;
 }
 
+
+// ---------------------------------------------------------------------------
+// v4 = v3 + tile-level software pipelining inside each wave: the MFMA chain of
+// tile t+1 is issued, then the VALU top-2 epilogue of tile t runs in its
+// shadow (sched_group_barrier interleaves 1 LDS read : 1 MFMA : N VALU), so
+// the matrix pipe and the VALU overlap within one wave instead of relying on
+// the partner wave (the per-group barrier keeps partners in phase).  G = 8
+// tiles per LDS group; padded tiles exist in the packed buffer with +inf
+// norms, so the loop body has no tail branches.
+// ---------------------------------------------------------------------------
+template <int KCH, int G>
+__global__ __launch_bounds__(512) void featnn_dual4(DualArgs3 a) {
+    constexpr int S2a = 8 * KCH + 1;
+    constexpr int kB = G * S2a * 64;
+    constexpr int kP = G * 8 * 32;
+    __shared__ __attribute__((aligned(16))) float smem[2 * kB + 2 * 3 * kP];
+    float *Bs = smem;
+    float *Pc1 = smem + 2 * kB;
+    float *Pc2 = Pc1 + 2 * kP;
+    int *Pci = reinterpret_cast<int *>(Pc2 + 2 * kP);
+    const int p = blockIdx.y, rb = blockIdx.x;
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    const int qt = rb * 8 + wid;
+    const bool active = qt * 32 < n;
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    const int ntp = a.ntm;  // packed tiles incl. padding (>= ngroups*G)
+
+    float A[S2a];
+    const float *qp = a.Ap + (((size_t)p * a.ntn + (active ? qt : 0)) * S2a) * 64 + l;
+#pragma unroll
+    for (int s = 0; s < S2a; ++s) A[s] = qp[(size_t)s * 64];
+    if (!active) {
+#pragma unroll
+        for (int s = 0; s < S2a - 1; ++s) A[s] = 0.0f;
+        A[S2a - 1] = h == 0 ? 1.0f : __builtin_inff();
+    }
+    float b1[16], b2[16];
+    int i1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); i1[r] = 0; }
+    const int rowbase = qt * 32 + 4 * h;
+
+    const float *bsrc = a.Bp + ((size_t)p * ntp * S2a) * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * S2a; c += 8) {
+            const int g = c / S2a, srow = c - g * S2a;
+            const int ct = grp * G + g;
+            const float *src = bsrc + ((size_t)ct * S2a + srow) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + (g * S2a + srow) * 64), 4,
+                0, 0);
+        }
+    };
+    auto chain = [&](const float *Bt) {
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < S2a; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], Bt[s * 64], acc, 0, 0, 0);
+        return acc;
+    };
+    auto epilogue = [&](const f32x16 &acc, int ct, int bufg) {
+        const int j = ct * 32 + (l & 31);
+        float c1[4], c2[4];
+        int ci[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { c1[q] = __builtin_inff(); c2[q] = __builtin_inff(); ci[q] = 0; }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float v = acc[r];
+            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], v);
+            const bool c = v < b1[r];
+            b1[r] = c ? v : b1[r];
+            i1[r] = c ? j : i1[r];
+            const int q = r & 3;
+            c2[q] = __builtin_amdgcn_fmed3f(c1[q], c2[q], v);
+            const bool cc = v < c1[q];
+            c1[q] = cc ? v : c1[q];
+            ci[q] = cc ? (rowbase + (r & 3) + 8 * (r >> 2)) : ci[q];
+        }
+        top2_merge(c1[0], ci[0], c2[0], c1[1], ci[1], c2[1]);
+        top2_merge(c1[2], ci[2], c2[2], c1[3], ci[3], c2[3]);
+        top2_merge(c1[0], ci[0], c2[0], c1[2], ci[2], c2[2]);
+        const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
+        const int oi = __shfl_xor(ci[0], 32, 64);
+        top2_merge(c1[0], ci[0], c2[0], o1, oi, o2);
+        // both half-waves hold the same merged state: both write (benign)
+        const int e = bufg * 256 + wid * 32 + (l & 31);
+        Pc1[e] = c1[0];
+        Pc2[e] = c2[0];
+        Pci[e] = ci[0];
+    };
+    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = grp & 1;
+        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        const float *Bb = Bs + buf * kB + l;
+        f32x16 cur = chain(Bb);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            f32x16 nxt;
+            if (g + 1 < G) nxt = chain(Bb + (g + 1) * S2a * 64);
+            epilogue(cur, grp * G + g, buf * G + g);
+            if (g + 1 < G) {
+#pragma unroll
+                for (int k = 0; k < S2a; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 10, 0); // VALU
+                }
+                cur = nxt;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < G * 32) {
+            const int g = t >> 5, col = t & 31, ct = grp * G + g;
+            if (ct < ntc) {
+                const int e0 = (buf * G + g) * 256 + col;
+                float m1 = Pc1[e0], m2 = Pc2[e0];
+                int mi = Pci[e0];
+#pragma unroll
+                for (int w = 1; w < 8; ++w)
+                    top2_merge(m1, mi, m2, Pc1[e0 + 32 * w], Pci[e0 + 32 * w], Pc2[e0 + 32 * w]);
+                const size_t o = cpoff + (size_t)ct * 32 + col;
+                a.cp1[o] = m1;
+                a.cp2[o] = m2;
+                a.cpi[o] = mi;
+            }
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float ob1 = __shfl_xor(b1[r], o, 64);
+            const float ob2 = __shfl_xor(b2[r], o, 64);
+            const int oi1 = __shfl_xor(i1[r], o, 64);
+            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+        }
+    }
+    const int lr = l & 31;
+    if (lr >= 16) return;
+    float mb1 = 0.f, mb2 = 0.f;
+    int mi1 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+    if (row >= n) return;
+    a.nn12[(size_t)p * a.Nmax + row] = mi1;
+    const double Gm = (double)__uint_as_float(a.gmax[p]);
+    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
+    const double K = 2.0 * S2a;
+    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (qn + Gm) * (qn + Gm);
+    if (!((double)mb2 - (double)mb1 > bound)) a.list12[atomicAdd(a.count12, 1)] = p * a.Nmax + row;
+}
+
 __global__ void featnn_colmerge3(DualArgs3 a, int32_t *nn21, int *list21, int *count21, int S2a) {
     const int p = blockIdx.y;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -628,11 +795,11 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
 
-static int featnn_mode() {  // 1: two-pass v1, 2: one-pass v2, 3 (default): one-pass v3
+static int featnn_mode() {  // 1: two-pass v1, 2: one-pass v2, 3: v3, 4 (default): pipelined v4
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("PCR_FEATNN_MODE");
-        v = (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 3;
+        v = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 4;
     }
     return v;
 }
@@ -642,7 +809,7 @@ static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int
                             int32_t *nn21, hipStream_t s) {
     const int KCH = cdiv(D, 16);
     const int S2a = 8 * KCH + 1;
-    const int ntn = cdiv(Nmax, 32), ntm = cdiv(Mmax, 32);
+    const int ntn = cdiv(Nmax, 32), ntm = cdiv(Mmax, 32) + 8;  // +8 padded (+inf) tiles
     const size_t ap = (size_t)P * ntn * S2a * 64, bp = (size_t)P * ntm * S2a * 64;
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes = 4 * (ap + bp + nn_n + nn_m + 2 * (size_t)P + 2 + (size_t)P * (Nmax + Mmax));
@@ -675,13 +842,24 @@ static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int
     d.cpi = (int *)(d.cp2 + cpn);
     const dim3 g(d.nrb, P);
     prof_begin(s, kProfFeatScreen);
-    switch (KCH) {
+    if (featnn_mode() == 4) {
+        switch (KCH) {
+#define PCR_D4CASE(K, GG) \
+    case K: hipLaunchKernelGGL((featnn_dual4<K, GG>), g, dim3(512), 0, s, d); break;
+            PCR_D4CASE(1, 4) PCR_D4CASE(2, 4) PCR_D4CASE(3, 4) PCR_D4CASE(4, 4)
+            PCR_D4CASE(5, 2) PCR_D4CASE(6, 2) PCR_D4CASE(7, 2) PCR_D4CASE(8, 2)
+#undef PCR_D4CASE
+            default: set_error("feature dim too large"); return PCR_ERR_ARG;
+        }
+    } else {
+        switch (KCH) {
 #define PCR_D3CASE(K, GG) \
     case K: hipLaunchKernelGGL((featnn_dual3<K, GG>), g, dim3(512), 0, s, d); break;
-        PCR_D3CASE(1, 4) PCR_D3CASE(2, 4) PCR_D3CASE(3, 3) PCR_D3CASE(4, 2)
-        PCR_D3CASE(5, 2) PCR_D3CASE(6, 2) PCR_D3CASE(7, 1) PCR_D3CASE(8, 1)
+            PCR_D3CASE(1, 4) PCR_D3CASE(2, 4) PCR_D3CASE(3, 3) PCR_D3CASE(4, 2)
+            PCR_D3CASE(5, 2) PCR_D3CASE(6, 2) PCR_D3CASE(7, 1) PCR_D3CASE(8, 1)
 #undef PCR_D3CASE
-        default: set_error("feature dim too large"); return PCR_ERR_ARG;
+            default: set_error("feature dim too large"); return PCR_ERR_ARG;
+        }
     }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfFeatScreen);
@@ -730,7 +908,7 @@ int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax
                        hipStream_t s) {
     const int KCH = cdiv(D, 16);
     PCR_REQUIRE(D >= 1 && KCH <= 8, PCR_ERR_ARG, "feature_match: D=%d unsupported (1..128)", D);
-    if (featnn_mode() == 3)
+    if (featnn_mode() >= 3)
         return feature_match_v3(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
     const int S2 = 8 * KCH;
     const int ntn = cdiv(Nmax, 32), ntm = cdiv(Mmax, 32);
