@@ -124,8 +124,9 @@ def main():
         step()
     torch.cuda.synchronize()
     _lib.profile_enable(True)
-    for pid in range(5):
+    for pid in range(7):
         _lib.profile_read(pid, reset=True)
+    _lib.featnn_rescan_rows(reset=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -138,8 +139,10 @@ def main():
     prof = {name: _lib.profile_read(pid) for name, pid in
             (("feature_screen", _lib.PROF_FEAT_SCREEN), ("nnd_fwd", _lib.PROF_NND_FWD),
              ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
-             ("icp", _lib.PROF_ICP))}
+             ("icp", _lib.PROF_ICP), ("feat_rescan", _lib.PROF_FEAT_RESCAN),
+             ("feat_pack", _lib.PROF_FEAT_PACK))}
     _lib.profile_enable(False)
+    rescan_rows = _lib.featnn_rescan_rows(reset=True)
 
     # stage split of one extra (untimed) step
     pipe.run(time_stages=True)
@@ -184,6 +187,7 @@ def main():
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch},
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+        "featnn_rescan_rows_per_step": [r / args.steps for r in rescan_rows],
         "stages_ms": stages,
         "accuracy": {"rre_deg_median": float(np.median(rre)), "rre_deg_max": float(np.max(rre)),
                      "rte_median": float(np.median(rte)), "rte_max": float(np.max(rte)),

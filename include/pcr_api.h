@@ -34,10 +34,15 @@ int pcr_version(void);
 
 /* Optional per-kernel timing with HIP events recorded on the launch stream
  * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,
- * 3 ICP, 4 RANSAC hypotheses).  pcr_profile_read synchronizes the pending
+ * 3 ICP, 4 RANSAC hypotheses, 5 feature rescan, 6 feature pack).  pcr_profile_read synchronizes the pending
  * events and returns the accumulated milliseconds and launch count. */
 void pcr_profile_enable(int32_t on);
 int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset);
+
+/* Diagnostic: rows (src->tgt, tgt->src) that the feature-NN screen could not
+ * certify and sent to the exact f64 rescan since the last reset.  Synchronizes
+ * the device. */
+int pcr_featnn_rescan_rows(int64_t *rows12, int64_t *rows21, int32_t reset);
 
 /* ---------------------------------------------------------------------------
  * a1 -- brute-force bidirectional 1-NN ("nnd" / Chamfer building block).

@@ -90,6 +90,8 @@ def load():
         lib.pcr_profile_enable.argtypes = [_i32]
         lib.pcr_profile_read.restype = ctypes.c_int
         lib.pcr_profile_read.argtypes = [_i32, ctypes.POINTER(_f64), ctypes.POINTER(_i64), _i32]
+        lib.pcr_featnn_rescan_rows.restype = ctypes.c_int
+        lib.pcr_featnn_rescan_rows.argtypes = [ctypes.POINTER(_i64), ctypes.POINTER(_i64), _i32]
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
@@ -99,10 +101,12 @@ def load():
 
 
 def exported_symbols():
-    return ["pcr_last_error", "pcr_version", "pcr_profile_enable", "pcr_profile_read"] + list(SIGNATURES)
+    return ["pcr_last_error", "pcr_version", "pcr_profile_enable", "pcr_profile_read",
+            "pcr_featnn_rescan_rows"] + list(SIGNATURES)
 
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
+PROF_FEAT_RESCAN, PROF_FEAT_PACK = 5, 6
 
 
 def profile_enable(on=True):
@@ -116,6 +120,15 @@ def profile_read(pid, reset=True):
     if rc != PCR_OK:
         raise PcrError(load().pcr_last_error().decode())
     return ms.value, cnt.value
+
+
+def featnn_rescan_rows(reset=True):
+    """(rows12, rows21) sent to the exact feature-NN rescan since the last reset."""
+    a, b = _i64(0), _i64(0)
+    rc = load().pcr_featnn_rescan_rows(ctypes.byref(a), ctypes.byref(b), 1 if reset else 0)
+    if rc != PCR_OK:
+        raise PcrError(load().pcr_last_error().decode())
+    return a.value, b.value
 
 
 def call(name, *args):

@@ -23,6 +23,7 @@
 #include "pcr_internal.h"
 #include "scan.h"
 #include <stdlib.h>
+#include <algorithm>
 
 namespace pcr {
 namespace {
@@ -791,17 +792,954 @@ __global__ void featnn_colmerge3(DualArgs3 a, int32_t *nn21, int *list21, int *c
     if (!((double)b2 - (double)b1 > bound)) list21[atomicAdd(count21, 1)] = p * a.Mmax + j;
 }
 
+// ---------------------------------------------------------------------------
+// v5: f16 x3 split screen on v_mfma_f32_32x32x16_f16 (32 cycles per 16-deep
+// k-step vs 64 per 2-deep step of the f32 MFMA: 7 instead of 17 x 4 cycles
+// per 32x32 tile at D = 32).
+//   scale: per pair x = f * 2^e (exact), e chosen so max|x| in [2^(T-1), 2^T)
+//          (T = 12 at D <= 64) -> every x fits f16 with room for the products.
+//   split: x = hi + lo + e_x, hi = f16(x), lo = f16(x - hi): |e_x| <= 2^-22|x|
+//          + 2^-14 (the 2^-14 covers f16 subnormals even if flushed).
+//   operands (k order): A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c]
+//                       B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo]
+//          nx = |x|^2 / c split into three f16 parts, c = 2^cs fits f16.
+//   C = 0 -> d'_ij = |x_i|^2 + |y_j|^2 - 2 x_i.y_j (scaled by 2^2e) with
+//   |d' - d'_exact| <= err(q, G) (bound5 below).  Products are exact in f32;
+//   the accumulation is charged 2 (Kt + 2) u (|x| + |y|)^2 whatever the
+//   MFMA's internal summation order.  Rows/columns whose top-2 gap is not
+//   above 2 err are rescanned exactly in f64 (featnn_rescan2).
+// Packed layout: [pair][tile][chunk][lane] of 8 halves (lane l: row/col l&31,
+// k = 16 chunk + 8 (l>>5) + j); padded tiles are valid encodings of +inf
+// rows, so no loop has a tail.  Grid: 1-D, XCD-aware: all row blocks of a
+// pair run on one XCD, whose L2 then holds that pair's B image (1.8 MB).
+// ---------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+struct Split5 {
+    int T;   // target exponent of max|x|
+    int cs;  // norm slot scale c = 2^cs
+};
+inline Split5 split5_params(int D) {
+    int L = 0;
+    while ((1 << L) < D) ++L;
+    Split5 s;
+    s.T = (30 - L) / 2 < 12 ? (30 - L) / 2 : 12;
+    s.cs = 2 * s.T + L - 15;
+    return s;
+}
+
+// max |element| of each pair's clouds (f32 bits; both clouds -> same slot)
+__global__ __launch_bounds__(256) void feat_maxabs(const float *X, const int32_t *n, int Nmax,
+                                                   int D, unsigned *mx) {
+    const int p = blockIdx.y;
+    const size_t tot = (size_t)count_of(n, p, Nmax) * D;
+    const float *x = X + (size_t)p * Nmax * D;
+    float m = 0.0f;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
+         i += (size_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(mx + p, __float_as_uint(m));
+}
+
+__device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
+    const int E = (int)((mbits >> 23) & 0xff);
+    if (E == 0 || E == 255) return 1.0f;
+    const int e = min(max(T + 126 - E, -126), 127);
+    return __int_as_float((e + 127) << 23);
+}
+
+// role 0: rows (A), role 1: columns (B).  256-thread blocks, one wave per
+// 32-row tile; each tile is staged through LDS with coalesced loads (scaled,
+// exact) and every lane emits its NCH 16-byte operand fragments.
+__global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t *n, int Nmax, int D,
+                                                  int NCH, int ntiles, int role, Split5 sp,
+                                                  const unsigned *mx, f16x8 *Xp, float *nrm,
+                                                  unsigned *nmax) {
+    __shared__ float xs[4][32][65];  // D <= 64 (+1 pad: conflict-free row reads)
+    const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
+    const int cnt = count_of(n, p, Nmax);
+    const int nrows = min(max(cnt - t * 32, 0), 32);
+    const float s = pair_scale5(mx[p], sp.T);
+    const float *base = X + ((size_t)p * Nmax + (size_t)t * 32) * D;
+    float (*x)[65] = xs[w];
+    for (int e = l; e < 32 * D; e += 64) {
+        const int r = e / D, k = e - r * D;
+        x[r][k] = r < nrows ? base[e] * s : 0.0f;
+    }
+    __syncthreads();
+    const int rr = l & 31, h = l >> 5;
+    const bool valid = rr < nrows;
+    double acc = 0.0;
+    for (int k = 0; k < D; ++k) {
+        const double v = (double)x[rr][k];
+        acc = acc + v * v;
+    }
+    // norm parts of acc / c (exact power-of-two division)
+    _Float16 np[3];
+    if (valid) {
+        double wv = acc * __builtin_ldexp(1.0, -sp.cs);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            np[q] = (_Float16)(float)wv;  // |wv| < 2^15: double->float->half may round twice;
+            wv = wv - (double)np[q];      // the bound charges 2^-11 per part regardless
+        }
+    } else {
+        // finite sentinel 3 * 65504 * c > any real distance (<= 4 D 2^2T):
+        // index bits are OR-ed into screen values, which must not be inf
+        np[0] = (_Float16)65504.0f;
+        np[1] = (_Float16)65504.0f;
+        np[2] = (_Float16)65504.0f;
+    }
+    const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
+    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NCH * 64 + l;
+    for (int c = 0; c < NCH; ++c) {
+        f16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * c + 8 * h + j;
+            _Float16 v = (_Float16)0.0f;
+            if (k < 3 * D) {
+                const int seg = (k >= D) + (k >= 2 * D);
+                const float xv = x[rr][k - seg * D];
+                const _Float16 hi = (_Float16)xv;
+                const _Float16 lo = (_Float16)(xv - (float)hi);
+                if (role == 0) v = (_Float16)(-2.0f * (float)(seg == 2 ? lo : hi));
+                else v = (seg == 1) ? lo : hi;
+            } else {
+                const int kk = k - 3 * D;
+                if (kk < 3) v = role == 0 ? np[kk] : cval;
+                else if (kk < 6) v = role == 0 ? cval : np[kk - 3];
+            }
+            o[j] = v;
+        }
+        dst[(size_t)c * 64] = o;
+    }
+    if (h == 0) {
+        const float r = valid ? (float)__builtin_sqrt(acc) : 0.0f;
+        nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+        if (valid) atomicMax(nmax + p, __float_as_uint(r));
+    }
+}
+
+// certification threshold for a top-2 gap in scaled units (see header)
+__device__ __forceinline__ double bound5(double q, double G, int Kt, int D) {
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double qg = q + G;
+    const double err = 2.0 * (Kt + 2) * u * qg * qg + 6.0 * 2.384185791015625e-07 * q * G +
+                       1.220703125e-04 * __builtin_sqrt((double)D) * qg +
+                       1.1641532182693481e-10 * (q * q + G * G) + 4.0;
+    return 2.0 * err;
+}
+
+struct DualArgs5 {
+    const f16x8 *Ap, *Bp;
+    const float *fnr, *gnr;  // scaled norms
+    const unsigned *fmax, *gmax;
+    const int32_t *n_src, *n_tgt;
+    int P, Nmax, Mmax, ntn, ntm, nrb, D, ctbits;
+    int32_t *nn12;
+    int *list12, *count12;
+    float *cp1, *cp2;
+    int *cpi;
+};
+
+// raw v_min / v_med3 on bit-packed values: as builtins the compiler inserts a
+// NaN canonicalisation (v_max x,x) per packed operand.  Inputs are never
+// signalling NaNs; a quiet NaN (NaN feature) is ignored by IEEE min, as the
+// oracle's strict < ignores it, or forces a rescan.
+__device__ __forceinline__ float vmin(float a, float b) {
+    float d;
+    asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ float vmed3(float a, float b, float c) {
+    float d;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// ABL (debug ablations, results invalid): 1 no epilogue, 2 no MFMA, 3 no
+// barrier/DMA (B read from buffer 0)
+template <int NCH, int G, int ABL = 0>
+__global__ __launch_bounds__(512) void featnn_dual5(DualArgs5 a) {
+    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
+    constexpr int kP = G * 8 * 32;
+    __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 2 * 2 * kP * 4];
+    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem);
+    float *Pc1 = reinterpret_cast<float *>(smem + 2 * kB * 16);  // [2][G][8 waves][32 cols]
+    float *Pc2 = Pc1 + 2 * kP;
+    // XCD-aware: hardware XCD = linear block id % 8; keep a pair on one XCD
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
+    if (p >= a.P) return;  // whole block
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    const int qt = rb * 8 + wid;  // < ntn (row tiles padded to nrb*8)
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    // index packing (the codes ride in the low mantissa bits; the
+    // certification charges the perturbation): row values carry the column
+    // tile ct in their low ctbits; column values carry (wave, half, register)
+    // = the row within the 256-row block in their low 8 bits.
+    const unsigned ctmask = (1u << a.ctbits) - 1u;
+    unsigned keep_r = ~ctmask;
+    asm("" : "+v"(keep_r));  // VGPR: a VOP3 reads one SGPR on gfx9 (ct is the other operand)
+    unsigned ccode[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        ccode[r] = (unsigned)((wid << 5) | (h << 4) | r);
+        asm("" : "+v"(ccode[r]));  // opaque: one v_and_or per column value
+    }
+
+    f16x8 A[NCH];
+    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NCH * 64 + l;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
+    float b1[16], b2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
+
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NCH * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * NCH; c += 8) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
+        }
+    };
+    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = ABL == 3 ? 0 : grp & 1;
+        if (ABL != 3 && grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        const f16x8 *Bb = Bs + buf * kB + l;
+        f32x16 acc[G];
+        if (ABL == 2) {
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[g][r] = __uint_as_float(ccode[r] ^ (unsigned)(grp * G + g));
+        } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bb[(g * NCH + c) * 64], acc[g],
+                                                                0, 0, 0);
+        }
+        if (ABL == 1) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) b1[g] = vmin(b1[g], acc[g][g]);
+        } else
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            unsigned ct = (unsigned)(grp * G + g);
+            asm("" : "+s"(ct));  // keep ct one scalar: one v_and_or per row value
+            float c1[4], c2[4];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const unsigned ub = __float_as_uint(acc[g][r]);
+                const float vr = __uint_as_float((ub & keep_r) | ct);
+                const float vc = __uint_as_float((ub & 0xFFFFFF00u) | ccode[r]);
+                b2[r] = vmed3(b1[r], b2[r], vr);
+                b1[r] = vmin(b1[r], vr);
+                const int q = r & 3;
+                if (r < 4) {  // chain q starts at r = q
+                    c1[q] = vc;
+                    c2[q] = __builtin_inff();
+                } else {
+                    c2[q] = vmed3(c1[q], c2[q], vc);
+                    c1[q] = vmin(c1[q], vc);
+                }
+            }
+            // packed top-2 merges: second of two sorted pairs = med3(a1, b1, min(a2, b2))
+#pragma unroll
+            for (int q = 0; q < 4; q += 2) {
+                const float m2 = vmin(c2[q], c2[q + 1]);
+                c2[q] = vmed3(c1[q], c1[q + 1], m2);
+                c1[q] = vmin(c1[q], c1[q + 1]);
+            }
+            float m2 = vmin(c2[0], c2[2]);
+            c2[0] = vmed3(c1[0], c1[2], m2);
+            c1[0] = vmin(c1[0], c1[2]);
+            const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
+            m2 = vmin(c2[0], o2);
+            c2[0] = vmed3(c1[0], o1, m2);
+            c1[0] = vmin(c1[0], o1);
+            // both halves hold the merged state; both write (same value)
+            const int e = (buf * G + g) * 256 + wid * 32 + (l & 31);
+            Pc1[e] = c1[0];
+            Pc2[e] = c2[0];
+        }
+        if (ABL == 3) continue;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < G * 32) {
+            const int g = t >> 5, col = t & 31, ct = grp * G + g;
+            if (ct < ntc) {
+                const int e0 = (buf * G + g) * 256 + col;
+                float m1 = Pc1[e0], mm2 = Pc2[e0];
+#pragma unroll
+                for (int w = 1; w < 8; ++w) {
+                    const float o1 = Pc1[e0 + 32 * w], o2 = Pc2[e0 + 32 * w];
+                    const float t2 = vmin(mm2, o2);
+                    mm2 = vmed3(m1, o1, t2);
+                    m1 = vmin(m1, o1);
+                }
+                const unsigned code = __float_as_uint(m1) & 255u;
+                const int r = code & 15;
+                const int mi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 +
+                               (r & 3) + 8 * (r >> 2);
+                const size_t o = cpoff + (size_t)ct * 32 + col;
+                a.cp1[o] = m1;
+                a.cp2[o] = mm2;
+                a.cpi[o] = mi;
+            }
+        }
+    }
+    if (qt * 32 >= n) return;
+    int i1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + (l & 31);
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float ob1 = __shfl_xor(b1[r], o, 64);
+            const float ob2 = __shfl_xor(b2[r], o, 64);
+            const int oi1 = __shfl_xor(i1[r], o, 64);
+            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+        }
+    }
+    const int lr = l & 31;
+    if (lr >= 16) return;
+    float mb1 = 0.f, mb2 = 0.f;
+    int mi1 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+    if (row >= n) return;
+    if (m == 0) { a.nn12[(size_t)p * a.Nmax + row] = 0; return; }
+    a.nn12[(size_t)p * a.Nmax + row] = mi1;
+    const double Gm = (double)__uint_as_float(a.gmax[p]);
+    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
+    const double pert = __builtin_ldexp(1.0, a.ctbits - 23) *
+                        (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2));
+    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NCH, a.D) + pert))
+        a.list12[(size_t)p * a.Nmax + atomicAdd(a.count12 + p, 1)] = row;
+}
+
+// ---------------------------------------------------------------------------
+// v6 = v5 with the two waves of each SIMD in complementary phases.  A
+// 512-thread workgroup places waves w and w+4 on the same SIMD; with one
+// barrier per LDS group both would issue their MFMAs together and then their
+// VALU epilogues together.  Waves 4-7 therefore lag one group: in barrier
+// interval k they run the epilogue of group k-1 (accumulators kept in
+// registers) and then the MFMAs of group k, while waves 0-3 run MFMAs of k
+// then its epilogue -- every SIMD pairs a matrix phase with a VALU phase.
+// Column partials rotate over 3 LDS buffers; group k's 8-wave merge runs in
+// interval k+2, after both halves have written it.  Waves 4-7 take
+// s_setprio 1 (the second-dispatched half otherwise loses VALU arbitration).
+// ---------------------------------------------------------------------------
+template <int NCH, int G>
+__global__ __launch_bounds__(512) void featnn_dual6(DualArgs5 a) {
+    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
+    constexpr int kP = G * 8 * 32;
+    __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 3 * 2 * kP * 4];
+    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem);
+    float *Pc1 = reinterpret_cast<float *>(smem + 2 * kB * 16);  // [3][G][8 waves][32 cols]
+    float *Pc2 = Pc1 + 3 * kP;
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
+    if (p >= a.P) return;  // whole block
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const bool lag = wid >= 4;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    const int qt = rb * 8 + wid;
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    const unsigned ctmask = (1u << a.ctbits) - 1u;
+    unsigned keep_r = ~ctmask;
+    asm("" : "+v"(keep_r));
+    unsigned ccode[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        ccode[r] = (unsigned)((wid << 5) | (h << 4) | r);
+        asm("" : "+v"(ccode[r]));
+    }
+    f16x8 A[NCH];
+    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NCH * 64 + l;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
+    float b1[16], b2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
+
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NCH * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * NCH; c += 8) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
+        }
+    };
+    auto chain = [&](int buf, f32x16 (&acc)[G]) {
+        const f16x8 *Bb = Bs + buf * kB + l;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bb[(g * NCH + c) * 64], acc[g],
+                                                                0, 0, 0);
+    };
+    auto epilogue = [&](const f32x16 (&acc)[G], int grp) {
+        const int pb = grp % 3;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            unsigned ct = (unsigned)(grp * G + g);
+            asm("" : "+s"(ct));
+            float c1[4], c2[4];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const unsigned ub = __float_as_uint(acc[g][r]);
+                const float vr = __uint_as_float((ub & keep_r) | ct);
+                const float vc = __uint_as_float((ub & 0xFFFFFF00u) | ccode[r]);
+                b2[r] = vmed3(b1[r], b2[r], vr);
+                b1[r] = vmin(b1[r], vr);
+                const int q = r & 3;
+                if (r < 4) {
+                    c1[q] = vc;
+                    c2[q] = __builtin_inff();
+                } else {
+                    c2[q] = vmed3(c1[q], c2[q], vc);
+                    c1[q] = vmin(c1[q], vc);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q += 2) {
+                const float m2 = vmin(c2[q], c2[q + 1]);
+                c2[q] = vmed3(c1[q], c1[q + 1], m2);
+                c1[q] = vmin(c1[q], c1[q + 1]);
+            }
+            float m2 = vmin(c2[0], c2[2]);
+            c2[0] = vmed3(c1[0], c1[2], m2);
+            c1[0] = vmin(c1[0], c1[2]);
+            const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
+            m2 = vmin(c2[0], o2);
+            c2[0] = vmed3(c1[0], o1, m2);
+            c1[0] = vmin(c1[0], o1);
+            const int e = (pb * G + g) * 256 + wid * 32 + (l & 31);
+            Pc1[e] = c1[0];
+            Pc2[e] = c2[0];
+        }
+    };
+    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
+    auto merge = [&](int grp) {  // 8-wave column merge of group grp
+        const int t = threadIdx.x;
+        if (t < G * 32) {
+            const int g = t >> 5, col = t & 31, ct = grp * G + g;
+            if (ct < ntc) {
+                const int e0 = ((grp % 3) * G + g) * 256 + col;
+                float m1 = Pc1[e0], mm2 = Pc2[e0];
+#pragma unroll
+                for (int w = 1; w < 8; ++w) {
+                    const float o1 = Pc1[e0 + 32 * w], o2 = Pc2[e0 + 32 * w];
+                    const float t2 = vmin(mm2, o2);
+                    mm2 = vmed3(m1, o1, t2);
+                    m1 = vmin(m1, o1);
+                }
+                const unsigned code = __float_as_uint(m1) & 255u;
+                const int r = code & 15;
+                const int mi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 +
+                               (r & 3) + 8 * (r >> 2);
+                const size_t o = cpoff + (size_t)ct * 32 + col;
+                a.cp1[o] = m1;
+                a.cp2[o] = mm2;
+                a.cpi[o] = mi;
+            }
+        }
+    };
+    if (lag) __builtin_amdgcn_s_setprio(1);
+    f32x16 acc[G];
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = grp & 1;
+        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        if (lag) {
+            if (grp > 0) epilogue(acc, grp - 1);
+            chain(buf, acc);
+        } else {
+            chain(buf, acc);
+            epilogue(acc, grp);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (grp >= 1) merge(grp - 1);
+    }
+    if (ngroups > 0) {
+        if (lag) epilogue(acc, ngroups - 1);
+        __syncthreads();
+        merge(ngroups - 1);
+    }
+    if (qt * 32 >= n) return;
+    int i1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + (l & 31);
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float ob1 = __shfl_xor(b1[r], o, 64);
+            const float ob2 = __shfl_xor(b2[r], o, 64);
+            const int oi1 = __shfl_xor(i1[r], o, 64);
+            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+        }
+    }
+    const int lr = l & 31;
+    if (lr >= 16) return;
+    float mb1 = 0.f, mb2 = 0.f;
+    int mi1 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+    if (row >= n) return;
+    if (m == 0) { a.nn12[(size_t)p * a.Nmax + row] = 0; return; }
+    a.nn12[(size_t)p * a.Nmax + row] = mi1;
+    const double Gm = (double)__uint_as_float(a.gmax[p]);
+    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
+    const double pert = __builtin_ldexp(1.0, a.ctbits - 23) *
+                        (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2));
+    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NCH, a.D) + pert))
+        a.list12[(size_t)p * a.Nmax + atomicAdd(a.count12 + p, 1)] = row;
+}
+
+// ---------------------------------------------------------------------------
+// v7 = v5 with an in-wave software pipeline.  Ablations of v5 showed its
+// phases add: MFMA chain (after its B-fragment LDS reads have landed) and
+// the VALU epilogue never overlap.  Here iteration g of a group issues, in one
+// scheduling region, the 7 MFMAs of tile g, the ds_read_b128 B fragments of
+// tile g+1 (register double buffer) and the epilogue of tile g-1, interleaved
+// 1 MFMA : 1 LDS read : V VALU by sched_group_barrier.  G = 8 tiles per LDS
+// group halves the barriers (B double buffer 2 x 57 KB + partials 32 KB).
+// ---------------------------------------------------------------------------
+template <int NCH, int G>
+__global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
+    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
+    constexpr int kP = G * 8 * 32;
+    __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 2 * 2 * kP * 4];
+    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem);
+    float *Pc1 = reinterpret_cast<float *>(smem + 2 * kB * 16);  // [2][G][8 waves][32 cols]
+    float *Pc2 = Pc1 + 2 * kP;
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
+    if (p >= a.P) return;  // whole block
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    const int qt = rb * 8 + wid;
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    const unsigned ctmask = (1u << a.ctbits) - 1u;
+    unsigned keep_r = ~ctmask;
+    asm("" : "+v"(keep_r));
+    unsigned ccode[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        ccode[r] = (unsigned)((wid << 5) | (h << 4) | r);
+        asm("" : "+v"(ccode[r]));
+    }
+    f16x8 A[NCH];
+    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NCH * 64 + l;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
+    float b1[16], b2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
+
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NCH * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * NCH; c += 8) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
+        }
+    };
+    auto epilogue = [&](const f32x16 &acc, unsigned ct, int pe) {
+        asm("" : "+s"(ct));
+        float c1[4], c2[4];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const unsigned ub = __float_as_uint(acc[r]);
+            const float vr = __uint_as_float((ub & keep_r) | ct);
+            const float vc = __uint_as_float((ub & 0xFFFFFF00u) | ccode[r]);
+            b2[r] = vmed3(b1[r], b2[r], vr);
+            b1[r] = vmin(b1[r], vr);
+            const int q = r & 3;
+            if (r < 4) {
+                c1[q] = vc;
+                c2[q] = __builtin_inff();
+            } else {
+                c2[q] = vmed3(c1[q], c2[q], vc);
+                c1[q] = vmin(c1[q], vc);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q += 2) {
+            const float m2 = vmin(c2[q], c2[q + 1]);
+            c2[q] = vmed3(c1[q], c1[q + 1], m2);
+            c1[q] = vmin(c1[q], c1[q + 1]);
+        }
+        float m2 = vmin(c2[0], c2[2]);
+        c2[0] = vmed3(c1[0], c1[2], m2);
+        c1[0] = vmin(c1[0], c1[2]);
+        const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
+        m2 = vmin(c2[0], o2);
+        c2[0] = vmed3(c1[0], o1, m2);
+        c1[0] = vmin(c1[0], o1);
+        const int e = pe * 256 + wid * 32 + (l & 31);
+        Pc1[e] = c1[0];
+        Pc2[e] = c2[0];
+    };
+    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = grp & 1;
+        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        const f16x8 *Bb = Bs + buf * kB + l;
+        f16x8 Bf[2][NCH];
+        f32x16 acc[2];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) Bf[0][c] = Bb[c * 64];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int cur = g & 1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[cur][r] = 0.0f;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+                acc[cur] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bf[cur][c], acc[cur], 0, 0, 0);
+            if (g + 1 < G) {
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NCH + c) * 64];
+            }
+            if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1), buf * G + g - 1);
+            // one region per iteration: MFMA : LDS read : VALU = 1 : 1 : 18
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, 18, 0);
+            }
+        }
+        epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1), buf * G + G - 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < G * 32) {
+            const int g = t >> 5, col = t & 31, ct = grp * G + g;
+            if (ct < ntc) {
+                const int e0 = (buf * G + g) * 256 + col;
+                float m1 = Pc1[e0], mm2 = Pc2[e0];
+#pragma unroll
+                for (int w = 1; w < 8; ++w) {
+                    const float o1 = Pc1[e0 + 32 * w], o2 = Pc2[e0 + 32 * w];
+                    const float t2 = vmin(mm2, o2);
+                    mm2 = vmed3(m1, o1, t2);
+                    m1 = vmin(m1, o1);
+                }
+                const unsigned code = __float_as_uint(m1) & 255u;
+                const int r = code & 15;
+                const int mi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 +
+                               (r & 3) + 8 * (r >> 2);
+                const size_t o = cpoff + (size_t)ct * 32 + col;
+                a.cp1[o] = m1;
+                a.cp2[o] = mm2;
+                a.cpi[o] = mi;
+            }
+        }
+    }
+    if (qt * 32 >= n) return;
+    int i1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + (l & 31);
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float ob1 = __shfl_xor(b1[r], o, 64);
+            const float ob2 = __shfl_xor(b2[r], o, 64);
+            const int oi1 = __shfl_xor(i1[r], o, 64);
+            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+        }
+    }
+    const int lr = l & 31;
+    if (lr >= 16) return;
+    float mb1 = 0.f, mb2 = 0.f;
+    int mi1 = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+    if (row >= n) return;
+    if (m == 0) { a.nn12[(size_t)p * a.Nmax + row] = 0; return; }
+    a.nn12[(size_t)p * a.Nmax + row] = mi1;
+    const double Gm = (double)__uint_as_float(a.gmax[p]);
+    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
+    const double pert = __builtin_ldexp(1.0, a.ctbits - 23) *
+                        (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2));
+    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NCH, a.D) + pert))
+        a.list12[(size_t)p * a.Nmax + atomicAdd(a.count12 + p, 1)] = row;
+}
+
+__global__ void featnn_colmerge5(DualArgs5 a, int32_t *nn21, int *list21, int *count21, int Kt) {
+    const int p = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = count_of(a.n_tgt, p, a.Mmax);
+    if (j >= m) return;
+    const int n = count_of(a.n_src, p, a.Nmax);
+    if (n == 0) { nn21[(size_t)p * a.Mmax + j] = 0; return; }
+    const int nrb_used = (((n + 31) >> 5) + 7) >> 3;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = 0;
+    for (int rb = 0; rb < nrb_used; ++rb) {
+        const size_t o = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32 + j;
+        top2_merge(b1, i1, b2, a.cp1[o], a.cpi[o], a.cp2[o]);
+    }
+    nn21[(size_t)p * a.Mmax + j] = i1;
+    const double F = (double)__uint_as_float(a.fmax[p]);
+    const double gn = (double)a.gnr[(size_t)p * a.ntm * 32 + j];
+    const double pert = 3.0517578125e-05 /* 2^-15: 8-bit row code */ *
+                        (__builtin_fabs((double)b1) + __builtin_fabs((double)b2));
+    if (!((double)b2 - (double)b1 > bound5(gn, F, Kt, a.D) + pert))
+        list21[(size_t)p * a.Mmax + atomicAdd(count21 + p, 1)] = j;
+}
+
+// exact f64 rescan of v5's per-pair ambiguous lists: one 256-thread block per
+// batch of R listed rows of one pair and direction; the rows sit in LDS as
+// f64, every thread streams candidates j = tid + 256 i once (float4 rows) and
+// keeps R running minima, so a pair's candidate cloud is read once per batch
+// instead of once per row.  blockIdx.z = direction (0: F->G, 1: G->F).
+// rows sent to the exact rescan since the last reset (diagnostic, pcr_featnn_rescan_rows)
+__device__ unsigned long long g_featnn_rescan_rows[2];
+
+struct RescanArgs5 {
+    const float *F, *G;
+    const int32_t *n_src, *n_tgt;
+    int Nmax, Mmax, D;
+    const int *list12, *list21, *cnt12, *cnt21;
+    int32_t *nn12, *nn21;
+};
+
+template <int DV, bool V4>
+__global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
+    // thread (row r = tid>>3, slice sl = tid&7): row r of the current batch of
+    // 32 listed rows (held as f64 in registers) against candidates sl, sl+8,
+    // ... of each 128-candidate chunk staged in LDS.  Row stride DV+4 floats:
+    // the 8 slices' ds_read_b128 hit disjoint banks, the rows of a slice
+    // broadcast.  Dims in [D, DV) are zero on both sides (exact zero terms).
+    constexpr int kChunk = 128, kSt = DV + 4;
+    __shared__ __attribute__((aligned(16))) float cs[kChunk * kSt];
+    const int dir = blockIdx.y, p = blockIdx.x;
+    const int tid = threadIdx.x, r = tid >> 3, sl = tid & 7;
+    const float *Q = dir ? a.G : a.F;
+    const float *C = dir ? a.F : a.G;
+    const int Nq = dir ? a.Mmax : a.Nmax, Nc = dir ? a.Nmax : a.Mmax;
+    const int nc = count_of(dir ? a.n_src : a.n_tgt, p, Nc);
+    const int *list = (dir ? a.list21 : a.list12) + (size_t)p * Nq;
+    const int cnt = (dir ? a.cnt21 : a.cnt12)[p];
+    if (tid == 0 && cnt > 0) atomicAdd(&g_featnn_rescan_rows[dir], (unsigned long long)cnt);
+    int32_t *nn = (dir ? a.nn21 : a.nn12) + (size_t)p * Nq;
+    const int D = a.D;
+    const float *cb = C + (size_t)p * Nc * D;
+    for (int b0 = 0; b0 < cnt; b0 += 32) {
+        const bool act = b0 + r < cnt;
+        const int row = act ? list[b0 + r] : 0;
+        const float *q = Q + ((size_t)p * Nq + row) * D;
+        double qd[DV];
+#pragma unroll
+        for (int k = 0; k < DV; ++k) qd[k] = k < D ? (double)q[k] : 0.0;
+        double best = __builtin_inf();
+        int bj = 0x7fffffff;
+        for (int c0 = 0; c0 < nc; c0 += kChunk) {
+            const int ncand = min(kChunk, nc - c0);
+            __syncthreads();  // previous chunk fully consumed
+            if (V4) {
+                for (int e = tid; e < kChunk * (DV / 4); e += 256) {
+                    const int i = e / (DV / 4), k = (e - i * (DV / 4)) * 4;
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (i < ncand && k < D)
+                        v = *reinterpret_cast<const float4 *>(cb + (size_t)(c0 + i) * D + k);
+                    *reinterpret_cast<float4 *>(cs + i * kSt + k) = v;
+                }
+            } else {
+                for (int e = tid; e < kChunk * DV; e += 256) {
+                    const int i = e / DV, k = e - i * DV;
+                    cs[i * kSt + k] = (i < ncand && k < D) ? cb[(size_t)(c0 + i) * D + k] : 0.0f;
+                }
+            }
+            __syncthreads();
+            for (int i = sl; i < ncand; i += 8) {
+                const float *cp = cs + i * kSt;
+                double acc = 0.0;
+#pragma unroll
+                for (int k = 0; k < DV; k += 4) {
+                    const float4 v = *reinterpret_cast<const float4 *>(cp + k);
+                    double df = qd[k] - (double)v.x;
+                    acc = acc + df * df;
+                    df = qd[k + 1] - (double)v.y;
+                    acc = acc + df * df;
+                    df = qd[k + 2] - (double)v.z;
+                    acc = acc + df * df;
+                    df = qd[k + 3] - (double)v.w;
+                    acc = acc + df * df;
+                }
+                if (acc < best) { best = acc; bj = c0 + i; }
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const double ob = __shfl_xor(best, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+        }
+        if (sl == 0 && act) nn[row] = (bj == 0x7fffffff) ? 0 : bj;
+    }
+}
+
+// exact f64 rescan (v3/v4 modes), one 256-thread block per listed row: the
+// query row is broadcast from LDS, each thread streams its candidates as
+// float4 rows with two independent chains in flight; lowest index wins ties.
+template <bool V4>
+__global__ __launch_bounds__(256) void featnn_rescan2(const float *Q, const float *C, int Nqmax,
+                                                      int Ncmax, int D, const int32_t *ncnt,
+                                                      const int *list, const int *list_count,
+                                                      int32_t *nn) {
+    __shared__ double qs[512];
+    __shared__ double wb[4];
+    __shared__ int wj[4];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int count = *list_count;
+    for (int e = blockIdx.x; e < count; e += gridDim.x) {
+        const int code = list[e];
+        const int p = code / Nqmax, row = code - p * Nqmax;
+        const int nc = count_of(ncnt, p, Ncmax);
+        const float *q = Q + ((size_t)p * Nqmax + row) * D;
+        for (int k = tid; k < D; k += 256) qs[k] = (double)q[k];
+        __syncthreads();
+        const float *cb = C + (size_t)p * Ncmax * D;
+        double best = __builtin_inf();
+        int bj = 0x7fffffff;
+        auto dist = [&](int j) {
+            const float *c = cb + (size_t)j * D;
+            double acc = 0.0;
+            if (V4) {
+                const float4 *c4 = reinterpret_cast<const float4 *>(c);
+                for (int k = 0; k < D; k += 4) {
+                    const float4 v = c4[k >> 2];
+                    double df = qs[k] - (double)v.x;
+                    acc = acc + df * df;
+                    df = qs[k + 1] - (double)v.y;
+                    acc = acc + df * df;
+                    df = qs[k + 2] - (double)v.z;
+                    acc = acc + df * df;
+                    df = qs[k + 3] - (double)v.w;
+                    acc = acc + df * df;
+                }
+            } else {
+                for (int k = 0; k < D; ++k) {
+                    const double df = qs[k] - (double)c[k];
+                    acc = acc + df * df;
+                }
+            }
+            return acc;
+        };
+        int j = tid;
+        for (; j + 256 < nc; j += 512) {
+            const double d0 = dist(j), d1 = dist(j + 256);
+            if (d0 < best) { best = d0; bj = j; }
+            if (d1 < best) { best = d1; bj = j + 256; }
+        }
+        if (j < nc) {
+            const double d0 = dist(j);
+            if (d0 < best) { best = d0; bj = j; }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double ob = __shfl_xor(best, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+        }
+        if (l == 0) { wb[w] = best; wj[w] = bj; }
+        __syncthreads();
+        if (tid == 0) {
+            best = wb[0];
+            bj = wj[0];
+            for (int k = 1; k < 4; ++k)
+                if (wb[k] < best || (wb[k] == best && wj[k] < bj)) { best = wb[k]; bj = wj[k]; }
+            nn[(size_t)p * Nqmax + row] = (bj == 0x7fffffff) ? 0 : bj;
+        }
+        __syncthreads();
+    }
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
 
-static int featnn_mode() {  // 1: two-pass v1, 2: one-pass v2, 3: v3, 4 (default): pipelined v4
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("PCR_FEATNN_MODE");
-        v = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 4;
+// exact f64 rescans of both directions' ambiguous lists
+static int launch_rescans(const float *F, const float *G, int Nmax, int Mmax, int D,
+                          const int32_t *n_src, const int32_t *n_tgt, const int *list12,
+                          const int *list21, const int *counts, int32_t *nn12, int32_t *nn21,
+                          hipStream_t s) {
+    PCR_REQUIRE(D <= 512, PCR_ERR_ARG, "feature_match: D=%d > 512", D);
+    const bool v4 = (D % 4) == 0 && ((uintptr_t)F & 15) == 0 && ((uintptr_t)G & 15) == 0;
+    prof_begin(s, kProfFeatRescan);
+    if (v4) {
+        hipLaunchKernelGGL(featnn_rescan2<true>, dim3(2048), dim3(256), 0, s, F, G, Nmax, Mmax, D,
+                           n_tgt, list12, counts, nn12);
+        PCR_LAUNCH_CHECK();
+        hipLaunchKernelGGL(featnn_rescan2<true>, dim3(2048), dim3(256), 0, s, G, F, Mmax, Nmax, D,
+                           n_src, list21, counts + 1, nn21);
+    } else {
+        hipLaunchKernelGGL(featnn_rescan2<false>, dim3(2048), dim3(256), 0, s, F, G, Nmax, Mmax, D,
+                           n_tgt, list12, counts, nn12);
+        PCR_LAUNCH_CHECK();
+        hipLaunchKernelGGL(featnn_rescan2<false>, dim3(2048), dim3(256), 0, s, G, F, Mmax, Nmax, D,
+                           n_src, list21, counts + 1, nn21);
     }
-    return v;
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatRescan);
+    return PCR_OK;
+}
+
+// 1: two-pass v1, 2: one-pass v2, 3: v3, 4: pipelined v4, 5: f16x3 split v5,
+// 6: v5 with phase-split wave pairs, 7 (default): v5 software-pipelined in-wave
+// (read per call: a getenv is noise next to a launch, and tests switch modes)
+static int featnn_mode() {
+    const char *e = getenv("PCR_FEATNN_MODE");
+    return (e && e[0] >= '1' && e[0] <= '7') ? e[0] - '0' : 7;
 }
 
 static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
@@ -866,12 +1804,116 @@ static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int
     hipLaunchKernelGGL(featnn_colmerge3, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, list21,
                        list_count + 1, S2a);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, F, G, Nmax, Mmax, D, n_tgt, list,
-                       list_count, nn12);
+    return launch_rescans(F, G, Nmax, Mmax, D, n_src, n_tgt, list, list21, list_count, nn12, nn21, s);
+}
+
+
+static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                            const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12,
+                            int32_t *nn21, hipStream_t s) {
+    const int NCH = cdiv(3 * D + 6, 16);
+    constexpr int G5 = 4;
+    const int mode = featnn_mode();
+    const Split5 sp = split5_params(D);
+    const int nrb = cdiv(cdiv(Nmax, 32), 8);
+    const int ntn = nrb * 8;                       // row tiles, padded to whole blocks
+    const int ntm = cdiv(cdiv(Mmax, 32), 8) * 8;   // column tiles, padded to whole groups (G | 8)
+    int ctbits = 1;
+    while ((1 << ctbits) < ntm) ++ctbits;
+    PCR_REQUIRE(ctbits <= 16, PCR_ERR_ARG, "feature_match: M=%d too large", Mmax);
+    const size_t ap = (size_t)P * ntn * NCH * 64, bp = (size_t)P * ntm * NCH * 64;  // f16x8
+    const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
+    const size_t bytes =
+        16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax));
+    char *ws = (char *)workspace(2, bytes + 256);
+    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
+    f16x8 *Ap = (f16x8 *)ws;
+    f16x8 *Bp = Ap + ap;
+    float *fnr = (float *)(Bp + bp);
+    float *gnr = fnr + nn_n;
+    // [0,P): max|y|  [P,2P): max|x|  [2P,3P): max|elem|  [3P,4P): cnt12  [4P,5P): cnt21
+    unsigned *gmax = (unsigned *)(gnr + nn_m);
+    unsigned *mx = gmax + 2 * P;
+    int *cnt12 = (int *)(gmax + 3 * P);
+    int *cnt21 = cnt12 + P;
+    int *list12 = cnt21 + P;                  // per pair, stride Nmax
+    int *list21 = list12 + (size_t)P * Nmax;  // per pair, stride Mmax
+    PCR_HIP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned) * 5 * P, s));
+    prof_begin(s, kProfFeatPack);
+    hipLaunchKernelGGL(feat_maxabs, dim3(cdiv((long long)Nmax * D, 256 * 16), P), dim3(256), 0, s, F,
+                       n_src, Nmax, D, mx);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, G, F, Mmax, Nmax, D, n_src,
-                       list21, list_count + 1, nn21);
+    hipLaunchKernelGGL(feat_maxabs, dim3(cdiv((long long)Mmax * D, 256 * 16), P), dim3(256), 0, s, G,
+                       n_tgt, Mmax, D, mx);
     PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D, NCH,
+                       ntn, 0, sp, mx, Ap, fnr, gmax + P);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax, D, NCH,
+                       ntm, 1, sp, mx, Bp, gnr, gmax);
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatPack);
+    DualArgs5 d;
+    d.Ap = Ap; d.Bp = Bp; d.fnr = fnr; d.gnr = gnr; d.fmax = gmax + P; d.gmax = gmax;
+    d.n_src = n_src; d.n_tgt = n_tgt; d.P = P; d.Nmax = Nmax; d.Mmax = Mmax; d.ntn = ntn;
+    d.ntm = ntm; d.nrb = nrb; d.D = D; d.ctbits = ctbits; d.nn12 = nn12; d.list12 = list12;
+    d.count12 = cnt12;
+    const size_t cpn = (size_t)P * nrb * ntm * 32;
+    char *cw = (char *)workspace(11, cpn * 12 + 64);
+    PCR_REQUIRE(cw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
+    d.cp1 = (float *)cw;
+    d.cp2 = d.cp1 + cpn;
+    d.cpi = (int *)(d.cp2 + cpn);
+    const long long nblk = 8LL * nrb * cdiv(P, 8);  // XCD-aware 1-D grid
+    PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_match: grid too large");
+    prof_begin(s, kProfFeatScreen);
+    const bool v6 = mode == 6, v7 = mode == 7;
+    const char *abl = getenv("PCR_FEATNN_ABL");
+    if (abl && NCH == 7 && abl[0] >= '1' && abl[0] <= '3') {  // debug ablations: screen only
+        const dim3 gr((unsigned)nblk), bl(512);
+        if (abl[0] == '1') hipLaunchKernelGGL((featnn_dual5<7, G5, 1>), gr, bl, 0, s, d);
+        if (abl[0] == '2') hipLaunchKernelGGL((featnn_dual5<7, G5, 2>), gr, bl, 0, s, d);
+        if (abl[0] == '3') hipLaunchKernelGGL((featnn_dual5<7, G5, 3>), gr, bl, 0, s, d);
+        PCR_LAUNCH_CHECK();
+        prof_end(s, kProfFeatScreen);
+        return PCR_OK;
+    }
+    switch (NCH) {
+#define PCR_D5CASE(K)                                                                             \
+    case K:                                                                                       \
+        if (v7) hipLaunchKernelGGL((featnn_dual7<K, (K <= 7 ? 8 : 4)>), dim3((unsigned)nblk),      \
+                                   dim3(512), 0, s, d);                                           \
+        else if (v6) hipLaunchKernelGGL((featnn_dual6<K, G5>), dim3((unsigned)nblk), dim3(512), 0, s, d); \
+        else hipLaunchKernelGGL((featnn_dual5<K, G5>), dim3((unsigned)nblk), dim3(512), 0, s, d);    \
+        break;
+        PCR_D5CASE(1) PCR_D5CASE(2) PCR_D5CASE(3) PCR_D5CASE(4) PCR_D5CASE(5) PCR_D5CASE(6)
+        PCR_D5CASE(7) PCR_D5CASE(8) PCR_D5CASE(9) PCR_D5CASE(10) PCR_D5CASE(11) PCR_D5CASE(12)
+        PCR_D5CASE(13)
+#undef PCR_D5CASE
+        default: set_error("feature dim too large for v5"); return PCR_ERR_ARG;
+    }
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatScreen);
+    hipLaunchKernelGGL(featnn_colmerge5, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, list21,
+                       cnt21, 16 * NCH);
+    PCR_LAUNCH_CHECK();
+    RescanArgs5 ra;
+    ra.F = F; ra.G = G; ra.n_src = n_src; ra.n_tgt = n_tgt; ra.Nmax = Nmax; ra.Mmax = Mmax;
+    ra.D = D; ra.list12 = list12; ra.list21 = list21; ra.cnt12 = cnt12; ra.cnt21 = cnt21;
+    ra.nn12 = nn12; ra.nn21 = nn21;
+    const bool v4 = (D % 4) == 0 && ((uintptr_t)F & 15) == 0 && ((uintptr_t)G & 15) == 0;
+    const dim3 rg(P, 2);
+    prof_begin(s, kProfFeatRescan);
+    const int dv = cdiv(D, 16) * 16;
+#define PCR_R3(DVV)                                                                    \
+    if (dv == DVV) {                                                                    \
+        if (v4) hipLaunchKernelGGL((featnn_rescan3<DVV, true>), rg, dim3(256), 0, s, ra); \
+        else hipLaunchKernelGGL((featnn_rescan3<DVV, false>), rg, dim3(256), 0, s, ra);  \
+    }
+    PCR_R3(16) PCR_R3(32) PCR_R3(48) PCR_R3(64)
+#undef PCR_R3
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatRescan);
     return PCR_OK;
 }
 
@@ -908,6 +1950,8 @@ int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax
                        hipStream_t s) {
     const int KCH = cdiv(D, 16);
     PCR_REQUIRE(D >= 1 && KCH <= 8, PCR_ERR_ARG, "feature_match: D=%d unsupported (1..128)", D);
+    if (featnn_mode() >= 5 && D <= 64)
+        return feature_match_v5(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
     if (featnn_mode() >= 3)
         return feature_match_v3(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
     const int S2 = 8 * KCH;
@@ -970,13 +2014,7 @@ int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax
     hipLaunchKernelGGL(featnn_colmerge, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, list21,
                        list_count + 1, S2);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, F, G, Nmax, Mmax, D, n_tgt, list,
-                       list_count, nn12);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, G, F, Mmax, Nmax, D, n_src,
-                       list21, list_count + 1, nn21);
-    PCR_LAUNCH_CHECK();
-    return PCR_OK;
+    return launch_rescans(F, G, Nmax, Mmax, D, n_src, n_tgt, list, list21, list_count, nn12, nn21, s);
 }
 
 int corres_impl(const int32_t *nn12, const int32_t *nn21, const int32_t *n_src,
@@ -1015,4 +2053,18 @@ extern "C" int pcr_correspondences(const int32_t *nn12, const int32_t *nn21, int
     PCR_REQUIRE(nn12 && nn21 && corres && n_corres, PCR_ERR_ARG, "correspondences: null pointer");
     return pcr::corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, Mmax, mutual_filter, ransac_n,
                             corres, n_corres, pcr::as_stream(stream));
+}
+
+extern "C" int pcr_featnn_rescan_rows(int64_t *rows12, int64_t *rows21, int32_t reset) {
+    pcr::clear_error();
+    unsigned long long v[2] = {0, 0};
+    PCR_HIP_CHECK(hipDeviceSynchronize());
+    PCR_HIP_CHECK(hipMemcpyFromSymbol(v, HIP_SYMBOL(pcr::g_featnn_rescan_rows), sizeof(v)));
+    if (rows12) *rows12 = (int64_t)v[0];
+    if (rows21) *rows21 = (int64_t)v[1];
+    if (reset) {
+        const unsigned long long z[2] = {0, 0};
+        PCR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pcr::g_featnn_rescan_rows), z, sizeof(z)));
+    }
+    return PCR_OK;
 }

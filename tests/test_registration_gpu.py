@@ -208,3 +208,59 @@ def test_procrustes_bitexact_vs_oracle(oracle):
     for absw, eps in ((0, 1e-8), (1, 1e-4)):
         T = pr.procrustes_batch(src, tgt, w, absw, eps)
         assert _bits_equal(_np(T), oracle.procrustes_batch(src, tgt, w, absw, eps))
+
+
+def _stress_cases():
+    rng = np.random.default_rng(77)
+    cases = {}
+    # per-dimension magnitudes over 9 decades
+    sc = (10.0 ** rng.uniform(-6, 3, 32)).astype(np.float32)
+    cases["dynamic_range"] = ((rng.standard_normal((900, 32)) * sc).astype(np.float32),
+                              (rng.standard_normal((1000, 32)) * sc).astype(np.float32))
+    # far from the origin, tiny spread: nearly every row is ambiguous -> rescan
+    base = rng.standard_normal(32).astype(np.float32) * 1000
+    cases["offset"] = ((base + rng.standard_normal((600, 32)) * 1e-3).astype(np.float32),
+                       (base + rng.standard_normal((700, 32)) * 1e-3).astype(np.float32))
+    # zero rows and repeated rows
+    a = rng.standard_normal((500, 32)).astype(np.float32)
+    a[::7] = 0
+    b = rng.standard_normal((450, 32)).astype(np.float32)
+    b[::5] = 0
+    b[1::9] = a[3]
+    cases["zeros_repeats"] = (a, b)
+    cases["d1"] = (rng.standard_normal((513, 1)).astype(np.float32),
+                   rng.standard_normal((300, 1)).astype(np.float32))
+    cases["d100_fallback"] = (rng.standard_normal((400, 100)).astype(np.float32),
+                              rng.standard_normal((333, 100)).astype(np.float32))
+    cases["subnormal"] = ((rng.standard_normal((300, 16)) * 1e-39).astype(np.float32),
+                          (rng.standard_normal((280, 16)) * 1e-39).astype(np.float32))
+    a = rng.standard_normal((400, 32)).astype(np.float32)
+    b = rng.standard_normal((380, 32)).astype(np.float32)
+    a[5, 3] = np.nan                  # NaN query row: every distance NaN -> index 0
+    b[[7, 100], 0] = np.nan           # NaN candidates never win (strict <)
+    cases["nan_rows"] = (a, b)
+    return cases
+
+
+@pytest.mark.parametrize("name", list(_stress_cases()))
+@pytest.mark.parametrize("mode", ["7", "6", "5", "3"])
+def test_feature_match_stress_vs_oracle(oracle, monkeypatch, name, mode):
+    """Screen + certification + rescan stay exact on adversarial descriptors
+    for the f16x3 split screen (mode 5, default) and the f32 screen (mode 3)."""
+    monkeypatch.setenv("PCR_FEATNN_MODE", mode)
+    fs, ft = _stress_cases()[name]
+    nn12, nn21 = reg.feature_match(fs[None], ft[None])
+    assert np.array_equal(_np(nn12)[0], oracle.featnn(fs, ft))
+    assert np.array_equal(_np(nn21)[0], oracle.featnn(ft, fs))
+
+
+def test_feature_match_many_pairs_xcd_mapping(oracle):
+    """P not a multiple of 8 exercises the XCD-aware block->pair map's idle blocks."""
+    P, N, M, D = 11, 300, 260, 32
+    rng = np.random.default_rng(11)
+    fs = rng.standard_normal((P, N, D)).astype(np.float32)
+    ft = rng.standard_normal((P, M, D)).astype(np.float32)
+    nn12, nn21 = reg.feature_match(fs, ft)
+    for p in range(P):
+        assert np.array_equal(_np(nn12)[p], oracle.featnn(fs[p], ft[p]))
+        assert np.array_equal(_np(nn21)[p], oracle.featnn(ft[p], fs[p]))
