@@ -183,6 +183,28 @@ int pcr_procrustes_batch(const float *src, const float *tgt, const float *weight
                          int32_t N, int32_t abs_weights, double eps, double *T,
                          pcr_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * a4 -- DIP local reference frames, batched.  Replaces lrf.get
+ * (dip/lrf.py:19-78) called per sampled point by dip/demo.py:109-114.
+ * Two phases so the reference's np.random.choice stream stays on the host:
+ *   pcr_lrf_count   -> counts (P,Qmax): radius neighbours of each query
+ *                      (d^2 < float(kernel^2), incl. the first hit);
+ *   host            -> inds (P,Qmax,patch_size) = np.random.choice(
+ *                      max(count, patch_size), patch_size, replace=False);
+ *   pcr_lrf_compute -> patches (P,Qmax,patch_size,3) f64 (lRg^T (p - pt) /
+ *                      kernel, zero rows past the count) and T (P,Qmax,16) f64
+ *                      row-major [[xp yp zp | pt],[0 0 0 1]] (det -1, as the
+ *                      reference).  max_count >= every count, <= 8192.
+ * Points/queries f64 (Open3D stores double).  counts may be NULL in phase 2.
+ * ------------------------------------------------------------------------- */
+int pcr_lrf_count(const double *pts, int32_t P, int32_t Nmax, const int32_t *n_pts,
+                  const double *queries, int32_t Qmax, const int32_t *n_q, double kernel,
+                  int32_t *counts, pcr_stream_t stream);
+int pcr_lrf_compute(const double *pts, int32_t P, int32_t Nmax, const int32_t *n_pts,
+                    const double *queries, int32_t Qmax, const int32_t *n_q, double kernel,
+                    int32_t patch_size, const int32_t *inds, int32_t max_count,
+                    double *patches, double *T, int32_t *counts, pcr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

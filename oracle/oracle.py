@@ -93,6 +93,11 @@ def _setup_sigs():
     L.oracle_corres.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
     L.oracle_philox.argtypes = [c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     L.oracle_horn_rotation.argtypes = [c.c_void_p, c.c_void_p]
+    L.oracle_lrf_count.restype = c.c_int
+    L.oracle_lrf_count.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_double]
+    L.oracle_lrf.restype = c.c_int
+    L.oracle_lrf.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_double, c.c_int, c.c_void_p,
+                             c.c_void_p, c.c_void_p]
     return L
 
 
@@ -192,3 +197,20 @@ def icp(src, tgt, max_corr_dist, init=None, max_iteration=30, relative_fitness=1
                         float(max_corr_dist), int(max_iteration), float(relative_fitness),
                         float(relative_rmse), _p(T), _p(fr), _p(it))
     return dict(T=T.reshape(4, 4), fitness=fr[0], inlier_rmse=fr[1], n_corr=nc, iters=int(it[0]))
+
+
+def lrf_count(pts, q, kernel):
+    """Radius-neighbour count of lrf.get (dip/lrf.py:21), incl. the first hit."""
+    pts, q = _f64(pts), _f64(q)
+    return int(L().oracle_lrf_count(_p(pts), len(pts), _p(q), float(kernel)))
+
+
+def lrf(pts, q, kernel, patch_size, inds):
+    """dip/lrf.py:19-78 with the caller's choice indices: (k, patch (ps,3), T (4,4))."""
+    pts, q = _f64(pts), _f64(q)
+    inds = _i32(inds)
+    patch = np.zeros((patch_size, 3), np.float64)
+    T = np.zeros(16, np.float64)
+    k = L().oracle_lrf(_p(pts), len(pts), _p(q), float(kernel), int(patch_size), _p(inds),
+                       _p(patch), _p(T))
+    return int(k), patch, T.reshape(4, 4)

@@ -775,3 +775,158 @@ int oracle_icp(const float *srcf, int n, const float *tgtf, int m, const double 
     free(P); free(Tg); free(cj);
     return cnt;
 }
+
+/* ------------------------------------------------------------------------- */
+/* a4: DIP local reference frame, dip/lrf.py:19-78 (lrf.get).                 */
+/*  - radius neighbours of pt: d2 = ((dx^2 + dy^2) + dz^2) < (double)(float)   */
+/*    (r*r) (Open3D KDTreeFlann::SearchRadius passes float(r*r) to FLANN,     */
+/*    strict <), sorted by (d2, index) (:21);                                  */
+/*  - ptnn = all but the first (:23); cov = 1/len(ptnn) * A A^T where          */
+/*    len(ptnn) == 3 (the array is 3 x k) (:27);                               */
+/*  - np_hat = eigenvector of the smallest eigenvalue (:33-35), here cyclic    */
+/*    Jacobi (first index on ties), normalised;                                */
+/*  - zp sign (:38), xp from the alpha*beta weighted projections (:40-46),     */
+/*    yp = xp x zp (:48), T = [[xp yp zp | pt]] (:50-61; det = -1);            */
+/*  - patch rows lRg^T (p - pt) / kernel over ptall (incl. the first), zero    */
+/*    padded to patch_size, rows picked by the caller's inds (:53-76; the      */
+/*    np.random.choice draw stays with the caller).                            */
+/* Sums use det_sum's 256-lane order so the GPU kernel matches bit for bit.   */
+/* ------------------------------------------------------------------------- */
+typedef struct { double d2; int idx; } lrf_hit;
+
+static int cmp_hit(const void *a, const void *b)
+{
+    const lrf_hit *x = (const lrf_hit *)a, *y = (const lrf_hit *)b;
+    if (x->d2 < y->d2) return -1;
+    if (x->d2 > y->d2) return 1;
+    return (x->idx > y->idx) - (x->idx < y->idx);
+}
+
+static void sym3_smallest(const double C[6], double v[3])
+{
+    /* C = xx xy xz yy yz zz; cyclic Jacobi, + - * / sqrt only */
+    double A[3][3] = {{C[0], C[1], C[2]}, {C[1], C[3], C[4]}, {C[2], C[4], C[5]}};
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 32; sweep++) {
+        const double off = (A[0][1] * A[0][1] + A[0][2] * A[0][2]) + A[1][2] * A[1][2];
+        if (off == 0.0) break;
+        for (int p = 0; p < 2; p++)
+            for (int r = p + 1; r < 3; r++) {
+                const double apr = A[p][r];
+                if (apr == 0.0) continue;
+                const double theta = (A[r][r] - A[p][p]) / (2.0 * apr);
+                double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                if (theta < 0.0) t = -t;
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                A[p][p] = A[p][p] - t * apr;
+                A[r][r] = A[r][r] + t * apr;
+                A[p][r] = 0.0;
+                A[r][p] = 0.0;
+                for (int k = 0; k < 3; k++) {
+                    if (k == p || k == r) continue;
+                    const double akp = A[k][p], akr = A[k][r];
+                    A[k][p] = c * akp - s * akr;
+                    A[p][k] = A[k][p];
+                    A[k][r] = s * akp + c * akr;
+                    A[r][k] = A[k][r];
+                }
+                for (int k = 0; k < 3; k++) {
+                    const double vkp = V[k][p], vkr = V[k][r];
+                    V[k][p] = c * vkp - s * vkr;
+                    V[k][r] = s * vkp + c * vkr;
+                }
+            }
+    }
+    int m = 0;
+    for (int k = 1; k < 3; k++)
+        if (A[k][k] < A[m][m]) m = k;
+    const double n = sqrt((V[0][m] * V[0][m] + V[1][m] * V[1][m]) + V[2][m] * V[2][m]);
+    for (int k = 0; k < 3; k++) v[k] = V[k][m] / n;
+}
+
+static int lrf_hits(const double *pts, int n, const double q[3], double kernel, lrf_hit *h)
+{
+    const double thr = (double)(float)(kernel * kernel);
+    int k = 0;
+    for (int i = 0; i < n; i++) {
+        const double dx = pts[3 * i] - q[0], dy = pts[3 * i + 1] - q[1], dz = pts[3 * i + 2] - q[2];
+        const double d2 = (dx * dx + dy * dy) + dz * dz;
+        if (d2 < thr) { if (h) { h[k].d2 = d2; h[k].idx = i; } k++; }
+    }
+    return k;
+}
+
+int oracle_lrf_count(const double *pts, int n, const double q[3], double kernel)
+{
+    return lrf_hits(pts, n, q, kernel, NULL);
+}
+
+/* returns k; fills T (16, row-major 4x4) and patch (patch_size x 3) */
+int oracle_lrf(const double *pts, int n, const double q[3], double kernel, int patch_size,
+               const int32_t *inds, double *patch, double *T)
+{
+    lrf_hit *h = (lrf_hit *)malloc(sizeof(lrf_hit) * (size_t)(n > 0 ? n : 1));
+    const int k = lrf_hits(pts, n, q, kernel, h);
+    qsort(h, (size_t)k, sizeof(lrf_hit), cmp_hit);
+    const int kn = k > 0 ? k - 1 : 0; /* ptnn = hits[1:] */
+    double *v = (double *)malloc(sizeof(double) * (size_t)(kn > 0 ? kn : 1));
+    double C[6];
+    const int ca[6] = {0, 0, 0, 1, 1, 2}, cb[6] = {0, 1, 2, 1, 2, 2};
+    for (int e = 0; e < 6; e++) {
+        for (int i = 0; i < kn; i++) {
+            const double *p = pts + 3 * h[i + 1].idx;
+            v[i] = (p[ca[e]] - q[ca[e]]) * (p[cb[e]] - q[cb[e]]);
+        }
+        C[e] = (1.0 / 3.0) * det_sum(v, NULL, kn);
+    }
+    double nh[3];
+    sym3_smallest(C, nh);
+    for (int i = 0; i < kn; i++) {
+        const double *p = pts + 3 * h[i + 1].idx;
+        v[i] = (nh[0] * (q[0] - p[0]) + nh[1] * (q[1] - p[1])) + nh[2] * (q[2] - p[2]);
+    }
+    const double zs = det_sum(v, NULL, kn);
+    double zp[3];
+    for (int c = 0; c < 3; c++) zp[c] = zs > 0.0 ? nh[c] : -nh[c];
+    double xs[3];
+    for (int c = 0; c < 3; c++) {
+        for (int i = 0; i < kn; i++) {
+            const double *p = pts + 3 * h[i + 1].idx;
+            const double dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
+            const double proj = (dx * zp[0] + dy * zp[1]) + dz * zp[2];
+            const double dc = c == 0 ? dx : (c == 1 ? dy : dz);
+            const double vc = dc - proj * zp[c];
+            const double ex = q[0] - p[0], ey = q[1] - p[1], ez = q[2] - p[2];
+            const double nr = sqrt((ex * ex + ey * ey) + ez * ez);
+            const double al = (kernel - nr) * (kernel - nr);
+            const double be = proj * proj;
+            v[i] = vc * (al * be);
+        }
+        xs[c] = det_sum(v, NULL, kn);
+    }
+    const double xn = 1.0 / sqrt((xs[0] * xs[0] + xs[1] * xs[1]) + xs[2] * xs[2]);
+    double xp[3], yp[3];
+    for (int c = 0; c < 3; c++) xp[c] = xn * xs[c];
+    yp[0] = xp[1] * zp[2] - xp[2] * zp[1];
+    yp[1] = xp[2] * zp[0] - xp[0] * zp[2];
+    yp[2] = xp[0] * zp[1] - xp[1] * zp[0];
+    for (int a = 0; a < 3; a++) {
+        T[4 * a + 0] = xp[a];
+        T[4 * a + 1] = yp[a];
+        T[4 * a + 2] = zp[a];
+        T[4 * a + 3] = q[a];
+    }
+    T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
+    for (int i = 0; i < patch_size; i++) {
+        const int s = inds[i];
+        if (s < 0 || s >= k) { patch[3 * i] = 0.0; patch[3 * i + 1] = 0.0; patch[3 * i + 2] = 0.0; continue; }
+        const double *p = pts + 3 * h[s].idx;
+        const double dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
+        patch[3 * i + 0] = ((xp[0] * dx + xp[1] * dy) + xp[2] * dz) / kernel;
+        patch[3 * i + 1] = ((yp[0] * dx + yp[1] * dy) + yp[2] * dz) / kernel;
+        patch[3 * i + 2] = ((zp[0] * dx + zp[1] * dy) + zp[2] * dz) / kernel;
+    }
+    free(v);
+    free(h);
+    return k;
+}
