@@ -205,6 +205,29 @@ int pcr_lrf_compute(const double *pts, int32_t P, int32_t Nmax, const int32_t *n
                     int32_t patch_size, const int32_t *inds, int32_t max_count,
                     double *patches, double *T, int32_t *counts, pcr_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * a10 -- NDP deformation-pyramid warp, all levels in one launch.  Replaces
+ * Deformation_Pyramid.warp (c2p-net/deformationpyramid/model/nets.py:36-48)
+ * over NDPLayer.forward (:111-140) with motion "SE3", rotation "axis_angle"
+ * (the C5 configuration, config/NDP.yaml).  Weights in nn.Linear layout
+ * (out, in) f32, device pointers; w_hid holds the depth-1 MLP layers
+ * contiguously; w_nr/b_nr NULL for levels without the nonrigidity branch.
+ * levels is a HOST array of n_levels (<= 16) entries.  x_levels (n_levels,N,3)
+ * and nonrigidity (n_levels,N) are optional per-level outputs (data[i]).
+ * ------------------------------------------------------------------------- */
+typedef struct pcr_ndp_level {
+    const float *w_in, *b_in;   /* (W,6), (W) */
+    const float *w_hid, *b_hid; /* (depth-1,W,W), (depth-1,W) */
+    const float *w_rot, *b_rot; /* (3,W), (3) */
+    const float *w_trn, *b_trn; /* (3,W), (3) */
+    const float *w_nr, *b_nr;   /* (1,W), (1) or NULL */
+    int32_t m;                  /* level index + 1: omega = 2^(m + k0) */
+    int32_t reserved;
+} pcr_ndp_level;
+int pcr_ndp_warp(const float *x, int32_t N, const pcr_ndp_level *levels, int32_t n_levels,
+                 int32_t width, int32_t depth, int32_t k0, float *x_out, float *x_levels,
+                 float *nonrigidity, pcr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -214,3 +214,51 @@ def lrf(pts, q, kernel, patch_size, inds):
     k = L().oracle_lrf(_p(pts), len(pts), _p(q), float(kernel), int(patch_size), _p(inds),
                        _p(patch), _p(T))
     return int(k), patch, T.reshape(4, 4)
+
+
+# ---------------------------------------------------------------------------
+# a10: NDP per-level warp, numpy f64 restatement of
+# c2p-net/deformationpyramid/model/nets.py NDPLayer.forward (:111-140),
+# posenc (:164-177), get_Rotation axis_angle (:144-161) -> rigid_body.exp_so3 /
+# skew (:89-95, :113-119), MLP (:295-304), Deformation_Pyramid.warp (:36-48).
+# Floating point: the GPU (f32) is held to 1e-5 of it (north_star tolerance).
+# ---------------------------------------------------------------------------
+def ndp_level(p, x, m, k0):
+    """One NDPLayer (SE3, axis_angle). p: dict of the layer's state_dict arrays."""
+    x = np.asarray(x, np.float64)
+    w = float(2.0 ** (m + k0))
+    pe = np.concatenate([np.sin(x[:, 0:1] * w), np.cos(x[:, 0:1] * w),
+                         np.sin(x[:, 1:2] * w), np.cos(x[:, 1:2] * w),
+                         np.sin(x[:, 2:3] * w), np.cos(x[:, 2:3] * w)], axis=1)
+    f = lambda k: np.asarray(p[k], np.float64)  # noqa: E731
+    h = np.maximum(pe @ f("input.0.weight").T + f("input.0.bias"), 0.0)
+    i = 0
+    while f"mlp.pts_linears.{i}.weight" in p:
+        h = np.maximum(h @ f(f"mlp.pts_linears.{i}.weight").T + f(f"mlp.pts_linears.{i}.bias"), 0.0)
+        i += 1
+    t = 0.001 * (h @ f("trn_branch.weight").T + f("trn_branch.bias"))
+    r = 0.001 * (h @ f("rot_brach.weight").T + f("rot_brach.bias"))
+    th = np.linalg.norm(r, axis=-1, keepdims=True)
+    wv = r / th
+    z = np.zeros(len(x))
+    K = np.stack([z, -wv[:, 2], wv[:, 1], wv[:, 2], z, -wv[:, 0], -wv[:, 1], wv[:, 0], z],
+                 -1).reshape(-1, 3, 3)
+    R = np.eye(3)[None] + np.sin(th)[..., None] * K + (1 - np.cos(th))[..., None] * (K @ K)
+    xn = (R @ x[..., None])[..., 0] + t
+    nr = None
+    if "nr_branch.weight" in p:
+        s = 1.0 / (1.0 + np.exp(-(0.001 * (h @ f("nr_branch.weight").T + f("nr_branch.bias")))))
+        xn = x + s * (xn - x)
+        nr = s[:, 0]
+    return xn, nr
+
+
+def ndp_warp(levels, x, k0=-8, max_level=None, min_level=0):
+    """Deformation_Pyramid.warp: levels[i] is level i's state dict (m = i + 1)."""
+    if max_level is None:
+        max_level = len(levels) - 1
+    data = {}
+    for i in range(min_level, max_level + 1):
+        x, nr = ndp_level(levels[i], x, i + 1, k0)
+        data[i] = (x, nr)
+    return x, data

@@ -65,6 +65,7 @@ SIGNATURES = {
     "pcr_procrustes_batch": [_p, _p, _p, _i32, _i32, _i32, _f64, _p, _p],
     "pcr_lrf_count": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _p, _p],
     "pcr_lrf_compute": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _i32, _p, _i32, _p, _p, _p, _p],
+    "pcr_ndp_warp": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
 }
 
 
