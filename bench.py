@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--feat-noise", type=float, default=1.0)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the a4 (LRF) / a10 (NDP warp) side measurements")
     return ap.parse_args()
 
 
@@ -102,6 +104,116 @@ def cpu_baseline(batch, params, budget_s):
                        f"{batch.src_feat.shape[2]}) through the oracle pipeline in {el:.1f}s; "
                        f"feature-NN on {threads} OpenMP threads, RANSAC/ICP/Chamfer 1 thread"},
             Ts)
+
+
+def _events_ms(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def measure_lrf(with_cpu):
+    """a4 on the C3 shape (dip/demo.py: 2 clouds, 2048 sampled points each,
+    kernel 3*sqrt(3), patch 256): synthetic surface clouds of 20k points scaled
+    to ~170 neighbours per ball.  GPU time = both phases (count + frames) for
+    4096 queries; the host choice draws are timed separately."""
+    from pointcloudregistration_amd import _lib, synth
+    from pointcloudregistration_amd import lrf as L
+    rng = np.random.default_rng(77)
+    clouds = np.stack([synth.surface_points(rng, 20000) * 40.0 for _ in range(2)])
+    qidx = np.stack([rng.choice(20000, 2048, replace=False) for _ in range(2)])
+    qs = np.stack([clouds[p][qidx[p]] for p in range(2)])
+    ker, ps = 3.0 * np.sqrt(3.0), 256
+    P_ = torch.as_tensor(clouds, device="cuda").contiguous()
+    Q_ = torch.as_tensor(qs, device="cuda").contiguous()
+    counts = torch.zeros(2, 2048, dtype=torch.int32, device="cuda")
+    st = _lib.stream_handle()
+    _lib.call("pcr_lrf_count", _lib.ptr(P_), 2, 20000, None, _lib.ptr(Q_), 2048, None, ker,
+              _lib.ptr(counts), st)
+    cnt = counts.cpu().numpy()
+    t0 = time.perf_counter()
+    inds = np.stack([np.stack([np.random.choice(max(int(c), ps), ps, replace=False)
+                               for c in cnt[p]]) for p in range(2)]).astype(np.int32)
+    host_ms = (time.perf_counter() - t0) * 1e3
+    I_ = torch.as_tensor(inds, device="cuda").contiguous()
+    patches = torch.empty(2, 2048, ps, 3, dtype=torch.float64, device="cuda")
+    T = torch.empty(2, 2048, 16, dtype=torch.float64, device="cuda")
+    kmax = int(cnt.max())
+
+    def run():
+        _lib.call("pcr_lrf_count", _lib.ptr(P_), 2, 20000, None, _lib.ptr(Q_), 2048, None, ker,
+                  _lib.ptr(counts), st)
+        _lib.call("pcr_lrf_compute", _lib.ptr(P_), 2, 20000, None, _lib.ptr(Q_), 2048, None, ker,
+                  ps, _lib.ptr(I_), kmax, _lib.ptr(patches), _lib.ptr(T), None, st)
+    ms = _events_ms(run, 5)
+    # algorithmic work: two f64 sweeps of the cloud per query (3 sub, 3 mul, 2 add)
+    flops = 4096 * 2 * 20000 * 8.0
+    res = {"workload": "C3 DIP: 2 clouds x 20000 pts, 2 x 2048 queries, kernel 3*sqrt(3), patch 256",
+           "gpu_ms": ms, "queries_per_s": 4096 / (ms * 1e-3), "host_choice_ms": host_ms,
+           "median_neighbours": float(np.median(cnt)),
+           "roofline": {"bound": "valu-f64", "achieved_tflops": flops / (ms * 1e-3) / 1e12,
+                        "peak_tflops": 78.6, "note": "brute-force f64 sweeps; cloud is L2-resident"}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        t0 = time.perf_counter()
+        n = 64
+        for i in range(n):
+            O.lrf(clouds[0], qs[0][i], ker, ps, inds[0][i])
+        cpu_ms = (time.perf_counter() - t0) * 1e3 / n
+        res["cpu_baseline"] = {"ms_per_query": cpu_ms, "cores": 1, "kind": "port",
+                               "sample": f"{n} queries through oracle_lrf (brute-force radius)",
+                               "reference_measured_ms_per_query": 0.47}
+    return res
+
+
+def measure_ndp(with_cpu):
+    """a10 on the C5 shape (config/NDP.yaml: width 128, depth 3, m 9 levels,
+    k0 -8, SE3 axis_angle, nonrigidity on levels > 0) over 20000 points."""
+    from pointcloudregistration_amd import ndp
+    rng = np.random.default_rng(5)
+    W, n = 128, 20000
+    levels = []
+    for i in range(9):
+        sd = {"input.0.weight": rng.normal(0, 0.5, (W, 6)), "input.0.bias": rng.normal(0, .1, W)}
+        for k in range(2):
+            sd[f"mlp.pts_linears.{k}.weight"] = rng.normal(0, 1 / np.sqrt(W), (W, W))
+            sd[f"mlp.pts_linears.{k}.bias"] = rng.normal(0, .1, W)
+        for b in ("rot_brach", "trn_branch"):
+            sd[f"{b}.weight"] = rng.normal(0, 1, (3, W))
+            sd[f"{b}.bias"] = rng.normal(0, .1, 3)
+        if i > 0:
+            sd["nr_branch.weight"] = rng.normal(0, 1, (1, W))
+            sd["nr_branch.bias"] = rng.normal(0, .1, 1)
+        levels.append({k: torch.as_tensor(v.astype(np.float32), device="cuda")
+                       for k, v in sd.items()})
+    x = torch.as_tensor(rng.uniform(-1, 1, (n, 3)).astype(np.float32), device="cuda")
+    ms = _events_ms(lambda: ndp.warp(levels, x), 10)
+    flops = n * 9 * 2.0 * (6 * W + 2 * W * W + 7 * W)
+    res = {"workload": "C5 NDP warp: 20000 pts x 9 levels, width 128, depth 3 (random init)",
+           "gpu_ms": ms, "point_levels_per_s": n * 9 / (ms * 1e-3),
+           "roofline": {"bound": "mfma", "achieved": flops / (ms * 1e-3) / 1e12,
+                        "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": flops / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS,
+                        "kernel": "ndp_warp_kernel<4> (v_mfma_f32_32x32x2_f32)"}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        lv = [{k: v.cpu().numpy() for k, v in L.items()} for L in levels]
+        xc = x.cpu().numpy()
+        t0 = time.perf_counter()
+        O.ndp_warp(lv, xc)
+        res["cpu_baseline"] = {"ms": (time.perf_counter() - t0) * 1e3,
+                               "cores": int(os.environ.get("OMP_NUM_THREADS", "1")),
+                               "kind": "port", "sample": "numpy f64 oracle, the full warp",
+                               "reference_measured_ms": 137.0}
+    return res
 
 
 def main():
@@ -220,6 +332,9 @@ def main():
                                          "T_icp_bitexact": bool(same_i),
                                          "rre_deg_max": float(np.max(d_rre)),
                                          "rte_max": float(np.max(d_rte))}
+    if rank == 0 and world == 1 and not args.no_secondary:
+        out["secondary"] = {"a4_lrf": measure_lrf(not args.no_cpu_baseline),
+                            "a10_ndp_warp": measure_ndp(not args.no_cpu_baseline)}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
