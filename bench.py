@@ -194,7 +194,8 @@ def measure_ndp(with_cpu):
         levels.append({k: torch.as_tensor(v.astype(np.float32), device="cuda")
                        for k, v in sd.items()})
     x = torch.as_tensor(rng.uniform(-1, 1, (n, 3)).astype(np.float32), device="cuda")
-    ms = _events_ms(lambda: ndp.warp(levels, x), 10)
+    pyr = ndp.PreparedPyramid(levels)
+    ms = _events_ms(lambda: pyr.warp(x, per_level=False), 10)
     flops = n * 9 * 2.0 * (6 * W + 2 * W * W + 7 * W)
     res = {"workload": "C5 NDP warp: 20000 pts x 9 levels, width 128, depth 3 (random init)",
            "gpu_ms": ms, "point_levels_per_s": n * 9 / (ms * 1e-3),

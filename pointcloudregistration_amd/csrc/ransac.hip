@@ -25,6 +25,10 @@
 #include "pcr_internal.h"
 #include "geom.h"
 #include "grid.h"
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 namespace pcr {
 namespace {
@@ -48,6 +52,7 @@ struct RArgs {
     int32_t *stats, *corr_tgt;
     uint32_t *mask;
     int words;
+    unsigned long long *timing;  // debug (PCR_RANSAC_TIMING): per pair, 6 phase clocks
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -151,6 +156,9 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
         else gg = a.grid.view(p);
     }
     __syncthreads();
+    unsigned long long tm_hyp = 0, tm_val = 0, tm0 = 0, tm_a = 0;
+    const bool tmg = a.timing != nullptr && tid == 0;
+    if (tmg) tm0 = tm_a = __builtin_readcyclecounter();
     const double scale = fx_scale(a.thr);
     while (ok) {
         const int base = sh.base;
@@ -176,6 +184,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
             sh.listItr[pos] = itr;
         }
         __syncthreads();
+        if (tmg) { const unsigned long long t = __builtin_readcyclecounter(); tm_hyp += t - tm_a; tm_a = t; }
         const int nlist = min(total, kCap);
         const int next_base = total > kCap ? sh.listItr[kCap - 1] + 1 : base + kThreads;
         for (int e = 0; e < nlist; ++e) {
@@ -231,6 +240,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
         }
         if (tid == 0) sh.base = next_base;
         __syncthreads();
+        if (tmg) { const unsigned long long t = __builtin_readcyclecounter(); tm_val += t - tm_a; tm_a = t; }
     }
     // loop exit iteration of the sequential algorithm: first itr >= est_k after the
     // last bound update (or max_iter)
@@ -276,6 +286,12 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
         st[2] = ok ? sh.best_itr : -1;
         st[3] = ok ? (found ? 1 : 0) : -1;
         st[4] = C;
+        if (a.timing) {
+            unsigned long long *tt = a.timing + (size_t)p * 6;
+            const unsigned long long t = __builtin_readcyclecounter();
+            tt[0] = tm_hyp; tt[1] = tm_val; tt[2] = t - tm_a; tt[3] = t - tm0;
+            tt[4] = (unsigned long long)sh.validated; tt[5] = (unsigned long long)sh.base;
+        }
     }
 }
 
@@ -302,6 +318,13 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.seed = prm->seed;
     a.T_out = T_out; a.fit_out = fit_out; a.stats = stats; a.corr_tgt = corr_tgt; a.mask = mask;
     a.words = (Nmax + 31) / 32;
+    a.timing = nullptr;
+    const bool want_timing = getenv("PCR_RANSAC_TIMING") != nullptr;
+    if (want_timing) {
+        a.timing = (unsigned long long *)workspace(12, sizeof(unsigned long long) * 6 * (size_t)P);
+        PCR_REQUIRE(a.timing, PCR_ERR_NOMEM, "ransac timing: %s", pcr_last_error());
+        PCR_HIP_CHECK(hipMemsetAsync(a.timing, 0, sizeof(unsigned long long) * 6 * (size_t)P, s));
+    }
     a.grid = GridBatch{};
     a.grid.S = 1;
     a.grid.cell = 1.0;
@@ -331,6 +354,19 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfRansacValidate);
+    if (want_timing) {  // debug: phase split in shader clocks (s_memtime), to stderr
+        std::vector<unsigned long long> h(6 * (size_t)P);
+        PCR_HIP_CHECK(hipMemcpyAsync(h.data(), a.timing, h.size() * 8, hipMemcpyDeviceToHost, s));
+        PCR_HIP_CHECK(hipStreamSynchronize(s));
+        double m[6] = {0, 0, 0, 0, 0, 0}, mx = 0;
+        for (int p = 0; p < P; ++p) {
+            for (int k = 0; k < 6; ++k) m[k] += (double)h[6 * p + k] / P;
+            mx = std::max(mx, (double)h[6 * p + 3]);
+        }
+        fprintf(stderr, "ransac timing (clocks, mean over %d pairs): hyp %.0f val %.0f final %.0f "
+                "total %.0f (max %.0f) validated %.1f last_base %.0f\n", P, m[0], m[1], m[2], m[3],
+                mx, m[4], m[5]);
+    }
     return PCR_OK;
 }
 

@@ -36,66 +36,87 @@ def _state(layer):
     return layer, None, None
 
 
-def warp(levels, x, k0=-8, max_level=None, min_level=0, ms=None):
-    """levels: NDPLayer modules or their state dicts (level i has m = i + 1
-    unless the module says otherwise or `ms` is given)."""
-    xt = torch.as_tensor(x)
-    dev = xt.device if xt.is_cuda else torch.device("cuda")
-    xt = xt.to(device=dev, dtype=torch.float32).contiguous().reshape(-1, 3)
-    if max_level is None:
-        max_level = len(levels) - 1
-    sel = list(range(min_level, max_level + 1))
-    keep, structs = [], []
-    width = depth = None
-    for i in sel:
-        sd, m_mod, k0_mod = _state(levels[i])
-        k0 = k0_mod if k0_mod is not None else k0
-        m = ms[i] if ms is not None else (m_mod if m_mod is not None else i + 1)
+class PreparedPyramid:
+    """Device-resident weights + level descriptors, built once (no per-call
+    host copies); `warp` then costs one launch."""
 
-        def dv(key):
-            t = torch.as_tensor(np.asarray(sd[key].detach().cpu() if hasattr(sd[key], "detach")
-                                           else sd[key]), dtype=torch.float32, device=dev)
-            t = t.contiguous()
-            keep.append(t)
-            return t
-        w_in = dv("input.0.weight")
+    def __init__(self, levels, k0=-8, ms=None, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda")
+        self.device, self.k0 = dev, k0
+        self._keep, self.structs, self.width, self.depth = [], [], None, None
+        for i, layer in enumerate(levels):
+            sd, m_mod, k0_mod = _state(layer)
+            if k0_mod is not None:
+                self.k0 = k0_mod
+            m = ms[i] if ms is not None else (m_mod if m_mod is not None else i + 1)
+            st = self._level(sd, int(m))
+            self.structs.append(st)
+
+    def _as_dev(self, v):
+        t = v.detach() if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+        return t.to(device=self.device, dtype=torch.float32)
+
+    def _dev(self, v):
+        t = self._as_dev(v).contiguous()
+        self._keep.append(t)
+        return t
+
+    def _level(self, sd, m):
+        w_in = self._dev(sd["input.0.weight"])
         W = w_in.shape[0]
         hid = []
         while f"mlp.pts_linears.{len(hid)}.weight" in sd:
             hid.append(len(hid))
         d = len(hid) + 1
-        if width is None:
-            width, depth = W, d
-        elif (W, d) != (width, depth):
+        if self.width is None:
+            self.width, self.depth = W, d
+        elif (W, d) != (self.width, self.depth):
             raise ValueError("all levels must share width and depth")
         st = _Level()
-        st.w_in, st.b_in = w_in.data_ptr(), dv("input.0.bias").data_ptr()
-        if hid:
-            wh = torch.stack([dv(f"mlp.pts_linears.{k}.weight") for k in hid]).contiguous()
-            bh = torch.stack([dv(f"mlp.pts_linears.{k}.bias") for k in hid]).contiguous()
-            keep += [wh, bh]
+        st.w_in, st.b_in = w_in.data_ptr(), self._dev(sd["input.0.bias"]).data_ptr()
+        if hid:  # the depth-1 MLP layers, contiguous (pcr_ndp_level.w_hid)
+            wh = self._dev(torch.stack([self._as_dev(sd[f"mlp.pts_linears.{k}.weight"]) for k in hid]))
+            bh = self._dev(torch.stack([self._as_dev(sd[f"mlp.pts_linears.{k}.bias"]) for k in hid]))
             st.w_hid, st.b_hid = wh.data_ptr(), bh.data_ptr()
-        st.w_rot, st.b_rot = dv("rot_brach.weight").data_ptr(), dv("rot_brach.bias").data_ptr()
-        st.w_trn, st.b_trn = dv("trn_branch.weight").data_ptr(), dv("trn_branch.bias").data_ptr()
+        st.w_rot, st.b_rot = self._dev(sd["rot_brach.weight"]).data_ptr(), self._dev(sd["rot_brach.bias"]).data_ptr()
+        st.w_trn, st.b_trn = self._dev(sd["trn_branch.weight"]).data_ptr(), self._dev(sd["trn_branch.bias"]).data_ptr()
         if "nr_branch.weight" in sd:
-            st.w_nr, st.b_nr = dv("nr_branch.weight").data_ptr(), dv("nr_branch.bias").data_ptr()
-        st.m = int(m)
-        structs.append(st)
-    n = xt.shape[0]
-    L = len(structs)
-    out = torch.empty_like(xt)
-    xl = torch.empty(L, n, 3, dtype=torch.float32, device=dev)
-    nr = torch.full((L, n), float("nan"), dtype=torch.float32, device=dev)
-    arr = (_Level * max(L, 1))(*structs)
-    with torch.cuda.device(dev):
-        _lib.call("pcr_ndp_warp", _lib.ptr(xt), n, ctypes.cast(arr, ctypes.c_void_p), L,
-                  int(width or 32), int(depth or 1), int(k0), _lib.ptr(out), _lib.ptr(xl),
-                  _lib.ptr(nr), _lib.stream_handle(dev))
-    data = {}
-    for k, i in enumerate(sel):
-        has_nr = structs[k].w_nr is not None
-        data[i] = (xl[k], nr[k] if has_nr else None)
-    return out, data
+            st.w_nr = self._dev(sd["nr_branch.weight"]).data_ptr()
+            st.b_nr = self._dev(sd["nr_branch.bias"]).data_ptr()
+        st.m = m
+        return st
+
+    def warp(self, x, max_level=None, min_level=0, per_level=True):
+        dev = self.device
+        xt = torch.as_tensor(x)
+        xt = xt.to(device=dev, dtype=torch.float32).contiguous().reshape(-1, 3)
+        if max_level is None:
+            max_level = len(self.structs) - 1
+        sel = list(range(min_level, max_level + 1))
+        structs = [self.structs[i] for i in sel]
+        n, L = xt.shape[0], len(structs)
+        out = torch.empty_like(xt)
+        xl = torch.empty(L, n, 3, dtype=torch.float32, device=dev) if per_level else None
+        nr = torch.full((L, n), float("nan"), dtype=torch.float32, device=dev) if per_level else None
+        arr = (_Level * max(L, 1))(*structs)
+        with torch.cuda.device(dev):
+            _lib.call("pcr_ndp_warp", _lib.ptr(xt), n, ctypes.cast(arr, ctypes.c_void_p), L,
+                      int(self.width or 32), int(self.depth or 1), int(self.k0), _lib.ptr(out),
+                      _lib.ptr(xl), _lib.ptr(nr), _lib.stream_handle(dev))
+        data = {}
+        if per_level:
+            for k, i in enumerate(sel):
+                data[i] = (xl[k], nr[k] if structs[k].w_nr is not None else None)
+        return out, data
+
+
+def warp(levels, x, k0=-8, max_level=None, min_level=0, ms=None):
+    """levels: NDPLayer modules or their state dicts (level i has m = i + 1
+    unless the module says otherwise or `ms` is given).  For repeated warps
+    with the same weights build a PreparedPyramid once."""
+    xt = torch.as_tensor(x)
+    dev = xt.device if xt.is_cuda else None
+    return PreparedPyramid(levels, k0=k0, ms=ms, device=dev).warp(x, max_level, min_level)
 
 
 def warp_pyramid(pyramid, x, max_level=None, min_level=0):
