@@ -31,32 +31,75 @@ struct GridT {
     const IdxT *start;
     int S;
     double cell;
+    double inv_cell;  // queries use v * inv_cell: the 1.001 r margin covers the rounding
 };
 using GridView = GridT<uint32_t>;
 
-// returns target index or -1; d2out = its squared distance
+// squared distance from p to cell c's box [c*cell, (c+1)*cell] along one axis,
+// the box grown by a relative 1e-12 (the build assigns cells by floor(v / cell):
+// a point may sit an ulp outside the multiplied bounds)
+__device__ __forceinline__ double cell_gap(double p, int c, double cell) {
+    const double lo = (double)c * cell, hi = (double)(c + 1) * cell;
+    const double eps = 1e-12 * (__builtin_fabs(lo) + __builtin_fabs(hi) + cell);
+    const double g = __builtin_fmax(__builtin_fmax((lo - eps) - p, p - (hi + eps)), 0.0);
+    return g * g;
+}
+
+// returns target index or -1; d2out = its squared distance.  Cells whose box
+// is farther than r from p are skipped (they cannot hold a point with
+// d2 < thr <= r^2 (1 + 2^-23)); candidates are taken two at a time so their
+// LDS loads overlap.  The update order (slot order, strict < then lower index
+// on ties) makes the result independent of both.
 template <typename IdxT>
 __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double thr, double px,
                                           double py, double pz, double &d2out) {
-    const double rr = 1.001 * r;
-    const int x0 = cell_coord(px - rr, g.cell), x1 = cell_coord(px + rr, g.cell);
-    const int y0 = cell_coord(py - rr, g.cell), y1 = cell_coord(py + rr, g.cell);
-    const int z0 = cell_coord(pz - rr, g.cell), z1 = cell_coord(pz + rr, g.cell);
+    // The build assigns cells by floor(v / cell); here floor(v * inv_cell) over
+    // [p - 1.001 r, p + 1.001 r]: the 0.1 % margin exceeds the rounding
+    // difference, so every point within r of p lies in a visited cell.
+    const double rr = 1.001 * r, ic = g.inv_cell;
+    const int x0 = (int)__builtin_floor((px - rr) * ic), x1 = (int)__builtin_floor((px + rr) * ic);
+    const int y0 = (int)__builtin_floor((py - rr) * ic), y1 = (int)__builtin_floor((py + rr) * ic);
+    const int z0 = (int)__builtin_floor((pz - rr) * ic), z1 = (int)__builtin_floor((pz + rr) * ic);
+    const double lim = thr * (1.0 + 1e-9);
     double best = __builtin_inf();
     int bj = -1;
-    for (int x = x0; x <= x1; ++x)
-        for (int y = y0; y <= y1; ++y)
+    auto take = [&](int s) {
+        const double d2 = dist2(px, py, pz, (double)g.x[s], (double)g.y[s], (double)g.z[s]);
+        if (d2 < thr) {
+            const int j = (int)g.idx[s];
+            if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; }
+        }
+    };
+    for (int x = x0; x <= x1; ++x) {
+        const double gx = cell_gap(px, x, g.cell);
+        if (gx > lim) continue;
+        for (int y = y0; y <= y1; ++y) {
+            const double gxy = gx + cell_gap(py, y, g.cell);
+            if (gxy > lim) continue;
             for (int z = z0; z <= z1; ++z) {
+                if (gxy + cell_gap(pz, z, g.cell) > lim) continue;
                 const unsigned h = cell_hash(x, y, z, g.S);
+                int s = (int)g.start[h];
                 const int s1 = (int)g.start[h + 1];
-                for (int s = (int)g.start[h]; s < s1; ++s) {
-                    const double d2 = dist2(px, py, pz, (double)g.x[s], (double)g.y[s], (double)g.z[s]);
-                    if (d2 < thr) {
+                for (; s + 1 < s1; s += 2) {
+                    // both loads first, then the two updates in slot order
+                    const float ax = g.x[s], ay = g.y[s], az = g.z[s];
+                    const float bx = g.x[s + 1], by = g.y[s + 1], bz = g.z[s + 1];
+                    const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
+                    const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
+                    if (da < thr) {
                         const int j = (int)g.idx[s];
-                        if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; }
+                        if (da < best || (da == best && j < bj)) { best = da; bj = j; }
+                    }
+                    if (db < thr) {
+                        const int j = (int)g.idx[s + 1];
+                        if (db < best || (db == best && j < bj)) { best = db; bj = j; }
                     }
                 }
+                if (s < s1) take(s);
             }
+        }
+    }
     d2out = best;
     return bj;
 }
@@ -71,7 +114,7 @@ struct GridBatch {
     double cell;
     __device__ GridView view(int p) const {
         const size_t o = (size_t)p * mstride;
-        return GridView{x + o, y + o, z + o, idx + o, start + (size_t)p * (S + 1), S, cell};
+        return GridView{x + o, y + o, z + o, idx + o, start + (size_t)p * (S + 1), S, cell, 1.0 / cell};
     }
 };
 
@@ -101,8 +144,13 @@ __device__ inline GridT<uint16_t> grid_to_lds(const GridBatch &gb, int p, int m,
     const uint32_t *st = gb.start + (size_t)p * (gb.S + 1);
     for (int i = threadIdx.x; i <= gb.S; i += blockDim.x) ls[i] = (uint16_t)st[i];
     __syncthreads();
-    return GridT<uint16_t>{lx, ly, lz, li, ls, gb.S, gb.cell};
+    return GridT<uint16_t>{lx, ly, lz, li, ls, gb.S, gb.cell, 1.0 / gb.cell};
 }
+
+// host: spatial (Morton-of-cell) order of each cloud's points, (P, Nmax) i32 in a
+// workspace slot; identity order for clouds too large for the LDS sort
+int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double cell, hipStream_t s,
+                  int ws_slot, const int32_t **order);
 
 // host: allocate (workspace slot) + build; returns PCR_OK or error
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r,

@@ -52,7 +52,93 @@ __global__ void grid_scatter(BuildArgs a) {
     a.idx[o] = (uint32_t)j;
 }
 
+
+// Spatial order of a cloud: points sorted by the Morton code of their grid
+// cell (10 bits per axis relative to the cloud's minimum cell), one
+// 1024-thread workgroup per cloud, bitonic sort of (key << 16 | index) in
+// LDS.  Sweeps that walk a cloud in this order give each wave neighbouring
+// queries: the same hash cells, similar candidate counts, coherent LDS reads.
+__device__ __forceinline__ unsigned spread10(unsigned v) {
+    v &= 1023u;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, const int32_t *n,
+                                                             int Nmax, double inv_cell, int np2max,
+                                                             int32_t *order) {
+    extern __shared__ unsigned long long keys[];
+    __shared__ int smin[3][16];
+    const int p = blockIdx.x, t = threadIdx.x;
+    const int cnt = count_of(n, p, Nmax);
+    const float *P = pts + (size_t)p * Nmax * 3;
+    int32_t *o = order + (size_t)p * Nmax;
+    int np2 = 1;
+    while (np2 < cnt) np2 <<= 1;
+    if (np2 > np2max) {  // too large for the LDS sort: identity order
+        for (int i = t; i < Nmax; i += 1024) o[i] = i;
+        return;
+    }
+    int mn[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
+    for (int i = t; i < cnt; i += 1024)
+        for (int c = 0; c < 3; ++c) mn[c] = min(mn[c], (int)__builtin_floor((double)P[3 * i + c] * inv_cell));
+    for (int c = 0; c < 3; ++c) {
+        for (int off = 32; off; off >>= 1) mn[c] = min(mn[c], __shfl_xor(mn[c], off, 64));
+        if ((t & 63) == 0) smin[c][t >> 6] = mn[c];
+    }
+    __syncthreads();
+    int base[3];
+    for (int c = 0; c < 3; ++c) {
+        int v = smin[c][0];
+        for (int w = 1; w < 16; ++w) v = min(v, smin[c][w]);
+        base[c] = v;
+    }
+    for (int i = t; i < np2; i += 1024) {
+        unsigned long long k = ~0ull;
+        if (i < cnt) {
+            unsigned m = 0;
+            for (int c = 0; c < 3; ++c) {
+                const int q = (int)__builtin_floor((double)P[3 * i + c] * inv_cell) - base[c];
+                m |= spread10((unsigned)min(max(q, 0), 1023)) << c;
+            }
+            k = ((unsigned long long)m << 16) | (unsigned)i;
+        }
+        keys[i] = k;
+    }
+    __syncthreads();
+    for (int size = 2; size <= np2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < np2; i += 1024) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const unsigned long long a = keys[i], b = keys[j];
+                    if ((a > b) == ((i & size) == 0)) { keys[i] = b; keys[j] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = t; i < Nmax; i += 1024) o[i] = i < cnt ? (int32_t)(keys[i] & 0xFFFFu) : i;
+}
+
 }  // namespace
+
+int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double cell, hipStream_t s,
+                  int ws_slot, const int32_t **order) {
+    int32_t *o = (int32_t *)workspace(ws_slot, sizeof(int32_t) * (size_t)P * Nmax + 64);
+    PCR_REQUIRE(o, PCR_ERR_NOMEM, "spatial_order: %s", pcr_last_error());
+    const int np2max = Nmax <= 65536 ? 16384 : 0;  // 128 KiB of keys; indices fit 16 bits
+    const size_t sm = sizeof(unsigned long long) * (size_t)(np2max > 0 ? np2max : 1);
+    PCR_HIP_CHECK(hipFuncSetAttribute((const void *)spatial_order_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+    hipLaunchKernelGGL(spatial_order_kernel, dim3(P), dim3(1024), sm, s, pts, n, Nmax, 1.0 / cell,
+                       np2max, o);
+    PCR_LAUNCH_CHECK();
+    *order = o;
+    return PCR_OK;
+}
 
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r, hipStream_t s,
                 int ws_slot, GridBatch &out) {

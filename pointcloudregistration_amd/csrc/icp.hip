@@ -28,6 +28,7 @@ struct IArgs {
     double *T_out, *fit_out;
     int32_t *stats;
     int32_t *corr_tgt;  // optional (P, Nmax): final correspondence per source point
+    const int32_t *order;  // (P, Nmax) spatial order of the source points, or null
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -91,7 +92,9 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
     auto evaluate = [&]() {
         unsigned long long acc = 0;
         int cnt = 0;
-        for (int i = tid; i < n; i += 1024) {
+        const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
+        for (int k = tid; k < n; k += 1024) {
+            const int i = ord ? ord[k] : k;  // spatial order: coherent waves
             double d2;
             int j;
             if constexpr (kLds) j = grid_query(gl, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
@@ -213,6 +216,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     IArgs a;
     a.src = src; a.tgt = tgt; a.n_src = n_src; a.n_tgt = n_tgt; a.Nmax = Nmax; a.Mmax = Mmax;
     a.init = init;
+    a.order = nullptr;
     a.d = prm->max_correspondence_distance;
     a.thr = radius_thr(a.d);
     a.rel_fit = prm->relative_fitness;
@@ -221,6 +225,10 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     if (a.d > 0.0) {
         int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
         if (rc != PCR_OK) return rc;
+        if (Nmax > 0) {
+            rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 14, &a.order);
+            if (rc != PCR_OK) return rc;
+        }
     } else {
         a.grid = GridBatch{};
         a.grid.S = 1;

@@ -53,6 +53,7 @@ struct RArgs {
     uint32_t *mask;
     int words;
     unsigned long long *timing;  // debug (PCR_RANSAC_TIMING): per pair, 6 phase clocks
+    const int32_t *order;        // (P, Nmax) spatial order of the source points, or null
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
     const int32_t *co = a.corres + (size_t)p * a.Kmax * 2;
+    const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
     GridT<uint16_t> gl{};
     GridView gg{};
     if (ok) {
@@ -193,7 +195,8 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
             const double *Te = sh.listT[e];
             unsigned long long acc = 0;
             int cnt = 0, cin = 0;
-            for (int i = tid; i < n; i += kThreads) {
+            for (int k = tid; k < n; k += kThreads) {
+                const int i = ord ? ord[k] : k;  // spatial order: coherent waves
                 double px, py, pz, d2;
                 xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
                 int j;
@@ -246,10 +249,14 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
     // last bound update (or max_iter)
     const int iters = ok ? min(a.max_iter, max(sh.last_upd + 1, sh.est_k)) : 0;
     const bool found = ok && sh.best_itr >= 0;
-    // correspondence set of the best transformation
+    // correspondence set of the best transformation, swept in spatial order;
+    // the inlier mask is assembled with atomicOr on words zeroed first
+    if (a.mask)
+        for (int w = tid; w < a.words; w += kThreads) a.mask[(size_t)p * a.words + w] = 0u;
+    __syncthreads();
     int cnt = 0;
-    for (int base = 0; base < a.Nmax; base += kThreads) {
-        const int i = base + tid;
+    for (int k = tid; k < a.Nmax; k += kThreads) {
+        const int i = (ord && k < n) ? ord[k] : k;
         int j = -1;
         if (found && i < n) {
             double px, py, pz, d2;
@@ -257,15 +264,9 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
             if constexpr (kLds) j = grid_query(gl, a.d, a.thr, px, py, pz, d2);
             else j = grid_query(gg, a.d, a.thr, px, py, pz, d2);
         }
-        if (i < a.Nmax && a.corr_tgt) a.corr_tgt[(size_t)p * a.Nmax + i] = j;
+        if (a.corr_tgt) a.corr_tgt[(size_t)p * a.Nmax + i] = j;
         cnt += (j >= 0);
-        if (a.mask) {
-            const unsigned long long bits = __ballot(j >= 0);
-            const int word = (base + (tid & ~63)) >> 5;
-            if (lane == 0 && word < a.words) a.mask[(size_t)p * a.words + word] = (uint32_t)bits;
-            if (lane == 32 && word + 1 < a.words)
-                a.mask[(size_t)p * a.words + word + 1] = (uint32_t)(bits >> 32);
-        }
+        if (a.mask && j >= 0) atomicOr(a.mask + (size_t)p * a.words + (i >> 5), 1u << (i & 31));
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
@@ -319,6 +320,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.T_out = T_out; a.fit_out = fit_out; a.stats = stats; a.corr_tgt = corr_tgt; a.mask = mask;
     a.words = (Nmax + 31) / 32;
     a.timing = nullptr;
+    a.order = nullptr;
     const bool want_timing = getenv("PCR_RANSAC_TIMING") != nullptr;
     if (want_timing) {
         a.timing = (unsigned long long *)workspace(12, sizeof(unsigned long long) * 6 * (size_t)P);
@@ -331,6 +333,10 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     if (a.d > 0.0 && Mmax > 0) {
         int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 4, a.grid);
         if (rc != PCR_OK) return rc;
+        if (Nmax > 0) {
+            rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 13, &a.order);
+            if (rc != PCR_OK) return rc;
+        }
     }
     const size_t hdr = (sizeof(Shared) + 15) & ~size_t(15);
     const size_t budget = 160 * 1024 - hdr;
