@@ -51,6 +51,7 @@ struct IShared {  // LDS header; the grid copy (if any) follows
     int s_cnt[16];
     double s_fit, s_rmse;
     int s_count;
+    int chunk;  // next 64-query chunk of the current sweep
 };
 
 template <bool kLds>
@@ -68,6 +69,7 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *G = a.tgt + (size_t)p * a.Mmax * 3;
     if (tid < 16) T[tid] = a.init[(size_t)p * 16 + tid];
+    if (tid == 0) sh.chunk = 0;
     __syncthreads();
     const bool valid = a.d > 0.0 && n > 0 && m > 0;
     bool ident = true;
@@ -93,14 +95,22 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
         unsigned long long acc = 0;
         int cnt = 0;
         const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
-        for (int k = tid; k < n; k += 1024) {
-            const int i = ord ? ord[k] : k;  // spatial order: coherent waves
-            double d2;
-            int j;
-            if constexpr (kLds) j = grid_query(gl, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
-            else j = grid_query(gg, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
-            cj[i] = j;
-            if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+        const int nch = (n + 63) >> 6, lane = tid & 63;
+        for (;;) {  // 64-query chunks in spatial order, taken dynamically
+            int c = 0;
+            if (lane == 0) c = atomicAdd(&sh.chunk, 1);
+            c = __shfl(c, 0, 64);
+            if (c >= nch) break;
+            const int k = (c << 6) + lane;
+            if (k < n) {
+                const int i = ord ? ord[k] : k;
+                double d2;
+                int j;
+                if constexpr (kLds) j = grid_query(gl, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
+                else j = grid_query(gg, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
+                cj[i] = j;
+                if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+            }
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
@@ -114,6 +124,7 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
             int C = 0;
             for (int w = 0; w < 16; ++w) { A += sh.s_acc[w]; C += sh.s_cnt[w]; }
             sh.s_count = C;
+            sh.chunk = 0;  // next sweep (published by the barrier below)
             if (C > 0) {
                 sh.s_fit = (double)C / (double)n;
                 sh.s_rmse = __builtin_sqrt(((double)A / scale) / (double)C);

@@ -131,6 +131,9 @@ struct Shared {  // LDS header (the grid copy follows)
     double bestT[12];
     double best_fit, best_rmse;
     int est_k, best_itr, validated, last_upd, base, found;
+    int chunk;     // next 64-query chunk of the current sweep (dynamic balance across waves)
+    int misses;    // source points without a correspondence so far in this sweep
+    int best_cnt;  // inlier count of the best hypothesis (0: none yet)
 };
 
 template <bool kLds, int RN>
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
         for (int k = 0; k < 12; ++k) sh.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
         sh.best_fit = 0.0; sh.best_rmse = 0.0;
         sh.est_k = a.max_iter; sh.best_itr = -1; sh.validated = 0; sh.last_upd = -1; sh.base = 0;
+        sh.chunk = 0; sh.misses = 0; sh.best_cnt = 0;
     }
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
@@ -195,22 +199,45 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
             const double *Te = sh.listT[e];
             unsigned long long acc = 0;
             int cnt = 0, cin = 0;
-            for (int k = tid; k < n; k += kThreads) {
-                const int i = ord ? ord[k] : k;  // spatial order: coherent waves
-                double px, py, pz, d2;
-                xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
-                int j;
-                if constexpr (kLds) j = grid_query(gl, a.d, a.thr, px, py, pz, d2);
-                else j = grid_query(gg, a.d, a.thr, px, py, pz, d2);
-                if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+            // waves take 64-query chunks (spatial order) from an LDS counter:
+            // dense and sparse regions cost different time, a static split
+            // left waves idle at the barrier
+            const int nch = (n + 63) >> 6;
+            // a hypothesis with more than n - best_cnt misses cannot reach the
+            // best fitness (not even tie it): Open3D's rule can never accept
+            // it, so its sweep stops there (exact; no effect on T, fitness,
+            // rmse or est_k)
+            const int lim_miss = sh.best_cnt > 0 ? n - sh.best_cnt : 0x7fffffff;
+            for (;;) {
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&sh.chunk, 1);
+                c = __shfl(c, 0, 64);
+                if (c >= nch) break;
+                const int k = (c << 6) + lane;
+                int j = 0;
+                if (k < n) {
+                    const int i = ord ? ord[k] : k;
+                    double px, py, pz, d2;
+                    xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
+                    if constexpr (kLds) j = grid_query(gl, a.d, a.thr, px, py, pz, d2);
+                    else j = grid_query(gg, a.d, a.thr, px, py, pz, d2);
+                    if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+                }
+                const int miss = __popcll(__ballot(k < n && j < 0));
+                int tot = 0;
+                if (lane == 0) tot = atomicAdd(&sh.misses, miss) + miss;
+                tot = __shfl(tot, 0, 64);
+                if (tot > lim_miss) break;
             }
-            for (int k = tid; k < K; k += kThreads) {
-                const int si = co[2 * k], ti = co[2 * k + 1];
-                double px, py, pz;
-                xform12(Te, (double)S[3 * si], (double)S[3 * si + 1], (double)S[3 * si + 2], px, py, pz);
-                if (dist2(px, py, pz, (double)Gt[3 * ti], (double)Gt[3 * ti + 1], (double)Gt[3 * ti + 2]) < a.dd)
-                    ++cin;
-            }
+            const bool hopeless = __atomic_load_n(&sh.misses, __ATOMIC_RELAXED) > lim_miss;
+            if (!hopeless)
+                for (int k = tid; k < K; k += kThreads) {
+                    const int si = co[2 * k], ti = co[2 * k + 1];
+                    double px, py, pz;
+                    xform12(Te, (double)S[3 * si], (double)S[3 * si + 1], (double)S[3 * si + 2], px, py, pz);
+                    if (dist2(px, py, pz, (double)Gt[3 * ti], (double)Gt[3 * ti + 1], (double)Gt[3 * ti + 2]) < a.dd)
+                        ++cin;
+                }
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) {
                 acc += __shfl_xor(acc, o, 64);
@@ -228,8 +255,12 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
                     fit = (double)C / (double)n;
                     rmse = __builtin_sqrt(((double)A / scale) / (double)C);
                 }
+                const bool cut = sh.misses > lim_miss;  // sweep stopped early: cannot win
                 sh.validated += 1;
-                if (fit > sh.best_fit || (fit == sh.best_fit && rmse < sh.best_rmse)) {
+                sh.chunk = 0;  // next sweep (published by the barrier below)
+                sh.misses = 0;
+                if (!cut && (fit > sh.best_fit || (fit == sh.best_fit && rmse < sh.best_rmse))) {
+                    sh.best_cnt = C;
                     sh.best_fit = fit;
                     sh.best_rmse = rmse;
                     sh.best_itr = itr_e;
