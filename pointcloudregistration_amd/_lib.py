@@ -109,7 +109,7 @@ def exported_symbols():
 
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
-PROF_FEAT_RESCAN, PROF_FEAT_PACK = 5, 6
+PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID = 5, 6, 7
 
 
 def profile_enable(on=True):

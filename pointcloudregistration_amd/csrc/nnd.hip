@@ -19,6 +19,7 @@
 // Numerics: d = (dx*dx + dy*dy) + dz*dz, each op rounded (built with
 // -ffp-contract=off), dx = cand.x - query.x as in my_lib.cpp:12-15.
 #include "pcr_internal.h"
+#include <cstdlib>
 #include <math.h>
 
 namespace {
@@ -340,6 +341,11 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
 
+namespace pcr {
+int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
+                     float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s);
+}
+
 extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, int32_t n,
                                int32_t m, float *dist1, float *dist2, int32_t *idx1,
                                int32_t *idx2, pcr_stream_t stream) {
@@ -360,6 +366,14 @@ extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, 
             PCR_HIP_CHECK(hipMemsetAsync(idx2, 0, sizeof(int32_t) * (size_t)b * m, s));
         }
         return PCR_OK;
+    }
+    // large clouds: exact certified grid search (nnd_grid.hip), identical results;
+    // PCR_NND_ALGO=brute|grid overrides the size rule
+    {
+        const char *e = getenv("PCR_NND_ALGO");
+        const bool force_brute = e && e[0] == 'b', force_grid = e && e[0] == 'g';
+        if (force_grid || (!force_brute && n >= 1024 && m >= 1024))
+            return pcr::nnd_forward_grid(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, s);
     }
     constexpr int QP = 4;  // 8 queries per lane as 4 packed pairs
     constexpr int Q = 2 * QP;

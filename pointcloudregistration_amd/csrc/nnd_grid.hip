@@ -1,0 +1,235 @@
+// a1 (large clouds): exact nearest neighbour by certified grid search.
+//
+// Same contract as the brute-force kernel (nnd.hip, my_lib.cpp:3-25): for each
+// query q the result is the candidate j minimising d_j = (dx*dx + dy*dy) +
+// dz*dz in f32 (dx = c_j - q, no FMA), lowest index on ties.  For finite
+// inputs that is the lexicographic minimum of (d_j, j), which a search over any
+// superset of the winners returns unchanged; clouds holding a NaN/Inf (where
+// the reference's seed rule matters) or too far from the origin for integer
+// cell coordinates are answered by the reference loop itself.
+//
+// Per cloud a hashed uniform grid (cell = 0.6 * cbrt(bbox volume / n),
+// degenerate boxes widened) stores float4 (x, y, z, index) sorted by slot.
+// A query scans the Chebyshev rings k = 0, 1, ... of cells around its own;
+// after ring k, every unvisited point is at least g = (distance from q to the
+// faces of the (2k+1)^3 block) away, and its computed f32 distance at least
+// g^2 (1 - 8 * 2^-24) (each of the 5 f32 roundings is relative); once that
+// exceeds the best distance (strictly) the answer is final.  Rings are capped
+// at kMaxRing, then the query scans every point (same exact rule).
+//
+// One thread per query, 256-thread blocks over all pairs and both directions;
+// the grids (160 KB per 8192-point cloud) stay L2-resident.
+#include "pcr_internal.h"
+#include "scan.h"
+
+namespace pcr {
+namespace {
+
+constexpr int kMaxRing = 3;
+
+struct NgArgs {
+    const float *xyz[2];  // set 0: xyz1 (B, n0, 3), set 1: xyz2 (B, n1, 3)
+    int n[2];
+    int B, S, nmax;
+    float *cell;          // [2][B]
+    int *flag;            // [B]: 1 = use the reference loop
+    int *hcnt;            // [2][B][S]
+    int *start;           // [2][B][S+1]
+    float4 *pts;          // [2][B][nmax]
+    float *dist[2];       // dist[0] = dist1: queries of set 0 against the grid of set 1
+    int32_t *idx[2];
+};
+
+__device__ __forceinline__ unsigned nhash(int x, int y, int z, int S) {
+    return (((unsigned)x * 73856093u) ^ ((unsigned)y * 19349663u) ^ ((unsigned)z * 83492791u)) &
+           (unsigned)(S - 1);
+}
+
+__device__ __forceinline__ int ccoord(float v, double ic) { return (int)__builtin_floor((double)v * ic); }
+
+__global__ __launch_bounds__(256) void nng_bbox(NgArgs a) {
+    const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x, n = a.n[s];
+    const float *P = a.xyz[s] + (size_t)b * n * 3;
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    int bad = 0;
+    for (int i = t; i < n; i += 256)
+        for (int c = 0; c < 3; ++c) {
+            const float v = P[3 * i + c];
+            bad |= !__builtin_isfinite(v);
+            lo[c] = fminf(lo[c], v);
+            hi[c] = fmaxf(hi[c], v);
+        }
+    __shared__ float sl[3][4], sh[3][4];
+    __shared__ int sb[4];
+    for (int c = 0; c < 3; ++c)
+        for (int o = 32; o; o >>= 1) {
+            lo[c] = fminf(lo[c], __shfl_xor(lo[c], o, 64));
+            hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o, 64));
+        }
+    for (int o = 32; o; o >>= 1) bad |= __shfl_xor(bad, o, 64);
+    if ((t & 63) == 0) {
+        for (int c = 0; c < 3; ++c) { sl[c][t >> 6] = lo[c]; sh[c][t >> 6] = hi[c]; }
+        sb[t >> 6] = bad;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    double e[3], m = 0.0, amax = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        float l = sl[c][0], h = sh[c][0];
+        for (int w = 1; w < 4; ++w) { l = fminf(l, sl[c][w]); h = fmaxf(h, sh[c][w]); }
+        e[c] = (double)h - (double)l;
+        m = fmax(m, e[c]);
+        amax = fmax(amax, fmax(fabs((double)l), fabs((double)h)));
+    }
+    bad = sb[0] | sb[1] | sb[2] | sb[3];
+    double cell = 1.0;
+    if (m > 0.0) {
+        double v = 1.0;
+        for (int c = 0; c < 3; ++c) v *= fmax(e[c], 1e-3 * m);
+        cell = 0.6 * cbrt(v / (double)(n > 0 ? n : 1));
+    }
+    // integer cell coordinates must stay far from int overflow
+    if (!(amax / cell < 1e9)) bad = 1;
+    a.cell[s * a.B + b] = (float)cell;
+    if (bad) atomicOr(a.flag + b, 1);
+}
+
+__global__ void nng_count(NgArgs a) {
+    const int s = blockIdx.z, b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n[s] || a.flag[b]) return;
+    const float *p = a.xyz[s] + ((size_t)b * a.n[s] + i) * 3;
+    const double ic = 1.0 / (double)a.cell[s * a.B + b];
+    const unsigned h = nhash(ccoord(p[0], ic), ccoord(p[1], ic), ccoord(p[2], ic), a.S);
+    atomicAdd(a.hcnt + ((size_t)s * a.B + b) * a.S + h, 1);
+}
+
+__global__ __launch_bounds__(1024) void nng_scan(NgArgs a) {
+    const int s = blockIdx.y, b = blockIdx.x;
+    if (a.flag[b]) return;
+    const size_t g = (size_t)s * a.B + b;
+    block_exclusive_scan_1024(a.hcnt + g * a.S, a.start + g * (a.S + 1), a.S, true);
+}
+
+__global__ void nng_scatter(NgArgs a) {
+    const int s = blockIdx.z, b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n[s] || a.flag[b]) return;
+    const float *p = a.xyz[s] + ((size_t)b * a.n[s] + i) * 3;
+    const size_t g = (size_t)s * a.B + b;
+    const double ic = 1.0 / (double)a.cell[g];
+    const unsigned h = nhash(ccoord(p[0], ic), ccoord(p[1], ic), ccoord(p[2], ic), a.S);
+    const int pos = a.start[g * (a.S + 1) + h] + atomicAdd(a.hcnt + g * a.S + h, 1);
+    a.pts[g * a.nmax + pos] = make_float4(p[0], p[1], p[2], __int_as_float(i));
+}
+
+__device__ __forceinline__ float d2f(float cx, float cy, float cz, float qx, float qy, float qz) {
+    const float dx = cx - qx, dy = cy - qy, dz = cz - qz;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+__global__ __launch_bounds__(256) void nng_query(NgArgs a) {
+    const int dir = blockIdx.z, b = blockIdx.y, qi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int qs = dir, gs = 1 - dir;  // queries from set dir, candidates from the other set
+    if (qi >= a.n[qs]) return;
+    const float *q = a.xyz[qs] + ((size_t)b * a.n[qs] + qi) * 3;
+    const float qx = q[0], qy = q[1], qz = q[2];
+    const int m = a.n[gs];
+    const float *C = a.xyz[gs] + (size_t)b * m * 3;
+    float best = __builtin_inff();
+    int bj = 0x7fffffff;
+    bool done = false;
+    if (a.flag[b]) {
+        // the reference loop: seed with candidate 0, strict < (my_lib.cpp:11-20)
+        best = d2f(C[0], C[1], C[2], qx, qy, qz);
+        bj = 0;
+        for (int j = 1; j < m; ++j) {
+            const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
+            if (d < best) { best = d; bj = j; }
+        }
+        done = true;
+    }
+    if (!done) {
+        const size_t g = (size_t)gs * a.B + b;
+        const float cellf = a.cell[g];
+        const double cell = (double)cellf, ic = 1.0 / cell;
+        const int cx = ccoord(qx, ic), cy = ccoord(qy, ic), cz = ccoord(qz, ic);
+        const int *st = a.start + g * (a.S + 1);
+        const float4 *pts = a.pts + g * a.nmax;
+        const double margin = 1e-6 * (fabs((double)qx) + fabs((double)qy) + fabs((double)qz) + cell);
+        auto scan_cell = [&](int x, int y, int z) {
+            const unsigned h = nhash(x, y, z, a.S);
+            const int s1 = st[h + 1];
+            for (int s = st[h]; s < s1; ++s) {
+                const float4 p = pts[s];
+                const float d = d2f(p.x, p.y, p.z, qx, qy, qz);
+                const int j = __float_as_int(p.w);
+                if (d < best || (d == best && j < bj)) { best = d; bj = j; }
+            }
+        };
+        for (int k = 0; k <= kMaxRing && !done; ++k) {
+            for (int dx = -k; dx <= k; ++dx)
+                for (int dy = -k; dy <= k; ++dy) {
+                    const bool face = (dx == -k || dx == k || dy == -k || dy == k);
+                    if (face) {
+                        for (int dz = -k; dz <= k; ++dz) scan_cell(cx + dx, cy + dy, cz + dz);
+                    } else {
+                        scan_cell(cx + dx, cy + dy, cz - k);
+                        scan_cell(cx + dx, cy + dy, cz + k);
+                    }
+                }
+            // distance from q to the faces of the visited (2k+1)^3 block
+            const double gx = fmin((double)qx - (double)(cx - k) * cell, (double)(cx + k + 1) * cell - (double)qx);
+            const double gy = fmin((double)qy - (double)(cy - k) * cell, (double)(cy + k + 1) * cell - (double)qy);
+            const double gz = fmin((double)qz - (double)(cz - k) * cell, (double)(cz + k + 1) * cell - (double)qz);
+            const double gmin = fmin(gx, fmin(gy, gz)) - margin;
+            if (gmin > 0.0 && gmin * gmin * (1.0 - 8.0 * 5.9604644775390625e-08) > (double)best) done = true;
+        }
+        if (!done) {  // not certified within kMaxRing rings: every candidate
+            for (int j = 0; j < m; ++j) {
+                const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
+                if (d < best || (d == best && j < bj)) { best = d; bj = j; }
+            }
+        }
+    }
+    a.dist[dir][(size_t)b * a.n[qs] + qi] = best;
+    a.idx[dir][(size_t)b * a.n[qs] + qi] = bj;
+}
+
+}  // namespace
+
+int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
+                     float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s) {
+    NgArgs a;
+    a.xyz[0] = xyz1; a.xyz[1] = xyz2; a.n[0] = n; a.n[1] = m; a.B = b;
+    a.nmax = n > m ? n : m;
+    int S = 256;
+    while (S < a.nmax) S <<= 1;
+    a.S = S;
+    const size_t cells = 2 * (size_t)b, hc = cells * S, stc = cells * (S + 1), pc = cells * a.nmax;
+    char *ws = (char *)workspace(15, 4 * (cells + b + hc + stc) + 16 * pc + 256);
+    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "nnd_forward (grid): %s", pcr_last_error());
+    a.pts = (float4 *)ws;
+    a.cell = (float *)(a.pts + pc);
+    a.flag = (int *)(a.cell + cells);
+    a.hcnt = a.flag + b;
+    a.start = a.hcnt + hc;
+    a.dist[0] = dist1; a.dist[1] = dist2; a.idx[0] = idx1; a.idx[1] = idx2;
+    PCR_HIP_CHECK(hipMemsetAsync(a.flag, 0, sizeof(int) * (b + hc), s));
+    hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    const dim3 pg((a.nmax + 255) / 256, b, 2);
+    hipLaunchKernelGGL(nng_count, pg, dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(nng_scan, dim3(b, 2), dim3(1024), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    PCR_HIP_CHECK(hipMemsetAsync(a.hcnt, 0, sizeof(int) * hc, s));
+    hipLaunchKernelGGL(nng_scatter, pg, dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    prof_begin(s, kProfNndGrid);
+    hipLaunchKernelGGL(nng_query, pg, dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfNndGrid);
+    return PCR_OK;
+}
+
+}  // namespace pcr

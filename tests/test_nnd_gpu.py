@@ -41,8 +41,13 @@ def assert_bitexact(got, exp, what):
         assert not bad.any(), f"{what}: {bad.sum()} of {bad.size} entries differ"
 
 
+ALGOS = ["auto", "brute", "grid"]  # PCR_NND_ALGO: size rule / forced brute force / forced grid
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_nnd_bitexact_vs_reference_golden(golden_nnd, name):
+def test_nnd_bitexact_vs_reference_golden(golden_nnd, monkeypatch, name, algo):
+    monkeypatch.setenv("PCR_NND_ALGO", algo)
     x1, x2, gd1, gd2 = make_inputs(CASES[name])
     got = _run_fwd_bwd(x1, x2, gd1, gd2)
     keys = ("d1", "d2", "i1", "i2", "g1", "g2")
@@ -61,8 +66,10 @@ def test_nnd_bitexact_vs_reference_golden(golden_nnd, name):
     assert h.digest() == bytes(golden_nnd[f"{name}/sha_bwd"]), name
 
 
-@pytest.mark.parametrize("b,n,m", [(1, 333, 4097), (3, 8192, 100), (64, 700, 900)])
-def test_nnd_bitexact_vs_oracle(oracle, b, n, m):
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("b,n,m", [(1, 333, 4097), (3, 8192, 100), (64, 700, 900), (2, 3000, 5000)])
+def test_nnd_bitexact_vs_oracle(oracle, monkeypatch, b, n, m, algo):
+    monkeypatch.setenv("PCR_NND_ALGO", algo)
     rng = np.random.default_rng(b * 7 + n)
     x1 = (rng.random((b, n, 3), dtype=np.float32) * 2 - 1).astype(np.float32)
     x2 = (rng.random((b, m, 3), dtype=np.float32) * 2 - 1).astype(np.float32)
@@ -117,3 +124,53 @@ def test_nnd_full_size_properties():
         best = dd.min(dim=1).values
         picked = dd.gather(1, i1[bat, rows].long()[:, None])[:, 0]
         assert torch.all(picked <= best * (1 + 1e-6) + 1e-12)
+
+
+def _adversarial(kind, rng):
+    if kind == "outliers":       # far queries: rings never certify -> per-query full scan
+        x1 = rng.random((2, 1500, 3), dtype=np.float32)
+        x1[:, ::50] += np.float32(100.0)
+        x2 = rng.random((2, 1400, 3), dtype=np.float32)
+    elif kind == "planar":       # zero-thickness box
+        x1 = rng.random((1, 2000, 3), dtype=np.float32)
+        x1[..., 2] = 0.5
+        x2 = rng.random((1, 2100, 3), dtype=np.float32)
+        x2[..., 2] = 0.5
+    elif kind == "identical":    # every point the same: all distances tie
+        x1 = np.full((1, 1200, 3), 0.25, np.float32)
+        x2 = np.full((1, 1300, 3), 0.25, np.float32)
+    elif kind == "quantised":    # many exact ties
+        x1 = (rng.integers(0, 8, (2, 2048, 3)) / 8).astype(np.float32)
+        x2 = (rng.integers(0, 8, (2, 2048, 3)) / 8).astype(np.float32)
+    elif kind == "huge_offset":
+        x1 = (rng.random((1, 1500, 3)) * 10 + 3e6).astype(np.float32)
+        x2 = (rng.random((1, 1600, 3)) * 10 + 3e6).astype(np.float32)
+    elif kind == "inf":          # non-finite: the reference loop (seed rule) answers
+        x1 = rng.random((2, 1100, 3), dtype=np.float32)
+        x2 = rng.random((2, 1200, 3), dtype=np.float32)
+        x2[1, 0, 1] = np.inf
+        x1[0, 5, 0] = -np.inf
+    else:                        # "nan"
+        x1 = rng.random((1, 1100, 3), dtype=np.float32)
+        x2 = rng.random((1, 1200, 3), dtype=np.float32)
+        x2[0, 0, 2] = np.nan
+        x1[0, 9, 1] = np.nan
+    return x1, x2
+
+
+@pytest.mark.parametrize("kind", ["outliers", "planar", "identical", "quantised",
+                                  "huge_offset", "inf", "nan"])
+def test_nnd_grid_adversarial_vs_oracle(oracle, monkeypatch, kind):
+    """The certified grid search stays exact where certification is hard."""
+    monkeypatch.setenv("PCR_NND_ALGO", "grid")
+    rng = np.random.default_rng(len(kind))
+    x1, x2 = _adversarial(kind, rng)
+    gd1 = rng.standard_normal(x1.shape[:2]).astype(np.float32)
+    gd2 = rng.standard_normal(x2.shape[:2]).astype(np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        got = _run_fwd_bwd(x1, x2, gd1, gd2)
+        e1, e2, j1, j2 = oracle.nnd_forward(x1, x2)
+        eg1, eg2 = oracle.nnd_backward(x1, x2, gd1, gd2, j1, j2)
+    for k, g, e in zip(("d1", "d2", "i1", "i2", "g1", "g2"), got, (e1, e2, j1, j2, eg1, eg2)):
+        assert_bitexact(g, e, f"{kind}/{k}")
+
