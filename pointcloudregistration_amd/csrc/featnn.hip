@@ -828,19 +828,38 @@ inline Split5 split5_params(int D) {
     return s;
 }
 
-// max |element| of each pair's clouds (f32 bits; both clouds -> same slot)
-__global__ __launch_bounds__(256) void feat_maxabs(const float *X, const int32_t *n, int Nmax,
-                                                   int D, unsigned *mx) {
-    const int p = blockIdx.y;
-    const size_t tot = (size_t)count_of(n, p, Nmax) * D;
-    const float *x = X + (size_t)p * Nmax * D;
+// max |element| of each pair's clouds (f32 bits; both clouds -> same slot):
+// one 1024-thread block per (pair, cloud), float4 loads, one atomic per block
+__global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_t *nf, int Nmax,
+                                                    const float *G, const int32_t *ng, int Mmax,
+                                                    int D, unsigned *mx) {
+    const int p = blockIdx.x, which = blockIdx.y, t = threadIdx.x;
+    const float *X = which ? G : F;
+    const int cnt = which ? count_of(ng, p, Mmax) : count_of(nf, p, Nmax);
+    const size_t tot = (size_t)cnt * D;
+    const float *x = X + (size_t)p * (which ? Mmax : Nmax) * D;
     float m = 0.0f;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
-         i += (size_t)gridDim.x * blockDim.x)
-        m = fmaxf(m, fabsf(x[i]));
+    if (((uintptr_t)x & 15) == 0) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(x);
+        const size_t t4 = tot >> 2;
+        for (size_t i = t; i < t4; i += 1024) {
+            const float4 v = x4[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+        for (size_t i = (t4 << 2) + t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
+    } else {
+        for (size_t i = t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
+    }
 #pragma unroll
     for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(mx + p, __float_as_uint(m));
+    __shared__ float wm[16];
+    if ((t & 63) == 0) wm[t >> 6] = m;
+    __syncthreads();
+    if (t == 0) {
+        float r = wm[0];
+        for (int w = 1; w < 16; ++w) r = fmaxf(r, wm[w]);
+        if (r > 0.0f) atomicMax(mx + p, __float_as_uint(r));
+    }
 }
 
 __device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
@@ -865,8 +884,10 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
     const float s = pair_scale5(mx[p], sp.T);
     const float *base = X + ((size_t)p * Nmax + (size_t)t * 32) * D;
     float (*x)[65] = xs[w];
+    // e / D by a 64-bit reciprocal (exact for e < 2^16; 2^32/D + 1 needs 33 bits at D = 1)
+    const unsigned long long invD = 0xFFFFFFFFull / (unsigned long long)D + 1ull;
     for (int e = l; e < 32 * D; e += 64) {
-        const int r = e / D, k = e - r * D;
+        const int r = (int)(((unsigned long long)e * invD) >> 32), k = e - r * D;
         x[r][k] = r < nrows ? base[e] * s : 0.0f;
     }
     __syncthreads();
@@ -1560,7 +1581,7 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
     // the 8 slices' ds_read_b128 hit disjoint banks, the rows of a slice
     // broadcast.  Dims in [D, DV) are zero on both sides (exact zero terms).
     constexpr int kChunk = 128, kSt = DV + 4;
-    __shared__ __attribute__((aligned(16))) float cs[kChunk * kSt];
+    __shared__ __attribute__((aligned(16))) float csb[2][kChunk * kSt];  // double buffer (V4 path)
     const int dir = blockIdx.y, p = blockIdx.x;
     const int tid = threadIdx.x, r = tid >> 3, sl = tid & 7;
     const float *Q = dir ? a.G : a.F;
@@ -1578,44 +1599,98 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
         const int row = act ? list[b0 + r] : 0;
         const float *q = Q + ((size_t)p * Nq + row) * D;
         double qd[DV];
+        float qf[DV];
 #pragma unroll
-        for (int k = 0; k < DV; ++k) qd[k] = k < D ? (double)q[k] : 0.0;
+        for (int k = 0; k < DV; ++k) {
+            qf[k] = k < D ? q[k] : 0.0f;
+            qd[k] = (double)qf[k];
+        }
         double best = __builtin_inf();
         int bj = 0x7fffffff;
-        for (int c0 = 0; c0 < nc; c0 += kChunk) {
-            const int ncand = min(kChunk, nc - c0);
-            __syncthreads();  // previous chunk fully consumed
-            if (V4) {
-                for (int e = tid; e < kChunk * (DV / 4); e += 256) {
-                    const int i = e / (DV / 4), k = (e - i * (DV / 4)) * 4;
-                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (i < ncand && k < D)
-                        v = *reinterpret_cast<const float4 *>(cb + (size_t)(c0 + i) * D + k);
-                    *reinterpret_cast<float4 *>(cs + i * kSt + k) = v;
-                }
-            } else {
-                for (int e = tid; e < kChunk * DV; e += 256) {
-                    const int i = e / DV, k = e - i * DV;
-                    cs[i * kSt + k] = (i < ncand && k < D) ? cb[(size_t)(c0 + i) * D + k] : 0.0f;
-                }
+        float m32 = __builtin_inff();
+        const float kRel = 1.0f + 3.0f * (float)(D + 5) * 5.9604644775390625e-08f;
+        // candidate chunk -> registers -> LDS; with V4 the next chunk's global
+        // loads are in flight while the current chunk is scanned
+        constexpr int kPer = kChunk * (DV / 4) / 256;  // float4 per thread per chunk
+        float4 stage[kPer];
+        auto gload = [&](int c0) {
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int e = tid + 256 * u, i = e / (DV / 4), k = (e - i * (DV / 4)) * 4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (c0 + i < nc && k < D)
+                    v = *reinterpret_cast<const float4 *>(cb + (size_t)(c0 + i) * D + k);
+                stage[u] = v;
             }
-            __syncthreads();
+        };
+        auto lstore = [&](float *cs) {
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int e = tid + 256 * u, i = e / (DV / 4), k = (e - i * (DV / 4)) * 4;
+                *reinterpret_cast<float4 *>(cs + i * kSt + k) = stage[u];
+            }
+        };
+        auto scan = [&](const float *cs, int c0, int ncand) {
             for (int i = sl; i < ncand; i += 8) {
                 const float *cp = cs + i * kSt;
-                double acc = 0.0;
+                // f32 fma screen: all terms are >= 0, so |d32 - d| <= (D+2) u d;
+                // only candidates within kRel of this thread's running f32 minimum
+                // (>= the global one) can be the exact winner -> f64 for those
+                float a32 = 0.0f;
 #pragma unroll
                 for (int k = 0; k < DV; k += 4) {
                     const float4 v = *reinterpret_cast<const float4 *>(cp + k);
-                    double df = qd[k] - (double)v.x;
-                    acc = acc + df * df;
-                    df = qd[k + 1] - (double)v.y;
-                    acc = acc + df * df;
-                    df = qd[k + 2] - (double)v.z;
-                    acc = acc + df * df;
-                    df = qd[k + 3] - (double)v.w;
-                    acc = acc + df * df;
+                    float df = v.x - qf[k];
+                    a32 = fmaf(df, df, a32);
+                    df = v.y - qf[k + 1];
+                    a32 = fmaf(df, df, a32);
+                    df = v.z - qf[k + 2];
+                    a32 = fmaf(df, df, a32);
+                    df = v.w - qf[k + 3];
+                    a32 = fmaf(df, df, a32);
                 }
-                if (acc < best) { best = acc; bj = c0 + i; }
+                if (a32 <= m32 * kRel + 1e-30f) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int k = 0; k < DV; k += 4) {
+                        const float4 v = *reinterpret_cast<const float4 *>(cp + k);
+                        double df = qd[k] - (double)v.x;
+                        acc = acc + df * df;
+                        df = qd[k + 1] - (double)v.y;
+                        acc = acc + df * df;
+                        df = qd[k + 2] - (double)v.z;
+                        acc = acc + df * df;
+                        df = qd[k + 3] - (double)v.w;
+                        acc = acc + df * df;
+                    }
+                    if (acc < best) { best = acc; bj = c0 + i; }
+                }
+                m32 = fminf(m32, a32);
+            }
+        };
+        if (V4) {
+            __syncthreads();  // previous batch done with both buffers
+            gload(0);
+            lstore(csb[0]);
+            __syncthreads();
+            int buf = 0;
+            for (int c0 = 0; c0 < nc; c0 += kChunk, buf ^= 1) {
+                const bool more = c0 + kChunk < nc;
+                if (more) gload(c0 + kChunk);
+                scan(csb[buf], c0, min(kChunk, nc - c0));
+                if (more) lstore(csb[buf ^ 1]);  // read last in the previous iteration
+                __syncthreads();
+            }
+        } else {
+            for (int c0 = 0; c0 < nc; c0 += kChunk) {
+                const int ncand = min(kChunk, nc - c0);
+                __syncthreads();  // previous chunk fully consumed
+                for (int e = tid; e < kChunk * DV; e += 256) {
+                    const int i = e / DV, k = e - i * DV;
+                    csb[0][i * kSt + k] = (i < ncand && k < D) ? cb[(size_t)(c0 + i) * D + k] : 0.0f;
+                }
+                __syncthreads();
+                scan(csb[0], c0, ncand);
             }
         }
 #pragma unroll
@@ -1840,11 +1915,8 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     int *list21 = list12 + (size_t)P * Nmax;  // per pair, stride Mmax
     PCR_HIP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned) * 5 * P, s));
     prof_begin(s, kProfFeatPack);
-    hipLaunchKernelGGL(feat_maxabs, dim3(cdiv((long long)Nmax * D, 256 * 16), P), dim3(256), 0, s, F,
-                       n_src, Nmax, D, mx);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(feat_maxabs, dim3(cdiv((long long)Mmax * D, 256 * 16), P), dim3(256), 0, s, G,
-                       n_tgt, Mmax, D, mx);
+    hipLaunchKernelGGL(feat_maxabs, dim3(P, 2), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax, D,
+                       mx);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D, NCH,
                        ntn, 0, sp, mx, Ap, fnr, gmax + P);
