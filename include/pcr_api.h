@@ -228,6 +228,54 @@ int pcr_ndp_warp(const float *x, int32_t N, const pcr_ndp_level *levels, int32_t
                  int32_t width, int32_t depth, int32_t k0, float *x_out, float *x_levels,
                  float *nonrigidity, pcr_stream_t stream);
 
+
+/* ---------------------------------------------------------------------------
+ * f2 -- KPConv input pyramid helpers (ngenet cpp_wrappers).
+ *
+ * pcr_grid_subsample replaces cpp_subsampling.subsample_batch
+ * (c2p-net/ngenet/cpp_wrappers/cpp_subsampling/wrapper.cpp:59-330 ->
+ * batch_grid_subsampling, grid_subsampling/grid_subsampling.cpp:109-211).
+ *   points (n,3) f32 and features (n,fdim) f32 (or NULL, fdim 0) are device
+ *   buffers; batch_len (nb) is a HOST array (cloud lengths, summing to <= n).
+ *   Per cloud: voxels of side dl from the floor(min/dl)*dl corner, barycentre
+ *   (f32 sums in input order, * (float)(1.0/count)) and mean features
+ *   (f / (float)count), emitted in the reference's unordered_map iteration order
+ *   and truncated to max_p per cloud (max_p < 1: n).  Writes out_points
+ *   (capacity n*3), out_features (capacity n*fdim), out_batch_len (HOST, nb)
+ *   and *out_total (HOST).  Bit-identical to the reference, order included.
+ *   Synchronous (the emission order is replayed on the host).  Non-finite
+ *   coordinates -> PCR_ERR_ARG (the reference's voxel index is undefined).
+ *
+ * pcr_voxel_map_order: host-only helper behind it -- the iteration order of a
+ * std::unordered_map<size_t,...> after inserting the n distinct keys in order:
+ * order[k] = insertion rank of the k-th visited key.
+ *
+ * pcr_radius_count / pcr_radius_neighbors replace cpp_neighbors.batch_query
+ * (cpp_neighbors/wrapper.cpp:63-230 -> batch_nanoflann_neighbors,
+ * neighbors/neighbors.cpp:211-332).
+ *   queries (nq,3), supports (ns,3) f32 device; q_batches / s_batches (nb) HOST.
+ *   Neighbours of a query: supports of its batch with f32
+ *   (dx*dx + dy*dy) + dz*dz < radius*radius, by ascending distance (equal
+ *   distances by ascending index), as global support indices.  counts (nq)
+ *   device (optional) and *max_count (HOST) = the reference's row width.
+ *   pcr_radius_neighbors writes out (nq,width) int32 device: the first `width`
+ *   neighbours of each query, padded with ns (supports.size()); width =
+ *   max_count is batch_query, min(max_count, max_nn) is dataloader.py
+ *   batch_neighbors (:12-25).  Both synchronize the stream once.
+ * ------------------------------------------------------------------------- */
+int pcr_grid_subsample(const float *points, int32_t n, const int32_t *batch_len, int32_t nb,
+                       const float *features, int32_t fdim, float dl, int32_t max_p,
+                       float *out_points, float *out_features, int32_t *out_batch_len,
+                       int32_t *out_total, pcr_stream_t stream);
+int pcr_voxel_map_order(const uint64_t *keys, int32_t n, int32_t *order);
+int pcr_radius_count(const float *queries, int32_t nq, const float *supports, int32_t ns,
+                     const int32_t *q_batches, const int32_t *s_batches, int32_t nb, float radius,
+                     int32_t *counts, int32_t *max_count, pcr_stream_t stream);
+int pcr_radius_neighbors(const float *queries, int32_t nq, const float *supports, int32_t ns,
+                         const int32_t *q_batches, const int32_t *s_batches, int32_t nb,
+                         float radius, int32_t width, int32_t *out, int32_t *max_count,
+                         pcr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

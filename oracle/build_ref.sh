@@ -13,12 +13,13 @@ set -euo pipefail
 HERE="$(cd "$(dirname "$0")" && pwd)"
 SRC=/root/reference/dip/torch-nndistance/src/my_lib.cpp
 OUT="$HERE/_ref/torch_nndistance_ref$(python3 -c 'import sysconfig;print(sysconfig.get_config_var("EXT_SUFFIX"))')"
+mkdir -p "$HERE/_ref"
+build_nnd() {
 if [ ! -f "$SRC" ]; then
   echo "reference source $SRC absent (expected on the GPU box); keeping prebuilt $OUT" >&2
-  exit 0
+  return 0
 fi
-mkdir -p "$HERE/_ref"
-if [ -f "$OUT" ] && [ "$OUT" -nt "$SRC" ] && [ "$OUT" -nt "$0" ]; then exit 0; fi
+if [ -f "$OUT" ] && [ "$OUT" -nt "$SRC" ] && [ "$OUT" -nt "$0" ]; then return 0; fi
 TORCH_DIR=$(python3 -c 'import torch,os;print(os.path.dirname(torch.__file__))')
 PYINC=$(python3 -c 'import sysconfig;print(sysconfig.get_paths()["include"])')
 PYBIND=$(python3 -c 'import pybind11;print(pybind11.get_include())')
@@ -33,3 +34,25 @@ g++ -O2 -std=c++17 -fPIC -shared -w \
   -L"$TORCH_DIR/lib" -lc10 -ltorch -ltorch_cpu -ltorch_python \
   -Wl,-rpath,"$TORCH_DIR/lib"
 echo "built $OUT"
+}
+build_nnd
+
+# --- KPConv helpers (c2p-net/ngenet/cpp_wrappers), SURVEY 8(f) row f2 -------------
+# The reference's grid_subsampling.cpp / neighbors.cpp / cloud.cpp compiled in place
+# with its own setup.py flags; oracle/ref_kpconv.cpp (ours) is the C-ABI marshalling
+# that replaces the CPython wrapper.cpp files (they do not compile against numpy 2).
+KP=/root/reference/c2p-net/ngenet/cpp_wrappers
+KPOUT="$HERE/_ref/libref_kpconv.so"
+if [ -d "$KP" ]; then
+  if [ ! -f "$KPOUT" ] || [ "$HERE/ref_kpconv.cpp" -nt "$KPOUT" ] || [ "$0" -nt "$KPOUT" ]; then
+    g++ -O2 -std=c++11 -D_GLIBCXX_USE_CXX11_ABI=0 -fPIC -shared -w \
+      -I"$KP/cpp_utils" -I"$KP/cpp_subsampling" -I"$KP/cpp_neighbors" \
+      "$HERE/ref_kpconv.cpp" "$KP/cpp_subsampling/grid_subsampling/grid_subsampling.cpp" \
+      "$KP/cpp_neighbors/neighbors/neighbors.cpp" "$KP/cpp_utils/cloud/cloud.cpp" \
+      -o "$KPOUT"
+    echo "built $KPOUT"
+  fi
+else
+  echo "reference KPConv sources absent; keeping prebuilt $KPOUT" >&2
+fi
+

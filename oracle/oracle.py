@@ -262,3 +262,106 @@ def ndp_warp(levels, x, k0=-8, max_level=None, min_level=0):
         x, nr = ndp_level(levels[i], x, i + 1, k0)
         data[i] = (x, nr)
     return x, data
+
+
+# ---------------------------------------------------------------------------
+# f2: KPConv grid subsampling / radius neighbours (ngenet/cpp_wrappers)
+# ---------------------------------------------------------------------------
+
+def _size_t(f):
+    """(size_t)f for float32 f as g++ emits it on x86-64: below 2^63 through the
+    signed conversion, so -1.0f -> 2^64 - 1 (cvttss2si)."""
+    f = np.asarray(f, np.float32)
+    return f.astype(np.float64).astype(np.int64).view(np.uint64)
+
+
+def voxel_keys(points, dl):
+    """Per-point mapIdx of one cloud, grid_subsampling.cpp:17-54, in float32:
+    origin = floor(min * (1/dl)) * dl, iX = (size_t)floor((x - origin.x) / dl),
+    mapIdx = iX + NX*iY + NX*NY*iZ in size_t (wrapping) arithmetic."""
+    p = np.asarray(points, np.float32).reshape(-1, 3)
+    dl = np.float32(dl)
+    inv = np.float32(1.0) / dl
+    mn, mx = p.min(0), p.max(0)  # cloud.cpp:27-68 (finite inputs)
+    org = (np.floor(mn * inv) * dl).astype(np.float32)
+    nx = _size_t(np.floor((mx[0] - org[0]) / dl)) + np.uint64(1)
+    ny = _size_t(np.floor((mx[1] - org[1]) / dl)) + np.uint64(1)
+    i = _size_t(np.floor((p - org) / dl))
+    with np.errstate(over="ignore"):
+        return (i[:, 0] + nx * i[:, 1]) + (nx * ny) * i[:, 2]
+
+
+def grid_subsample(points, batches, dl, features=None, max_p=0, order=None):
+    """batch_grid_subsampling (grid_subsampling.cpp:109-211) restated with numpy.
+
+    Voxel sums are float32 additions in input order (np.add.at is sequential,
+    SampledData::update_* :41-79), barycentre = sum * float32(1.0 / count),
+    features f / float32(count) (:86-95).  The emission order of the reference
+    is the iteration order of its unordered_map; `order(keys)` must return it
+    for the distinct keys given in first-occurrence order (e.g. the product's
+    pcr_voxel_map_order, itself checked against the compiled reference);
+    without it voxels come out in first-occurrence order."""
+    p = np.asarray(points, np.float32).reshape(-1, 3)
+    f = None if features is None else np.asarray(features, np.float32).reshape(p.shape[0], -1)
+    bl = np.asarray(batches, np.int64).reshape(-1)
+    cap = p.shape[0] if max_p < 1 else int(max_p)
+    out_p, out_f, out_len = [], [], []
+    o = 0
+    for L in bl:
+        bp = p[o:o + L]
+        if L == 0:
+            out_len.append(0)
+            continue
+        keys = voxel_keys(bp, dl)
+        uk, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+        rank = np.argsort(first, kind="stable")           # voxel ids in first-occurrence order
+        vox_of_rank = rank
+        sums = np.zeros((len(uk), 3), np.float32)
+        np.add.at(sums, inv.reshape(-1), bp)
+        cnt = np.bincount(inv.reshape(-1), minlength=len(uk))
+        seq = np.arange(len(uk)) if order is None else np.asarray(order(uk[vox_of_rank]))
+        sel = vox_of_rank[seq][:cap]
+        scale = (1.0 / cnt[sel].astype(np.float64)).astype(np.float32)
+        out_p.append(sums[sel] * scale[:, None])
+        if f is not None:
+            fs = np.zeros((len(uk), f.shape[1]), np.float32)
+            np.add.at(fs, inv.reshape(-1), f[o:o + L])
+            out_f.append(fs[sel] / cnt[sel].astype(np.float32)[:, None])
+        out_len.append(len(sel))
+        o += L
+    P = np.concatenate(out_p) if out_p else np.zeros((0, 3), np.float32)
+    res = (P, np.asarray(out_len, np.int32))
+    if f is not None:
+        res = res + (np.concatenate(out_f) if out_f else np.zeros((0, f.shape[1]), np.float32),)
+    return res
+
+
+def radius_neighbors(queries, supports, q_batches, s_batches, radius):
+    """batch_nanoflann_neighbors (neighbors.cpp:211-332) restated brute force:
+    per query, the supports of its batch with float32 ((dx*dx + dy*dy) + dz*dz)
+    < radius*radius (L2_Simple_Adaptor::evalMetric, RadiusResultSet::addPoint),
+    ascending distance, equal distances by index, padded with len(supports).
+    Returns (rows (nq, max_count) int32, distances as a list of arrays)."""
+    q = np.asarray(queries, np.float32).reshape(-1, 3)
+    s = np.asarray(supports, np.float32).reshape(-1, 3)
+    qb = np.asarray(q_batches, np.int64)
+    sb = np.asarray(s_batches, np.int64)
+    r2 = np.float32(radius) * np.float32(radius)
+    rows, dists = [], []
+    qo = so = 0
+    for b in range(len(qb)):
+        S = s[so:so + sb[b]]
+        for i in range(qo, qo + qb[b]):
+            d = q[i] - S
+            dd = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+            j = np.nonzero(dd < r2)[0]
+            o = np.lexsort((j, dd[j]))
+            rows.append(j[o] + so)
+            dists.append(dd[j][o])
+        qo += qb[b]
+        so += sb[b]
+    mc = max((len(r) for r in rows), default=0)
+    out = np.full((len(rows), mc), s.shape[0], np.int32)
+    for i, r in enumerate(rows):
+        out[i, :len(r)] = r
+    return out, dists

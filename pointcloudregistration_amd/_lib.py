@@ -66,6 +66,10 @@ SIGNATURES = {
     "pcr_lrf_count": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _p, _p],
     "pcr_lrf_compute": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _i32, _p, _i32, _p, _p, _p, _p],
     "pcr_ndp_warp": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
+    "pcr_grid_subsample": [_p, _i32, _p, _i32, _p, _i32, _f32, _i32, _p, _p, _p, _p, _p],
+    "pcr_voxel_map_order": [_p, _i32, _p],
+    "pcr_radius_count": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _p, _p, _p],
+    "pcr_radius_neighbors": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _i32, _p, _p, _p],
 }
 
 
