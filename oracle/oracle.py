@@ -341,7 +341,11 @@ def radius_neighbors(queries, supports, q_batches, s_batches, radius):
     per query, the supports of its batch with float32 ((dx*dx + dy*dy) + dz*dz)
     < radius*radius (L2_Simple_Adaptor::evalMetric, RadiusResultSet::addPoint),
     ascending distance, equal distances by index, padded with len(supports).
-    Returns (rows (nq, max_count) int32, distances as a list of arrays)."""
+    Returns (rows (nq, max_count) int32, distances as a list of arrays).
+    Not restated: the reference's order among EQUAL distances (nanoflann's
+    leaf-visit order permuted by std::sort, neighbors.cpp:298 via
+    nanoflann.hpp radiusSearch) -- tie-bearing cases are checked against the
+    compiled reference (oracle/_ref/libref_kpconv.so) instead."""
     q = np.asarray(queries, np.float32).reshape(-1, 3)
     s = np.asarray(supports, np.float32).reshape(-1, 3)
     qb = np.asarray(q_batches, np.int64)

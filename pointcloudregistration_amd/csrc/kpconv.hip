@@ -26,19 +26,29 @@
 // RadiusResultSet::addPoint: strict), counts them (pass 1), writes
 // (d bits, index) keys (pass 2) that a segmented radix sort orders by
 // ascending distance, and the rows are padded with supports.size().
-// Equal distances are ordered by index; the reference leaves them in nanoflann's
-// tree-traversal order as permuted by std::sort (not stable), which no
-// tree-free search can reproduce -- see DESIGN.md "f2".
+// Equal distances come out of the reference in nanoflann's leaf-visit order as
+// permuted by std::sort (not stable), and its float box-distance pruning could
+// drop a point within ulps of the radius: the GPU flags rows holding a distance
+// tie or a near-radius distance, and the host recomputes exactly those rows with
+// the reference's tree (kdreplay.cpp).  Every other row is decided by distance
+// alone, so the (distance, index) sort gives the reference's order.
 #include "pcr_internal.h"
 
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
 
+#include <algorithm>
+#include <iterator>
 #include <unordered_map>
 #include <vector>
 
 namespace pcr {
+
+// kdreplay.cpp
+void kd_replay_rows(const float *q, const float *s, const int *soff, const std::vector<int> &rows,
+                    const std::vector<int> &qbatch, float r2, std::vector<std::vector<int>> &res);
+
 namespace {
 
 typedef unsigned long long u64;
@@ -243,6 +253,9 @@ struct RnArgs {
     const unsigned *offs;    // [nq+1] exclusive scan of counts
     u64 *keys;               // [total]
     int ibits;
+    float r2lo;              // d in [r2lo, r2): near-radius row, replayed on the host
+    int *bcnt, *blist;       // near-radius rows (pass 1)
+    int *tcnt, *tlist;       // rows with an equal-distance pair (after the sort)
 };
 
 constexpr double kCoordLimit = 1073741824.0;  // 2^30
@@ -300,12 +313,14 @@ __global__ __launch_bounds__(256) void rn_query(RnArgs a) {
     const float *qp = a.q + 3 * (size_t)qi;
     const float qx = qp[0], qy = qp[1], qz = qp[2];
     int cnt = 0;
+    bool edge = false;
     u64 *out = nullptr;
     if (FILL) out = a.keys + a.offs[qi];
     auto take = [&](float d, int j) {
         if (live && d < a.r2) {
             if (FILL) out[cnt] = ((u64)__float_as_uint(d) << a.ibits) | (u64)(unsigned)j;
             ++cnt;
+            edge |= d >= a.r2lo;
         }
     };
     int cx, cy, cz;
@@ -336,12 +351,28 @@ __global__ __launch_bounds__(256) void rn_query(RnArgs a) {
         }
     }
     if (!FILL) {
+        if (live && edge) a.blist[atomicAdd(a.bcnt, 1)] = qi;
         if (live) a.counts[qi] = cnt;
         atomicMax(a.maxcnt, cnt);
         u64 t = (u64)cnt;
         for (int o = 32; o; o >>= 1) t += __shfl_xor(t, o, 64);
         if ((threadIdx.x & 63) == 0) atomicAdd(a.total, t);
     }
+}
+
+// rows whose sorted keys hold two equal distances (d > 0: the reference's own
+// order decides them)
+__global__ void rn_ties(const u64 *keys, const unsigned *offs, const int *counts, int nq, int ibits,
+                        int *tcnt, int *tlist) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const u64 *k = keys + offs[q];
+    const int c = counts[q];
+    for (int j = 1; j < c; ++j)
+        if ((k[j] >> ibits) == (k[j - 1] >> ibits)) {
+            tlist[atomicAdd(tcnt, 1)] = q;
+            return;
+        }
 }
 
 __global__ void rn_emit(const u64 *keys, const unsigned *offs, const int *counts, int nq, int width,
@@ -396,6 +427,7 @@ int rn_prepare(const float *q, int nq, const float *s, int ns, const int32_t *qb
     a = RnArgs{};
     a.q = q; a.s = s; a.nq = nq; a.ns = ns; a.nb = nb;
     a.r2 = radius * radius;  // neighbors.cpp :226, f32
+    a.r2lo = (float)((double)a.r2 * (1.0 - 1.0 / 131072.0));
     const double cell = fabs((double)radius) * (1.0 + 1e-6);
     a.ic = (a.r2 > 0.0f && cell < 1e300) ? 1.0 / cell : 0.0;
     int S = 1024;
@@ -403,15 +435,17 @@ int rn_prepare(const float *q, int nq, const float *s, int ns, const int32_t *qb
     a.S = S;
     a.ibits = (int)nbits((u64)(ns > 0 ? ns : 1));
     Carver c;
-    const size_t o_off = c.take<int>(2 * (nb + 1)), o_hdr = c.take<u64>(2), o_h = c.take<int>(S + 1),
+    const size_t o_off = c.take<int>(2 * (nb + 1)), o_hdr = c.take<u64>(3), o_h = c.take<int>(S + 1),
                  o_st = c.take<int>(S + 1), o_pts = c.take<float4>(ns), o_cnt = c.take<int>(nq),
-                 o_offs = c.take<unsigned>(nq + 1);
+                 o_offs = c.take<unsigned>(nq + 1), o_bl = c.take<int>(nq), o_tl = c.take<int>(nq);
     char *ws = (char *)workspace(18, c.used);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "radius_neighbors: %s", pcr_last_error());
     int *dev_off = (int *)(ws + o_off);
     a.qoff = dev_off; a.soff = dev_off + nb + 1;
     a.total = (u64 *)(ws + o_hdr);
     a.bad = (int *)(a.total + 1); a.maxcnt = a.bad + 1;
+    a.bcnt = (int *)(a.total + 2); a.tcnt = a.bcnt + 1;
+    a.blist = (int *)(ws + o_bl); a.tlist = (int *)(ws + o_tl);
     a.hcnt = (int *)(ws + o_h); a.start = (int *)(ws + o_st);
     a.cell_pts = (float4 *)(ws + o_pts);
     a.counts = (int *)(ws + o_cnt);
@@ -419,7 +453,7 @@ int rn_prepare(const float *q, int nq, const float *s, int ns, const int32_t *qb
     std::vector<int> offs(P.qoff);
     offs.insert(offs.end(), P.soff.begin(), P.soff.end());
     PCR_HIP_CHECK(hipMemcpyAsync(dev_off, offs.data(), sizeof(int) * offs.size(), hipMemcpyHostToDevice, st));
-    PCR_HIP_CHECK(hipMemsetAsync(a.total, 0, 2 * sizeof(u64), st));
+    PCR_HIP_CHECK(hipMemsetAsync(a.total, 0, 3 * sizeof(u64), st));
     size_t tb = 0, tb2 = 0;
     PCR_HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, a.hcnt, a.start, 0, (size_t)S + 1,
                                           rocprim::plus<int>(), st));
@@ -445,6 +479,56 @@ int rn_prepare(const float *q, int nq, const float *s, int ns, const int32_t *qb
         hipLaunchKernelGGL(rn_query<false>, dim3((nq + 255) / 256), dim3(256), 0, st, a);
         PCR_LAUNCH_CHECK();
     }
+    return PCR_OK;
+}
+
+// host copies of the queries / supports, fetched only when a row needs the replay
+struct RnHost {
+    std::vector<float> q, s;
+    bool loaded = false;
+};
+
+int rn_fetch(const RnPlan &P, hipStream_t st, RnHost &H) {
+    if (H.loaded) return PCR_OK;
+    H.q.resize(3 * (size_t)P.a.nq);
+    H.s.resize(3 * (size_t)P.a.ns);
+    if (P.a.nq) PCR_HIP_CHECK(hipMemcpyAsync(H.q.data(), P.a.q, 12 * (size_t)P.a.nq, hipMemcpyDeviceToHost, st));
+    if (P.a.ns) PCR_HIP_CHECK(hipMemcpyAsync(H.s.data(), P.a.s, 12 * (size_t)P.a.ns, hipMemcpyDeviceToHost, st));
+    PCR_HIP_CHECK(hipStreamSynchronize(st));
+    H.loaded = true;
+    return PCR_OK;
+}
+
+// the reference's neighbour lists of `rows` (ascending), recomputed on the host
+int rn_replay(const RnPlan &P, hipStream_t st, RnHost &H, const std::vector<int> &rows,
+              std::vector<std::vector<int>> &res) {
+    const int rc = rn_fetch(P, st, H);
+    if (rc != PCR_OK) return rc;
+    std::vector<int> qb(rows.size());
+    for (size_t k = 0; k < rows.size(); ++k)
+        qb[k] = (int)(std::upper_bound(P.qoff.begin(), P.qoff.end(), rows[k]) - P.qoff.begin()) - 1;
+    kd_replay_rows(H.q.data(), H.s.data(), P.soff.data(), rows, qb, P.a.r2, res);
+    return PCR_OK;
+}
+
+// pass-1 epilogue: exact counts of the near-radius rows and the reference's
+// max_count (hdr = the synchronized header)
+int rn_boundary(const RnPlan &P, hipStream_t st, const u64 *hdr, RnHost &H, std::vector<int> &rows,
+                std::vector<std::vector<int>> &res, int &max_count) {
+    max_count = (int)(hdr[1] >> 32);
+    rows.assign((size_t)(hdr[2] & 0xffffffffu), 0);
+    res.clear();
+    if (rows.empty()) return PCR_OK;
+    std::vector<int> cnt((size_t)P.a.nq);
+    PCR_HIP_CHECK(hipMemcpyAsync(rows.data(), P.a.blist, sizeof(int) * rows.size(), hipMemcpyDeviceToHost, st));
+    PCR_HIP_CHECK(hipMemcpyAsync(cnt.data(), P.a.counts, sizeof(int) * cnt.size(), hipMemcpyDeviceToHost, st));
+    PCR_HIP_CHECK(hipStreamSynchronize(st));
+    std::sort(rows.begin(), rows.end());
+    const int rc = rn_replay(P, st, H, rows, res);
+    if (rc != PCR_OK) return rc;
+    for (size_t k = 0; k < rows.size(); ++k) cnt[rows[k]] = (int)res[k].size();
+    max_count = 0;
+    for (int c : cnt) max_count = c > max_count ? c : max_count;
     return PCR_OK;
 }
 
@@ -612,10 +696,24 @@ extern "C" int pcr_radius_count(const float *queries, int32_t nq, const float *s
     if (rc != PCR_OK) return rc;
     if (counts && nq > 0)
         PCR_HIP_CHECK(hipMemcpyAsync(counts, P.a.counts, sizeof(int) * nq, hipMemcpyDeviceToDevice, st));
-    u64 hdr[2];
+    u64 hdr[3];
     PCR_HIP_CHECK(hipMemcpyAsync(hdr, P.a.total, sizeof(hdr), hipMemcpyDeviceToHost, st));
     PCR_HIP_CHECK(hipStreamSynchronize(st));
-    *max_count = (int)(hdr[1] >> 32);
+    RnHost H;
+    std::vector<int> brows;
+    std::vector<std::vector<int>> bres;
+    int mc = 0;
+    const int rb = rn_boundary(P, st, hdr, H, brows, bres, mc);
+    if (rb != PCR_OK) return rb;
+    *max_count = mc;
+    if (counts && !brows.empty()) {
+        std::vector<int> bc(brows.size());
+        for (size_t k = 0; k < brows.size(); ++k) {
+            bc[k] = (int)bres[k].size();
+            PCR_HIP_CHECK(hipMemcpyAsync(counts + brows[k], &bc[k], sizeof(int), hipMemcpyHostToDevice, st));
+        }
+        PCR_HIP_CHECK(hipStreamSynchronize(st));
+    }
     return PCR_OK;
 }
 
@@ -630,11 +728,17 @@ extern "C" int pcr_radius_neighbors(const float *queries, int32_t nq, const floa
     RnPlan P;
     int rc = rn_prepare(queries, nq, supports, ns, q_batches, s_batches, nb, radius, st, P);
     if (rc != PCR_OK) return rc;
-    u64 hdr[2];
+    u64 hdr[3];
     PCR_HIP_CHECK(hipMemcpyAsync(hdr, P.a.total, sizeof(hdr), hipMemcpyDeviceToHost, st));
     PCR_HIP_CHECK(hipStreamSynchronize(st));
     const u64 total = hdr[0];
-    if (max_count) *max_count = (int)(hdr[1] >> 32);
+    RnHost H;
+    std::vector<int> brows;
+    std::vector<std::vector<int>> bres;
+    int mc = 0;
+    rc = rn_boundary(P, st, hdr, H, brows, bres, mc);
+    if (rc != PCR_OK) return rc;
+    if (max_count) *max_count = mc;
     const size_t cells = (size_t)nq * width;
     if (cells == 0) return PCR_OK;
     PCR_REQUIRE(total < 0xFFFFFFFFull, PCR_ERR_ARG, "radius_neighbors: %llu neighbour pairs exceed 2^32",
@@ -661,9 +765,41 @@ extern "C" int pcr_radius_neighbors(const float *queries, int32_t nq, const floa
         PCR_HIP_CHECK(rocprim::segmented_radix_sort_keys(ws + o_t, tb, (const u64 *)P.a.keys, keys2,
                                                          (unsigned)total, (unsigned)nq, P.a.offs, P.a.offs + 1,
                                                          0u, ebit, st));
+        hipLaunchKernelGGL(rn_ties, dim3((nq + 255) / 256), dim3(256), 0, st, (const u64 *)keys2, P.a.offs,
+                           (const int *)P.a.counts, nq, P.a.ibits, P.a.tcnt, P.a.tlist);
+        PCR_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(rn_emit, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, keys2, P.a.offs,
                        P.a.counts, nq, width, ns, (unsigned)((1ull << P.a.ibits) - 1), out);
     PCR_LAUNCH_CHECK();
+    if (total == 0) return PCR_OK;
+    // rows the distance sort cannot decide: the reference's own order, from the host
+    int ntie = 0;
+    PCR_HIP_CHECK(hipMemcpyAsync(&ntie, P.a.tcnt, sizeof(int), hipMemcpyDeviceToHost, st));
+    PCR_HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<int> rows(brows);
+    std::vector<std::vector<int>> res(bres);
+    if (ntie > 0) {
+        std::vector<int> trows((size_t)ntie);
+        PCR_HIP_CHECK(hipMemcpyAsync(trows.data(), P.a.tlist, sizeof(int) * trows.size(), hipMemcpyDeviceToHost, st));
+        PCR_HIP_CHECK(hipStreamSynchronize(st));
+        std::sort(trows.begin(), trows.end());
+        std::vector<int> extra;
+        std::set_difference(trows.begin(), trows.end(), brows.begin(), brows.end(), std::back_inserter(extra));
+        std::vector<std::vector<int>> eres;
+        rc = rn_replay(P, st, H, extra, eres);
+        if (rc != PCR_OK) return rc;
+        rows.insert(rows.end(), extra.begin(), extra.end());
+        res.insert(res.end(), eres.begin(), eres.end());
+    }
+    if (rows.empty()) return PCR_OK;
+    std::vector<int32_t> rowbuf(rows.size() * (size_t)width);
+    for (size_t k = 0; k < rows.size(); ++k) {
+        int32_t *r = rowbuf.data() + k * width;
+        for (int j = 0; j < width; ++j) r[j] = j < (int)res[k].size() ? res[k][j] : ns;
+        PCR_HIP_CHECK(hipMemcpyAsync(out + (size_t)rows[k] * width, r, sizeof(int32_t) * width,
+                                     hipMemcpyHostToDevice, st));
+    }
+    PCR_HIP_CHECK(hipStreamSynchronize(st));
     return PCR_OK;
 }

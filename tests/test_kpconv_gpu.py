@@ -175,6 +175,30 @@ def test_batch_query_random_against_reference(K, oracle):
         assert np.array_equal(got, want), t
 
 
+def test_batch_query_ties_against_reference(K):
+    """Quantised clouds: most rows hold equal distances, whose order is the
+    reference's nanoflann leaf-visit order through std::sort (replayed on the host)."""
+    R = _ref()
+    if R is None:
+        pytest.skip("oracle/_ref/libref_kpconv.so not available")
+    rng = np.random.default_rng(9)
+    for t in range(5):
+        nb = int(rng.integers(1, 4))
+        ss = rng.integers(1, 6000, nb)
+        qs = rng.integers(1, 3000, nb)
+        s = np.concatenate([np.round(rng.uniform(-1, 1, (k, 3)) * 16) / 16 for k in ss]).astype(np.float32)
+        q = np.concatenate([np.round(rng.uniform(-1.1, 1.1, (k, 3)) * 16) / 16 for k in qs]).astype(np.float32)
+        r = float(rng.uniform(0.1, 0.3))
+        try:
+            want = R.batch_query(q, s, qs, ss, radius=r)
+        except RuntimeError:
+            continue
+        got = K.batch_query(q, s, qs, ss, radius=r)
+        assert np.array_equal(got, want), t
+        got7 = K.batch_neighbors(q, s, qs, ss, r, 7).numpy()
+        assert np.array_equal(got7, want[:, :7]), t
+
+
 def test_batch_neighbors_truncation_and_device(K):
     c = nb_case("nb_self")
     full = K.batch_query(c["queries"], c["supports"], c["q_batches"], c["s_batches"], radius=c["radius"])
