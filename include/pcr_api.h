@@ -183,6 +183,13 @@ int pcr_procrustes_batch(const float *src, const float *tgt, const float *weight
                          int32_t N, int32_t abs_weights, double eps, double *T,
                          pcr_stream_t stream);
 
+/* out (B,N,3) f32 = (float)(R p + t) in f64 for each item's T (B,16) f64
+ * row-major 4x4 (registration outputs).  Replaces the per-pair
+ * source.transform(T) (Open3D PointCloud::Transform, RANSAC.py / QualityCheck.py)
+ * before the Chamfer check. */
+int pcr_transform_batch(const float *xyz, int32_t B, int32_t N, const double *T, float *out,
+                        pcr_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * a4 -- DIP local reference frames, batched.  Replaces lrf.get
  * (dip/lrf.py:19-78) called per sampled point by dip/demo.py:109-114.
@@ -275,6 +282,41 @@ int pcr_radius_neighbors(const float *queries, int32_t nq, const float *supports
                          const int32_t *q_batches, const int32_t *s_batches, int32_t nb,
                          float radius, int32_t width, int32_t *out, int32_t *max_count,
                          pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * f1 -- normal estimation and FPFH, the preprocessing of
+ * DataPreparation/RANSAC.py:12-22 (Open3D 0.13 PointCloud::estimate_normals
+ * with KDTreeSearchParamHybrid(4 voxel, 30) and
+ * pipelines.registration.compute_fpfh_feature with
+ * KDTreeSearchParamHybrid(7 voxel, 100)), batched over P clouds.
+ * Semantics restated in oracle/fpfh_oracle.c (Open3D absent: parity vs the
+ * reference unpinned; GPU == restatement bit for bit).
+ *
+ * pcr_hybrid_search replaces KDTreeFlann::SearchHybrid(points[i], radius,
+ *   max_nn) for every point of every cloud: the max_nn nearest points with
+ *   f64 (dx*dx + dy*dy) + dz*dz < (double)(float)(radius^2), ascending
+ *   (d2, index).  idx (P,Nmax,max_nn) local indices (-1 padded), d2 same shape
+ *   f64, counts (P,Nmax).  1 <= max_nn <= 448.
+ * pcr_estimate_normals: normals (P,Nmax,3) f64 (ComputeCovariance over the
+ *   hybrid neighbourhood incl. the point, FastEigen3x3 smallest eigenvector;
+ *   < 3 neighbours -> (0,0,1)).  prior_normals (P,Nmax,3) f64 or NULL: when
+ *   given (the cloud already had normals) each result is flipped to agree
+ *   with it, and a zero result takes it (EstimateNormals' has_normal branch).
+ * pcr_compute_fpfh: fpfh (P,Nmax,33) f64 = Open3D's Feature::data_ (33, N)
+ *   column-major; fpfh_f32 (optional) the same rounded to f32 (the input of
+ *   pcr_feature_match); spfh (optional) the intermediate SPFH histograms.
+ * Clouds are xyz (P,Nmax,3) f32 with n_pts (P) valid points (NULL = Nmax);
+ * rows past a cloud's count are left untouched.
+ * ------------------------------------------------------------------------- */
+int pcr_hybrid_search(const float *xyz, int32_t P, int32_t Nmax, const int32_t *n_pts,
+                      double radius, int32_t max_nn, int32_t *idx, double *d2, int32_t *counts,
+                      pcr_stream_t stream);
+int pcr_estimate_normals(const float *xyz, int32_t P, int32_t Nmax, const int32_t *n_pts,
+                         double radius, int32_t max_nn, const double *prior_normals,
+                         double *normals, pcr_stream_t stream);
+int pcr_compute_fpfh(const float *xyz, const double *normals, int32_t P, int32_t Nmax,
+                     const int32_t *n_pts, double radius, int32_t max_nn, double *fpfh,
+                     float *fpfh_f32, double *spfh, pcr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -369,3 +369,92 @@ def radius_neighbors(queries, supports, q_batches, s_batches, radius):
     for i, r in enumerate(rows):
         out[i, :len(r)] = r
     return out, dists
+
+
+# --------------------------------------------------------------------------
+# f1: normals + FPFH (fpfh_oracle.c; Open3D restated, parity vs Open3D unpinned)
+# --------------------------------------------------------------------------
+
+def _fpfh_sigs():
+    Lb = lib()
+    c = ctypes
+    for f in ("oracle_det_acos", "oracle_det_cos"):
+        getattr(Lb, f).restype = c.c_double
+        getattr(Lb, f).argtypes = [c.c_double]
+    Lb.oracle_det_atan2.restype = c.c_double
+    Lb.oracle_det_atan2.argtypes = [c.c_double, c.c_double]
+    Lb.oracle_hybrid_search.argtypes = [c.c_void_p, c.c_int, c.c_double, c.c_int, c.c_void_p,
+                                        c.c_void_p, c.c_void_p]
+    Lb.oracle_estimate_normals.argtypes = [c.c_void_p, c.c_int, c.c_double, c.c_int, c.c_void_p,
+                                           c.c_void_p]
+    Lb.oracle_fpfh.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_double, c.c_int, c.c_void_p,
+                               c.c_void_p]
+    Lb.oracle_fast_eigen3x3.argtypes = [c.c_void_p, c.c_void_p]
+    Lb.oracle_pair_features.argtypes = [c.c_void_p] * 5
+    return Lb
+
+
+_fs = None
+
+
+def FL():
+    global _fs
+    if _fs is None:
+        _fs = _fpfh_sigs()
+    return _fs
+
+
+def det_atan2(y, x):
+    return FL().oracle_det_atan2(float(y), float(x))
+
+
+def det_acos(x):
+    return FL().oracle_det_acos(float(x))
+
+
+def det_cos(x):
+    return FL().oracle_det_cos(float(x))
+
+
+def hybrid_search(pts, radius, max_nn):
+    """KDTreeFlann::SearchHybrid(points[i], radius, max_nn) for every point:
+    (idx (n,K) int32 -1 padded, d2 (n,K) f64, counts (n,))."""
+    p = _f32(pts).reshape(-1, 3)
+    n = p.shape[0]
+    idx = np.zeros((n, max_nn), np.int32)
+    d2 = np.zeros((n, max_nn), np.float64)
+    cnt = np.zeros(n, np.int32)
+    FL().oracle_hybrid_search(_p(p), n, float(radius), int(max_nn), _p(idx), _p(d2), _p(cnt))
+    return idx, d2, cnt
+
+
+def estimate_normals(pts, radius, max_nn, prior=None):
+    p = _f32(pts).reshape(-1, 3)
+    out = np.zeros((p.shape[0], 3), np.float64)
+    pr = None if prior is None else _f64(prior).reshape(-1, 3)
+    FL().oracle_estimate_normals(_p(p), p.shape[0], float(radius), int(max_nn),
+                                 None if pr is None else _p(pr), _p(out))
+    return out
+
+
+def fpfh(pts, normals, radius, max_nn):
+    """(spfh (n,33), fpfh (n,33)) f64 (Open3D Feature::data_ transposed)."""
+    p = _f32(pts).reshape(-1, 3)
+    nm = _f64(normals).reshape(-1, 3)
+    sp = np.zeros((p.shape[0], 33), np.float64)
+    fp = np.zeros((p.shape[0], 33), np.float64)
+    FL().oracle_fpfh(_p(p), _p(nm), p.shape[0], float(radius), int(max_nn), _p(sp), _p(fp))
+    return sp, fp
+
+
+def fast_eigen3x3(C):
+    C = _f64(C).reshape(9)
+    v = np.zeros(3, np.float64)
+    FL().oracle_fast_eigen3x3(_p(C), _p(v))
+    return v
+
+
+def pair_features(p1, n1, p2, n2):
+    f = np.zeros(4, np.float64)
+    FL().oracle_pair_features(_p(_f64(p1)), _p(_f64(n1)), _p(_f64(p2)), _p(_f64(n2)), _p(f))
+    return f
