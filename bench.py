@@ -217,6 +217,76 @@ def measure_ndp(with_cpu):
     return res
 
 
+def measure_fpfh(with_cpu):
+    """f1 on the C1 shape (DataPreparation/RANSAC.py:12-64, voxel 0.01: normals
+    r 0.04 / 30, FPFH r 0.07 / 100, feature RANSAC d 0.04 mutual, ICP d 0.02) for
+    one 1024-point pair, end to end through the Open3D-shaped drop-ins; plus the
+    batched normals+FPFH kernels on 64 clouds x 8192 points (C4 cloud shape)."""
+    from pointcloudregistration_amd import features as F
+    from pointcloudregistration_amd import registration as reg
+    from pointcloudregistration_amd import synth
+    rng = np.random.default_rng(1)
+    tgt = (synth.surface_points(rng, 1024) * 0.5).astype(np.float32)
+    R = synth.rotation_xyz(*np.deg2rad(rng.uniform(-90, 90, 3)))
+    t = rng.uniform(-1.5, 1.5, 3)
+    src = ((tgt.astype(np.float64) @ R.T + t)
+           + np.clip(rng.normal(0, 0.001, tgt.shape), -0.005, 0.005)).astype(np.float32)
+    voxel, d = 0.01, 0.04
+
+    def c1():
+        s_pcd, t_pcd = reg.PointCloud(src), reg.PointCloud(tgt)
+        s_pcd, s_f = F.preprocess_point_cloud(s_pcd, voxel)
+        t_pcd, t_f = F.preprocess_point_cloud(t_pcd, voxel)
+        res = reg.registration_ransac_based_on_feature_matching(
+            s_pcd, t_pcd, s_f, t_f, True, d, reg.TransformationEstimationPointToPoint(False), 3,
+            [reg.CorrespondenceCheckerBasedOnEdgeLength(0.9),
+             reg.CorrespondenceCheckerBasedOnDistance(d)],
+            reg.RANSACConvergenceCriteria(100000, 0.999))
+        return reg.registration_icp(s_pcd, t_pcd, 0.02, res.transformation,
+                                    reg.TransformationEstimationPointToPoint())
+    icp = c1()
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        c1()
+    torch.cuda.synchronize()
+    c1_ms = (time.perf_counter() - t0) * 1e3 / reps
+    rre, rte = synth.rre_rte(icp.transformation[None, :3, :3], icp.transformation[None, :3, 3],
+                             R.T[None], (-R.T @ t)[None])
+    # batched kernels: normals (r 0.04, 30) + FPFH (r 0.07, 100) on 64 x 8192 points
+    P, N = 64, 8192
+    clouds = np.stack([synth.surface_points(np.random.default_rng(100 + p), N) for p in range(P)])
+    X = torch.as_tensor(clouds.astype(np.float32), device="cuda")
+
+    def batch():
+        nm = F.estimate_normals_batch(X, 0.04, 30)
+        return F.compute_fpfh_batch(X, nm, 0.07, 100)
+    ms = _events_ms(batch, 3)
+    _, _, cnt = F.hybrid_search_batch(X, 0.07, 100)
+    res = {"workload": "C1 RANSAC.py: 2 x 1024 pts, normals + FPFH + feature RANSAC + ICP (wall "
+                       "clock, host-synchronous drop-ins); batch: 64 x 8192 pts normals + FPFH",
+           "c1_ms_per_pair": c1_ms, "c1_rre_deg": float(rre[0]), "c1_rte": float(rte[0]),
+           "c1_fitness": icp.fitness,
+           "batch_gpu_ms": ms, "batch_points_per_s": P * N / (ms * 1e-3),
+           "batch_median_fpfh_neighbours": float(cnt.float().median().item())}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        t0 = time.perf_counter()
+        ns, nt = O.estimate_normals(src, 4 * voxel, 30), O.estimate_normals(tgt, 4 * voxel, 30)
+        fs = O.fpfh(src, ns, 7 * voxel, 100)[1].astype(np.float32)
+        ft = O.fpfh(tgt, nt, 7 * voxel, 100)[1].astype(np.float32)
+        corr = O.corres(O.featnn(fs, ft), O.featnn(ft, fs), True, 3)
+        o = O.ransac(src, tgt, corr, d, dist_check=d)
+        oi = O.icp(src, tgt, 0.02, o["T"])
+        cpu_ms = (time.perf_counter() - t0) * 1e3
+        res["cpu_baseline"] = {"c1_ms_per_pair": cpu_ms, "cores": 1, "kind": "port",
+                               "sample": "one C1 pair through the oracle (brute-force search)",
+                               "T_icp_bitexact": bool(np.array_equal(oi["T"], icp.transformation))}
+    return res
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -335,7 +405,8 @@ def main():
                                          "rte_max": float(np.max(d_rte))}
     if rank == 0 and world == 1 and not args.no_secondary:
         out["secondary"] = {"a4_lrf": measure_lrf(not args.no_cpu_baseline),
-                            "a10_ndp_warp": measure_ndp(not args.no_cpu_baseline)}
+                            "a10_ndp_warp": measure_ndp(not args.no_cpu_baseline),
+                            "f1_fpfh": measure_fpfh(not args.no_cpu_baseline)}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -87,3 +87,41 @@ extern "C" int pcr_procrustes_batch(const float *src, const float *tgt, const fl
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
+
+// ---------------------------------------------------------------------------
+// apply per-item rigid transforms: out = (float)(R p + t) in f64, T (B,16)
+// row-major 4x4 (the registration outputs).  The pipeline's "transform" stage
+// (aligned source for the Chamfer quality check) -- one fused pass instead of a
+// f64 batched GEMM plus casts.  float4 loads/stores over the flat (B*N*3) array.
+// ---------------------------------------------------------------------------
+namespace pcr {
+namespace {
+__global__ __launch_bounds__(256) void transform_kernel(const float *xyz, int N, const double *T,
+                                                        float *out) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double *M = T + (size_t)b * 16;
+    const float *p = xyz + ((size_t)b * N + i) * 3;
+    double x, y, z;
+    xform12(M, (double)p[0], (double)p[1], (double)p[2], x, y, z);
+    float *o = out + ((size_t)b * N + i) * 3;
+    o[0] = (float)x;
+    o[1] = (float)y;
+    o[2] = (float)z;
+}
+}  // namespace
+}  // namespace pcr
+
+extern "C" int pcr_transform_batch(const float *xyz, int32_t B, int32_t N, const double *T,
+                                   float *out, pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(B >= 0 && N >= 0, PCR_ERR_ARG, "transform_batch: negative size");
+    if (B == 0 || N == 0) return PCR_OK;
+    PCR_REQUIRE(xyz && T && out, PCR_ERR_ARG, "transform_batch: null pointer");
+    PCR_REQUIRE(B <= 65535, PCR_ERR_ARG, "transform_batch: B=%d > 65535", B);
+    hipLaunchKernelGGL(pcr::transform_kernel, dim3((N + 255) / 256, B), dim3(256), 0,
+                       pcr::as_stream(stream), xyz, N, T, out);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}

@@ -10,8 +10,9 @@ Mirrors of the reference's Python-facing functions:
   (c2p-net/ngenet/data/dataloader.py:12-66), returning torch tensors.
 
 Same argument names, defaults and results (subsampled points and features
-bit-identical and in the same order; neighbour rows identical up to the order
-of exactly equal distances, see DESIGN.md "f2"), RuntimeError("Error") on an
+bit-identical and in the same order; neighbour rows identical, including the
+reference's order among exactly equal distances, which the library replays on
+the host for the rows that hold them, see DESIGN.md "f2"), RuntimeError("Error") on an
 empty result like the wrappers.  The work runs in libpcr (pcr_grid_subsample,
 pcr_radius_count / pcr_radius_neighbors); there is no CPU path.  numpy / CPU
 inputs give numpy outputs (as the reference); CUDA tensors stay on the device.

@@ -62,6 +62,7 @@ class PairPipeline:
         self.d2 = torch.empty(self.P, self.M, device=dev)
         self.i1 = torch.empty(self.P, self.N, dtype=torch.int32, device=dev)
         self.i2 = torch.empty(self.P, self.M, dtype=torch.int32, device=dev)
+        self.aligned = torch.empty_like(self.src)
 
     def run(self, time_stages=False):
         ev = None
@@ -81,8 +82,7 @@ class PairPipeline:
         if ev:
             ev[3].record()
         T = ir.transformation
-        aligned = (torch.matmul(self.src.double(), T[:, :3, :3].transpose(1, 2))
-                   + T[:, None, :3, 3]).float().contiguous()
+        aligned = reg.transform_batch(self.src, T, out=self.aligned)
         if ev:
             ev[4].record()
         nndistance.nnd_forward_cuda(aligned, self.tgt, self.d1, self.d2, self.i1, self.i2)

@@ -233,6 +233,19 @@ def icp_batch(src, tgt, init, params: IcpParams, n_src=None, n_tgt=None, want_co
     return BatchResult(T, fr[:, 0], fr[:, 1], st, ct)
 
 
+def transform_batch(xyz, T, out=None):
+    """(P,N,3) f32 points through per-pair T (P,4,4) f64: (float)(R p + t) computed in f64."""
+    X = _batch3(xyz, "xyz")
+    P, N = X.shape[0], X.shape[1]
+    M = _cuda(T, torch.float64, X.device).reshape(P, 16)
+    if out is None:
+        out = torch.empty_like(X)
+    with torch.cuda.device(X.device):
+        _lib.call("pcr_transform_batch", _lib.ptr(X), P, N, _lib.ptr(M), _lib.ptr(out),
+                  _stream(X.device))
+    return out
+
+
 def radius_nn(tgt, queries, r, n_tgt=None, n_q=None):
     """Radius-limited 1-NN of f64 queries (P,Q,3) among targets (P,M,3):
     (idx (P,Q) int32, -1 if none; d2 (P,Q) f64)."""
