@@ -870,86 +870,176 @@ __device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
 }
 
 // role 0: rows (A), role 1: columns (B).  256-thread blocks, one wave per
-// 32-row tile.  The tile is staged through LDS with coalesced loads (scaled,
-// exact); while staging, each element's f16 split is written once into an LDS
-// image of the tile's operand rows (row stride NCH*16 halves), so every lane
-// then emits its NCH 16-byte fragments as plain 16-byte LDS reads (no per-half
-// segment arithmetic).
+// 32-row tile; each tile is staged through LDS with coalesced loads (scaled,
+// exact) and every lane emits its NCH 16-byte operand fragments.
 __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t *n, int Nmax, int D,
                                                   int NCH, int ntiles, int role, Split5 sp,
                                                   const unsigned *mx, f16x8 *Xp, float *nrm,
                                                   unsigned *nmax) {
-    extern __shared__ f16x8 pack_img[];  // 4 waves x 32 operand rows x 2*NCH fragments
+    __shared__ float xs[4][32][65];  // D <= 64 (+1 pad: conflict-free row reads)
     const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
     const int cnt = count_of(n, p, Nmax);
     const int nrows = min(max(cnt - t * 32, 0), 32);
     const float s = pair_scale5(mx[p], sp.T);
     const float *base = X + ((size_t)p * Nmax + (size_t)t * 32) * D;
-    f16x8 *img = pack_img + (size_t)w * 32 * 2 * NCH;
-    _Float16 *im = reinterpret_cast<_Float16 *>(img);
-    const int KS = NCH * 16;  // halves per operand row
+    float (*x)[65] = xs[w];
     // e / D by a 64-bit reciprocal (exact for e < 2^16; 2^32/D + 1 needs 33 bits at D = 1)
     const unsigned long long invD = 0xFFFFFFFFull / (unsigned long long)D + 1ull;
     for (int e = l; e < 32 * D; e += 64) {
         const int r = (int)(((unsigned long long)e * invD) >> 32), k = e - r * D;
-        const float xv = r < nrows ? base[e] * s : 0.0f;
-        const _Float16 hi = (_Float16)xv;
-        const _Float16 lo = (_Float16)(xv - (float)hi);
-        _Float16 *row = im + r * KS;
-        if (role == 0) {
-            const _Float16 h2 = (_Float16)(-2.0f * (float)hi);
-            row[k] = h2;
-            row[D + k] = h2;
-            row[2 * D + k] = (_Float16)(-2.0f * (float)lo);
-        } else {
-            row[k] = hi;
-            row[D + k] = lo;
-            row[2 * D + k] = hi;
-        }
+        x[r][k] = r < nrows ? base[e] * s : 0.0f;
     }
+    __syncthreads();
     const int rr = l & 31, h = l >> 5;
     const bool valid = rr < nrows;
-    if (h == 0) {
-        // |x|^2 in f64, k order, from the (cache-resident) row the wave just staged
-        double acc = 0.0;
-        if (valid)
-            for (int k = 0; k < D; ++k) {
-                const double v = (double)(base[rr * D + k] * s);
-                acc = acc + v * v;
-            }
-        // norm parts of acc / c (exact power-of-two division)
-        _Float16 np[3];
-        if (valid) {
-            double wv = acc * __builtin_ldexp(1.0, -sp.cs);
+    double acc = 0.0;
+    for (int k = 0; k < D; ++k) {
+        const double v = (double)x[rr][k];
+        acc = acc + v * v;
+    }
+    // norm parts of acc / c (exact power-of-two division)
+    _Float16 np[3];
+    if (valid) {
+        double wv = acc * __builtin_ldexp(1.0, -sp.cs);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                np[q] = (_Float16)(float)wv;  // |wv| < 2^15: double->float->half may round twice;
-                wv = wv - (double)np[q];      // the bound charges 2^-11 per part regardless
-            }
-        } else {
-            // finite sentinel 3 * 65504 * c > any real distance (<= 4 D 2^2T):
-            // index bits are OR-ed into screen values, which must not be inf
-            np[0] = (_Float16)65504.0f;
-            np[1] = (_Float16)65504.0f;
-            np[2] = (_Float16)65504.0f;
+        for (int q = 0; q < 3; ++q) {
+            np[q] = (_Float16)(float)wv;  // |wv| < 2^15: double->float->half may round twice;
+            wv = wv - (double)np[q];      // the bound charges 2^-11 per part regardless
         }
-        const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
-        _Float16 *row = im + rr * KS;
-        for (int kk = 0; kk < KS - 3 * D; ++kk) {
+    } else {
+        // finite sentinel 3 * 65504 * c > any real distance (<= 4 D 2^2T):
+        // index bits are OR-ed into screen values, which must not be inf
+        np[0] = (_Float16)65504.0f;
+        np[1] = (_Float16)65504.0f;
+        np[2] = (_Float16)65504.0f;
+    }
+    const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
+    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NCH * 64 + l;
+    for (int c = 0; c < NCH; ++c) {
+        f16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * c + 8 * h + j;
             _Float16 v = (_Float16)0.0f;
-            if (kk < 3) v = role == 0 ? np[kk] : cval;
-            else if (kk < 6) v = role == 0 ? cval : np[kk - 3];
-            row[3 * D + kk] = v;
+            if (k < 3 * D) {
+                const int seg = (k >= D) + (k >= 2 * D);
+                const float xv = x[rr][k - seg * D];
+                const _Float16 hi = (_Float16)xv;
+                const _Float16 lo = (_Float16)(xv - (float)hi);
+                if (role == 0) v = (_Float16)(-2.0f * (float)(seg == 2 ? lo : hi));
+                else v = (seg == 1) ? lo : hi;
+            } else {
+                const int kk = k - 3 * D;
+                if (kk < 3) v = role == 0 ? np[kk] : cval;
+                else if (kk < 6) v = role == 0 ? cval : np[kk - 3];
+            }
+            o[j] = v;
         }
+        dst[(size_t)c * 64] = o;
+    }
+    if (h == 0) {
         const float r = valid ? (float)__builtin_sqrt(acc) : 0.0f;
         nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
         if (valid) atomicMax(nmax + p, __float_as_uint(r));
     }
-    __syncthreads();
+}
+
+// Register-resident pack for a compile-time D (the hot D = 32): one lane per
+// (row, half), the row loaded with 16-byte loads (both halves of the wave share
+// the cache lines), the split computed once per element, and each 16-byte
+// operand fragment selected between the two compile-time candidates of the
+// lane's half -- no LDS, no per-half segment arithmetic.  Same values as
+// feat_pack5 (same operations, same order).
+template <int D>
+__global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t *n, int Nmax,
+                                                   int ntiles, int role, Split5 sp,
+                                                   const unsigned *mx, f16x8 *Xp, float *nrm,
+                                                   unsigned *nmax) {
+    static_assert(D % 8 == 0, "segments must align to 8-half fragments");
+    constexpr int NCH = (3 * D + 6 + 15) / 16;
+    constexpr int G = D / 8;  // fragments per segment
+    const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
+    const int cnt = count_of(n, p, Nmax);
+    const int nrows = min(max(cnt - t * 32, 0), 32);
+    const float s = pair_scale5(mx[p], sp.T);
+    const int rr = l & 31, h = l >> 5;
+    const bool valid = rr < nrows;
+    float x[D];
+    if (valid) {
+        const float4 *row = reinterpret_cast<const float4 *>(X + ((size_t)p * Nmax + (size_t)t * 32 + rr) * D);
+#pragma unroll
+        for (int q = 0; q < D / 4; ++q) {
+            const float4 v = row[q];
+            x[4 * q] = v.x * s; x[4 * q + 1] = v.y * s; x[4 * q + 2] = v.z * s; x[4 * q + 3] = v.w * s;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = 0.0f;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const double v = (double)x[k];
+        acc = acc + v * v;
+    }
+    _Float16 np[3];
+    if (valid) {
+        double wv = acc * __builtin_ldexp(1.0, -sp.cs);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            np[q] = (_Float16)(float)wv;
+            wv = wv - (double)np[q];
+        }
+    } else {
+        np[0] = (_Float16)65504.0f;
+        np[1] = (_Float16)65504.0f;
+        np[2] = (_Float16)65504.0f;
+    }
+    const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
+    _Float16 s0[D], s1[D], s2[D];  // the three segments of this role
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const _Float16 hi = (_Float16)x[k];
+        const _Float16 lo = (_Float16)(x[k] - (float)hi);
+        if (role == 0) {
+            s0[k] = (_Float16)(-2.0f * (float)hi);
+            s1[k] = s0[k];
+            s2[k] = (_Float16)(-2.0f * (float)lo);
+        } else {
+            s0[k] = hi;
+            s1[k] = lo;
+            s2[k] = hi;
+        }
+    }
+    auto frag = [&](int g) {  // compile-time g after unrolling
+        f16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            _Float16 v = (_Float16)0.0f;
+            if (g < G) v = s0[8 * g + j];
+            else if (g < 2 * G) v = s1[8 * (g - G) + j];
+            else if (g < 3 * G) v = s2[8 * (g - 2 * G) + j];
+            else if (g == 3 * G) {
+                if (j < 3) v = role == 0 ? np[j] : cval;
+                else if (j < 6) v = role == 0 ? cval : np[j - 3];
+            }
+            o[j] = v;
+        }
+        return o;
+    };
     f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NCH * 64 + l;
-    const f16x8 *src = img + rr * 2 * NCH + h;
-    for (int c = 0; c < NCH; ++c) dst[(size_t)c * 64] = src[2 * c];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const f16x8 a = frag(2 * c), b = frag(2 * c + 1);
+        dst[(size_t)c * 64] = h ? b : a;
+    }
+    if (h == 0) {
+        const float r = valid ? (float)__builtin_sqrt(acc) : 0.0f;
+        nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+        if (valid) atomicMax(nmax + p, __float_as_uint(r));
+    }
 }
 
 // certification threshold for a top-2 gap in scaled units (see header)
@@ -1925,13 +2015,21 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     hipLaunchKernelGGL(feat_maxabs, dim3(P, 2), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax, D,
                        mx);
     PCR_LAUNCH_CHECK();
-    const size_t pack_lds = sizeof(f16x8) * 4 * 32 * 2 * NCH;
-    hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), pack_lds, s, F, n_src, Nmax, D,
-                       NCH, ntn, 0, sp, mx, Ap, fnr, gmax + P);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), pack_lds, s, G, n_tgt, Mmax, D,
-                       NCH, ntm, 1, sp, mx, Bp, gnr, gmax);
-    PCR_LAUNCH_CHECK();
+    if (D == 32) {  // the hot shape: register-resident pack
+        hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax,
+                           ntn, 0, sp, mx, Ap, fnr, gmax + P);
+        PCR_LAUNCH_CHECK();
+        hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax,
+                           ntm, 1, sp, mx, Bp, gnr, gmax);
+        PCR_LAUNCH_CHECK();
+    } else {
+        hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D,
+                           NCH, ntn, 0, sp, mx, Ap, fnr, gmax + P);
+        PCR_LAUNCH_CHECK();
+        hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax, D,
+                           NCH, ntm, 1, sp, mx, Bp, gnr, gmax);
+        PCR_LAUNCH_CHECK();
+    }
     prof_end(s, kProfFeatPack);
     DualArgs5 d;
     d.Ap = Ap; d.Bp = Bp; d.fnr = fnr; d.gnr = gnr; d.fmax = gmax + P; d.gmax = gmax;
