@@ -182,9 +182,11 @@ def ransac_batch(src, tgt, corres, n_corres, params: RansacParams, n_src=None, n
     pid = None if pair_ids is None else _cuda(pair_ids, torch.int32, S.device).reshape(P)
     T, fr, st, ct, mk = _ransac_outputs(P, N, S.device, want_corr, want_mask)
     cp = params.to_c()
+    # count tensors held in locals: a temporary freed before the launch would
+    # hand its (reused) block to the next one
+    ns, nt = _counts(n_src, P, S.device), _counts(n_tgt, P, S.device)
     with torch.cuda.device(S.device):
-        _lib.call("pcr_ransac_batch", _lib.ptr(S), _lib.ptr(G), P, N, M,
-                  _lib.ptr(_counts(n_src, P, S.device)), _lib.ptr(_counts(n_tgt, P, S.device)),
+        _lib.call("pcr_ransac_batch", _lib.ptr(S), _lib.ptr(G), P, N, M, _lib.ptr(ns), _lib.ptr(nt),
                   _lib.ptr(C), _lib.ptr(nc), K, _lib.ptr(pid), ctypes.byref(cp), _lib.ptr(T),
                   _lib.ptr(fr), _lib.ptr(st), _lib.ptr(ct), _lib.ptr(mk), _stream(S.device))
     return BatchResult(T, fr[:, 0], fr[:, 1], st, ct, mk)
@@ -206,10 +208,10 @@ def register_feature_ransac_batch(src, tgt, src_feat, tgt_feat, params: RansacPa
     pid = None if pair_ids is None else _cuda(pair_ids, torch.int32, S.device).reshape(P)
     T, fr, st, ct, mk = _ransac_outputs(P, N, S.device, want_corr, want_mask)
     cp = params.to_c()
+    ns, nt = _counts(n_src, P, S.device), _counts(n_tgt, P, S.device)
     with torch.cuda.device(S.device):
         _lib.call("pcr_register_feature_ransac", _lib.ptr(S), _lib.ptr(G), _lib.ptr(F),
-                  _lib.ptr(H), P, N, M, D, _lib.ptr(_counts(n_src, P, S.device)),
-                  _lib.ptr(_counts(n_tgt, P, S.device)), _lib.ptr(pid), ctypes.byref(cp),
+                  _lib.ptr(H), P, N, M, D, _lib.ptr(ns), _lib.ptr(nt), _lib.ptr(pid), ctypes.byref(cp),
                   _lib.ptr(T), _lib.ptr(fr), _lib.ptr(st), _lib.ptr(ct), _lib.ptr(mk),
                   _stream(S.device))
     return BatchResult(T, fr[:, 0], fr[:, 1], st, ct, mk)
@@ -225,9 +227,9 @@ def icp_batch(src, tgt, init, params: IcpParams, n_src=None, n_tgt=None, want_co
     st = torch.empty(P, 2, dtype=torch.int32, device=S.device)
     ct = torch.empty(P, N, dtype=torch.int32, device=S.device) if want_corr else None
     cp = params.to_c()
+    ns, nt = _counts(n_src, P, S.device), _counts(n_tgt, P, S.device)
     with torch.cuda.device(S.device):
-        _lib.call("pcr_icp_batch", _lib.ptr(S), _lib.ptr(G), P, N, M,
-                  _lib.ptr(_counts(n_src, P, S.device)), _lib.ptr(_counts(n_tgt, P, S.device)),
+        _lib.call("pcr_icp_batch", _lib.ptr(S), _lib.ptr(G), P, N, M, _lib.ptr(ns), _lib.ptr(nt),
                   _lib.ptr(I), ctypes.byref(cp), _lib.ptr(T), _lib.ptr(fr), _lib.ptr(st),
                   _lib.ptr(ct), _stream(S.device))
     return BatchResult(T, fr[:, 0], fr[:, 1], st, ct)
@@ -256,9 +258,10 @@ def radius_nn(tgt, queries, r, n_tgt=None, n_q=None):
     P, Nq, M = Q.shape[0], Q.shape[1], G.shape[1]
     idx = torch.empty(P, Nq, dtype=torch.int32, device=G.device)
     d2 = torch.empty(P, Nq, dtype=torch.float64, device=G.device)
+    nt, nq = _counts(n_tgt, P, G.device), _counts(n_q, P, G.device)
     with torch.cuda.device(G.device):
-        _lib.call("pcr_radius_nn", _lib.ptr(G), P, M, _lib.ptr(_counts(n_tgt, P, G.device)),
-                  _lib.ptr(Q), Nq, _lib.ptr(_counts(n_q, P, G.device)), float(r), _lib.ptr(idx),
+        _lib.call("pcr_radius_nn", _lib.ptr(G), P, M, _lib.ptr(nt), _lib.ptr(Q), Nq, _lib.ptr(nq),
+                  float(r), _lib.ptr(idx),
                   _lib.ptr(d2), _stream(G.device))
     return idx, d2
 

@@ -264,3 +264,36 @@ def test_feature_match_many_pairs_xcd_mapping(oracle):
     for p in range(P):
         assert np.array_equal(_np(nn12)[p], oracle.featnn(fs[p], ft[p]))
         assert np.array_equal(_np(nn21)[p], oracle.featnn(ft[p], fs[p]))
+
+
+def test_ragged_batches_equal_per_pair_runs(oracle):
+    """Pairs with n_src != n_tgt padded into one batch give each pair's own result
+    (regression: per-call count tensors must stay alive across the launch)."""
+    sizes = [(1200, 1100), (900, 1300), (1500, 1500), (700, 1000)]
+    S = np.zeros((4, 1500, 3), np.float32)
+    G = np.zeros((4, 1500, 3), np.float32)
+    FS = np.zeros((4, 1500, 16), np.float32)
+    FG = np.zeros((4, 1500, 16), np.float32)
+    T0 = np.tile(np.eye(4), (4, 1, 1))
+    for p, (n, m) in enumerate(sizes):
+        b = synth.make_pair(70 + p, n, m, 16, feat_noise=0.3)
+        S[p, :n], G[p, :m], FS[p, :n], FG[p, :m] = b[0], b[1], b[2], b[3]
+        T0[p, :3, :3], T0[p, :3, 3] = b[4], b[5] + 0.005
+    ns = np.array([s[0] for s in sizes], np.int32)
+    nt = np.array([s[1] for s in sizes], np.int32)
+    prm = reg.RansacParams(max_correspondence_distance=0.04, seed=3)
+    rb = reg.register_feature_ransac_batch(S, G, FS, FG, prm, n_src=ns, n_tgt=nt,
+                                           pair_ids=np.arange(4, dtype=np.int32))
+    ib = reg.icp_batch(S, G, T0, reg.IcpParams(max_correspondence_distance=0.02), n_src=ns, n_tgt=nt)
+    for p, (n, m) in enumerate(sizes):
+        r1 = reg.register_feature_ransac_batch(S[p:p + 1, :n], G[p:p + 1, :m], FS[p:p + 1, :n],
+                                               FG[p:p + 1, :m], prm,
+                                               pair_ids=np.array([p], np.int32))
+        assert torch.equal(rb.transformation[p], r1.transformation[0]), p
+        assert rb.fitness[p].item() == r1.fitness[0].item(), p
+        i1 = reg.icp_batch(S[p:p + 1, :n], G[p:p + 1, :m], T0[p:p + 1],
+                           reg.IcpParams(max_correspondence_distance=0.02))
+        assert torch.equal(ib.transformation[p], i1.transformation[0]), p
+        assert np.array_equal(ib.correspondence_set(p), i1.correspondence_set(0)), p
+        o = oracle.icp(S[p, :n], G[p, :m], 0.02, T0[p])
+        assert np.array_equal(o["T"], _np(ib.transformation[p]))
