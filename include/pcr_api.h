@@ -318,6 +318,33 @@ int pcr_compute_fpfh(const float *xyz, const double *normals, int32_t P, int32_t
                      const int32_t *n_pts, double radius, int32_t max_nn, double *fpfh,
                      float *fpfh_f32, double *spfh, pcr_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * f4 -- device-side pieces of the NDP level optimisation
+ * (c2p-net/deformationpyramid/model/registration.py:196-262), so one iteration
+ * can be captured in a HIP graph and replayed without host round trips.
+ *
+ * pcr_ndp_control: the early-stop rule of :246-256 on the device (f64 on the f32
+ *   loss, as Python evaluates loss.item()).  state (device f64[8]) =
+ *   {active, break_count, loss_prev, steps, last_loss, step_flag, evaluated, 0},
+ *   initialise to {1, 0, 1e6, 0, 0, 0, 0, 0} per level; stop_loss 1e-4.
+ * pcr_adam_masked: torch.optim.Adam's update for n_tensors parameter tensors
+ *   (a DEVICE table of pcr_adam_tensor), skipped when state[5] == 0; bias
+ *   corrections from state[3] (steps taken, incremented by pcr_ndp_control).
+ * ------------------------------------------------------------------------- */
+typedef struct pcr_adam_tensor {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int32_t n;
+    int32_t reserved;
+} pcr_adam_tensor;
+int pcr_ndp_control(const float *loss, double *state, double break_threshold_ratio,
+                    int32_t max_break_count, double stop_loss, pcr_stream_t stream);
+int pcr_adam_masked(const pcr_adam_tensor *tensors, int32_t n_tensors, int32_t max_numel,
+                    const double *state, double lr, double beta1, double beta2, double eps,
+                    pcr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,8 @@ SIGNATURES = {
     "pcr_radius_count": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _p, _p, _p],
     "pcr_radius_neighbors": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _i32, _p, _p, _p],
     "pcr_transform_batch": [_p, _i32, _i32, _p, _p, _p],
+    "pcr_ndp_control": [_p, _p, _f64, _i32, _f64, _p],
+    "pcr_adam_masked": [_p, _i32, _i32, _p, _f64, _f64, _f64, _f64, _p],
     "pcr_hybrid_search": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
     "pcr_estimate_normals": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p],
     "pcr_compute_fpfh": [_p, _p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
