@@ -1,0 +1,29 @@
+"""Profile helper: the f4 NDP optimisation on the C5 shape (bench secondary f4)."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pointcloudregistration_amd import ndp_opt  # noqa: E402
+
+rng = np.random.default_rng(9)
+n = 20000
+u = rng.standard_normal((n, 3))
+src = (u / np.linalg.norm(u, axis=1, keepdims=True)).astype(np.float32)
+w = rng.standard_normal((n, 3))
+w = w / np.linalg.norm(w, axis=1, keepdims=True)
+tgt = (w + 0.05 * np.sin(3 * w[:, [1, 2, 0]])).astype(np.float32)
+inds = np.sort(rng.choice(n, 5000, replace=False))
+cfg = ndp_opt.NDPConfig(max_break_count=10**6, m=int(os.environ.get("LEVELS", "9")))
+S, G = torch.from_numpy(src).cuda(), torch.from_numpy(tgt).cuda()
+for rep in range(2):
+    torch.manual_seed(0)
+    P = ndp_opt.DeformationPyramid(3, 128, torch.device("cuda"), -8, cfg.m, True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ndp_opt.optimize_deformation_pyramid(S, G, inds, cfg, NDP=P, use_graph=os.environ.get("GRAPH", "1") == "1")
+    torch.cuda.synchronize()
+    print(rep, (time.perf_counter() - t0) * 1e3, "ms")
