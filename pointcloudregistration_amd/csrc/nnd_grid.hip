@@ -17,8 +17,9 @@
 // exceeds the best distance (strictly) the answer is final.  Rings are capped
 // at kMaxRing, then the query scans every point (same exact rule).
 //
-// One thread per query, 256-thread blocks over all pairs and both directions;
-// the grids (160 KB per 8192-point cloud) stay L2-resident.
+// One thread per query, 256-thread blocks over all pairs and both directions,
+// ordered per XCD (xcd_slot) so each grid (160 KB per 8192-point cloud) is
+// served from one XCD's L2.
 #include "pcr_internal.h"
 #include "scan.h"
 
@@ -127,8 +128,20 @@ __device__ __forceinline__ float d2f(float cx, float cy, float cz, float qx, flo
     return (dx * dx + dy * dy) + dz * dz;
 }
 
-__global__ __launch_bounds__(256) void nng_query(NgArgs a) {
-    const int dir = blockIdx.z, b = blockIdx.y, qi = blockIdx.x * blockDim.x + threadIdx.x;
+// XCD-aware block order: the hardware deals linear block ids round-robin over
+// the 8 XCDs; the k-th block an XCD receives takes the k-th slot of that XCD's
+// contiguous range of (direction, pair, chunk) work, so every grid is read by
+// one XCD at a time and stays in its L2 while its 32 chunks run (row-major
+// order spread each grid over all 8 L2s: 5.3 GB of fabric reads per C4 launch).
+__device__ __forceinline__ int xcd_slot(int L, int total) {
+    const int xcd = L & 7, k = L >> 3, per = total >> 3, rem = total & 7;
+    return (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + k;
+}
+
+__global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
+    const int w = xcd_slot(blockIdx.x, gridDim.x);
+    const int grp = w / nchunk, chunk = w - grp * nchunk;
+    const int dir = grp / a.B, b = grp - dir * a.B, qi = chunk * blockDim.x + threadIdx.x;
     const int qs = dir, gs = 1 - dir;  // queries from set dir, candidates from the other set
     if (qi >= a.n[qs]) return;
     const float *q = a.xyz[qs] + ((size_t)b * a.n[qs] + qi) * 3;
@@ -226,7 +239,8 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
     hipLaunchKernelGGL(nng_scatter, pg, dim3(256), 0, s, a);
     PCR_LAUNCH_CHECK();
     prof_begin(s, kProfNndGrid);
-    hipLaunchKernelGGL(nng_query, pg, dim3(256), 0, s, a);
+    const int nchunk = (a.nmax + 255) / 256;
+    hipLaunchKernelGGL(nng_query, dim3(2 * b * nchunk), dim3(256), 0, s, a, nchunk);
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfNndGrid);
     return PCR_OK;
