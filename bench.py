@@ -375,6 +375,23 @@ def measure_ndp_opt(with_cpu):
     return res
 
 
+TRAFFIC_FILE = "profiles/r01/v10_pmc_traffic.json"
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch (fetch + write) of `kernel` from the committed PMC summary
+    (tools/pmc_traffic.sh on this bench), or None when absent."""
+    try:
+        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for k, v in ks.items():
+        if kernel in k:
+            return v.get("fetch_size_bytes", 0.0) + v.get("write_size_bytes", 0.0)
+    return None
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup()
@@ -462,7 +479,9 @@ def main():
                    "icp": "d=0.02 (1e-6,1e-6,30)", "parallelism": f"pair-sharded x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_F16_MFMA_TFLOPS,
-                     "traffic": None,
+                     "traffic": _pmc_traffic("featnn_dual7"),
+                     "traffic_source": TRAFFIC_FILE + " (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                                       "passes of this bench; FETCH_SIZE x2 per the gfx950 note)",
                      "kernel": "featnn_dual7 (v_mfma_f32_32x32x16_f16, f16x3 split, top-2 epilogue)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,

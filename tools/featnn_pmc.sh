@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-M=${1:-6}; P=${2:-64}
+M=${1:-7}; P=${2:-64}
 OUT=gpurun_out/pmc_m$M
 mkdir -p "$OUT"
 run() {  # name counters...
