@@ -54,6 +54,8 @@ struct RArgs {
     int words;
     unsigned long long *timing;  // debug (PCR_RANSAC_TIMING): per pair, 6 phase clocks
     const int32_t *order;        // (P, Nmax) spatial order of the source points, or null
+    int32_t *cand;               // (P, 2, Nmax): target index per source point of a sweep,
+                                 // two buffers: the best hypothesis' and the current one's
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -134,6 +136,7 @@ struct Shared {  // LDS header (the grid copy follows)
     int chunk;     // next 64-query chunk of the current sweep (dynamic balance across waves)
     int misses;    // source points without a correspondence so far in this sweep
     int best_cnt;  // inlier count of the best hypothesis (0: none yet)
+    int cur_buf, best_buf;  // cand buffer of the running sweep / of the best hypothesis
 };
 
 template <bool kLds, int RN>
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
         for (int k = 0; k < 12; ++k) sh.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
         sh.best_fit = 0.0; sh.best_rmse = 0.0;
         sh.est_k = a.max_iter; sh.best_itr = -1; sh.validated = 0; sh.last_upd = -1; sh.base = 0;
-        sh.chunk = 0; sh.misses = 0; sh.best_cnt = 0;
+        sh.chunk = 0; sh.misses = 0; sh.best_cnt = 0; sh.cur_buf = 0; sh.best_buf = 0;
     }
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
@@ -208,6 +211,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
             // it, so its sweep stops there (exact; no effect on T, fitness,
             // rmse or est_k)
             const int lim_miss = sh.best_cnt > 0 ? n - sh.best_cnt : 0x7fffffff;
+            int32_t *cbuf = a.cand + ((size_t)p * 2 + sh.cur_buf) * a.Nmax;
             for (;;) {
                 int c = 0;
                 if (lane == 0) c = atomicAdd(&sh.chunk, 1);
@@ -222,6 +226,7 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
                     if constexpr (kLds) j = grid_query(gl, a.d, a.thr, px, py, pz, d2);
                     else j = grid_query(gg, a.d, a.thr, px, py, pz, d2);
                     if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+                    cbuf[i] = j;
                 }
                 const int miss = __popcll(__ballot(k < n && j < 0));
                 int tot = 0;
@@ -265,6 +270,8 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
                     sh.best_rmse = rmse;
                     sh.best_itr = itr_e;
                     sh.last_upd = itr_e;
+                    sh.best_buf = sh.cur_buf;  // its correspondences stay; the next sweep
+                    sh.cur_buf ^= 1;           // writes the other buffer
                     for (int k = 0; k < 12; ++k) sh.bestT[k] = Te[k];
                     const double kd = est_k_bound((double)CI / (double)K, RN, a.conf);
                     if (kd < (double)sh.est_k) sh.est_k = (int)__builtin_ceil(kd);
@@ -280,21 +287,17 @@ __global__ __launch_bounds__(kThreads) void ransac_pair_kernel(RArgs a) {
     // last bound update (or max_iter)
     const int iters = ok ? min(a.max_iter, max(sh.last_upd + 1, sh.est_k)) : 0;
     const bool found = ok && sh.best_itr >= 0;
-    // correspondence set of the best transformation, swept in spatial order;
-    // the inlier mask is assembled with atomicOr on words zeroed first
+    // correspondence set of the best transformation: the targets its validation
+    // sweep found (a sweep that became the best ran to completion, and the same
+    // grid_query on the same transform gives the same answer); the inlier mask is
+    // assembled with atomicOr on words zeroed first
     if (a.mask)
         for (int w = tid; w < a.words; w += kThreads) a.mask[(size_t)p * a.words + w] = 0u;
     __syncthreads();
     int cnt = 0;
-    for (int k = tid; k < a.Nmax; k += kThreads) {
-        const int i = (ord && k < n) ? ord[k] : k;
-        int j = -1;
-        if (found && i < n) {
-            double px, py, pz, d2;
-            xform12(sh.bestT, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
-            if constexpr (kLds) j = grid_query(gl, a.d, a.thr, px, py, pz, d2);
-            else j = grid_query(gg, a.d, a.thr, px, py, pz, d2);
-        }
+    const int32_t *bbuf = a.cand + ((size_t)p * 2 + sh.best_buf) * a.Nmax;
+    for (int i = tid; i < a.Nmax; i += kThreads) {
+        const int j = (found && i < n) ? bbuf[i] : -1;
         if (a.corr_tgt) a.corr_tgt[(size_t)p * a.Nmax + i] = j;
         cnt += (j >= 0);
         if (a.mask && j >= 0) atomicOr(a.mask + (size_t)p * a.words + (i >> 5), 1u << (i & 31));
@@ -352,6 +355,8 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.words = (Nmax + 31) / 32;
     a.timing = nullptr;
     a.order = nullptr;
+    a.cand = (int32_t *)workspace(21, sizeof(int32_t) * 2 * (size_t)P * (size_t)(Nmax > 0 ? Nmax : 1));
+    PCR_REQUIRE(a.cand, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
     const bool want_timing = getenv("PCR_RANSAC_TIMING") != nullptr;
     if (want_timing) {
         a.timing = (unsigned long long *)workspace(12, sizeof(unsigned long long) * 6 * (size_t)P);
