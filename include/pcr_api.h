@@ -345,6 +345,37 @@ int pcr_adam_masked(const pcr_adam_tensor *tensors, int32_t n_tensors, int32_t m
                     const double *state, double lr, double beta1, double beta2, double eps,
                     pcr_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * f4 -- fused NDP level training step (one level of
+ * registration.py:208-262 without PyTorch autograd).  One descriptor:
+ *   x (N,3) level input; level weights in nn.Linear layout (level.w_hid /
+ *   level.b_hid unused: the hidden layers are w_hid[k] / b_hid[k], k < depth-1,
+ *   read in place so the optimizer updates them directly); width 128.
+ *   Scratch (device, feature-major [F][N]): pe [6][N], H [depth][W][N],
+ *   aux [8][N], dO [8][N], D [depth][W][N]; x_out (N,3) the warped points.
+ *   g (N,3) = dL/dx_out (e.g. the Chamfer gradient), bce_scale = w_reg / N for
+ *   a level with the nonrigidity branch (BCE(s, 0) mean), else 0.
+ * pcr_ndp_train_forward: x_out, and the saved activations.
+ * pcr_ndp_train_backward: the gradients of every parameter of the level into
+ *   grads (HOST array of device pointers): {w_in, b_in, w_hid[0], b_hid[0], ...,
+ *   w_branch (7 x W rows: rot 0-2, trn 3-5, nr 6), b_branch (7)}; part is
+ *   scratch of pcr_ndp_train_partial_floats(N, width, depth, chunk) floats.
+ * ------------------------------------------------------------------------- */
+typedef struct pcr_ndp_train {
+    const float *x;
+    int32_t N, width, depth, k0;
+    pcr_ndp_level level;
+    const float *w_hid[4], *b_hid[4];
+    float *pe, *H, *aux, *x_out;
+    const float *g;
+    double bce_scale;
+    float *dO, *D;
+} pcr_ndp_train;
+int pcr_ndp_train_forward(const pcr_ndp_train *t, pcr_stream_t stream);
+int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32_t chunk,
+                           float *const *grads, pcr_stream_t stream);
+int64_t pcr_ndp_train_partial_floats(int32_t N, int32_t width, int32_t depth, int32_t chunk);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,8 @@ SIGNATURES = {
     "pcr_transform_batch": [_p, _i32, _i32, _p, _p, _p],
     "pcr_ndp_control": [_p, _p, _f64, _i32, _f64, _p],
     "pcr_adam_masked": [_p, _i32, _i32, _p, _f64, _f64, _f64, _f64, _p],
+    "pcr_ndp_train_forward": [_p, _p],
+    "pcr_ndp_train_backward": [_p, _p, _i32, _p, _p],
     "pcr_hybrid_search": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
     "pcr_estimate_normals": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p],
     "pcr_compute_fpfh": [_p, _p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
@@ -105,6 +107,8 @@ def load():
         lib.pcr_profile_read.argtypes = [_i32, ctypes.POINTER(_f64), ctypes.POINTER(_i64), _i32]
         lib.pcr_featnn_rescan_rows.restype = ctypes.c_int
         lib.pcr_featnn_rescan_rows.argtypes = [ctypes.POINTER(_i64), ctypes.POINTER(_i64), _i32]
+        lib.pcr_ndp_train_partial_floats.restype = _i64
+        lib.pcr_ndp_train_partial_floats.argtypes = [_i32, _i32, _i32, _i32]
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
@@ -115,7 +119,7 @@ def load():
 
 def exported_symbols():
     return ["pcr_last_error", "pcr_version", "pcr_profile_enable", "pcr_profile_read",
-            "pcr_featnn_rescan_rows"] + list(SIGNATURES)
+            "pcr_featnn_rescan_rows", "pcr_ndp_train_partial_floats"] + list(SIGNATURES)
 
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4

@@ -1,0 +1,472 @@
+// f4: the fused NDP level training step -- one level's warp
+// forward with saved activations, the warp backward, and the weight gradients --
+// as libpcr kernels, so an optimisation iteration of
+// c2p-net/deformationpyramid/model/registration.py:208-262 is
+//   ndp_train_fwd -> nnd Chamfer fwd/bwd (a1/a2) -> ndp_train_bwd -> ndp_wgrad
+//   -> ndp_wgrad_reduce -> pcr_ndp_control -> pcr_adam_masked
+// with no PyTorch autograd on the path.  Semantics: NDPLayer.forward
+// (nets.py:111-140, motion SE3, rotation axis_angle, rigid_body.py:89-119) in
+// f32, its gradient by the chain rule written out below, nn.Linear weight
+// gradients dW = sum_p delta_p (x) a_p, bias gradients sum_p delta_p.
+//
+// Layouts (N points of the level):
+//   activations H_l, deltas D_l, positional encoding, branch data: FEATURE-major
+//   [F][N] f32 -- lane j of a wave writes point j of a 32-point tile, so every
+//   save and load is a coalesced 128-byte row segment, and the weight-gradient
+//   GEMMs (K = points) read contiguous rows.
+//   aux [8][N]: r (3, = 1e-3 o_r), y = R x + t (3), s (nonrigidity), 0.
+//   dO [8][N]: dL/d(branch pre-activation): rot (3), trn (3), nr (1), 0.
+// MFMA mapping: as ndp.hip -- one wave owns 32 points, a 32-feature tile is 16
+// accumulator registers (feature frow(r, h) of point j); a layer is a chain of
+// exact-f32 v_mfma_f32_32x32x2_f32 whose B operand is the previous tile.  The
+// backward products use the transposed weights (A[i][k] = W[k][i], lanes read
+// consecutive columns: coalesced).  Weight gradients are split-K GEMMs over
+// 128-point chunks with per-chunk partials reduced in chunk order
+// (deterministic).
+#include "pcr_internal.h"
+
+namespace pcr {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxHid = 4;
+
+struct TrainArgs {
+    const float *x;                 // (N, 3) level input
+    int N, W, nhid, m, k0;          // nhid = depth - 1
+    const float *w_in, *b_in;       // (W, 6), (W)
+    const float *w_hid[kMaxHid], *b_hid[kMaxHid];  // (W, W), (W)
+    const float *w_rot, *b_rot, *w_trn, *b_trn, *w_nr, *b_nr;
+    float *pe;                      // [6][N]
+    float *H;                       // [nhid + 1][W][N]: H_0 = relu(input), H_l = relu(hidden l)
+    float *aux;                     // [8][N]
+    float *x_out;                   // (N, 3)
+    // backward
+    const float *g;                 // (N, 3) dL/dx'
+    double bce_scale;               // w_reg / N when the level has the nonrigidity branch, else 0
+    float *dO;                      // [8][N]
+    float *D;                       // [nhid + 1][W][N]: dL/d(pre-activation) of layer l
+};
+
+__device__ __forceinline__ int frow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ float sgn_mask(float a, float d) { return a > 0.0f ? d : 0.0f; }
+
+// ---- forward of one level, saving what the backward needs -------------------
+template <int NT>
+__global__ __launch_bounds__(256) void ndp_train_fwd(TrainArgs a) {
+    constexpr int W = 32 * NT;
+    const int l = threadIdx.x & 63, h = l >> 5, j = l & 31;
+    const int pt = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + j;
+    const bool valid = pt < a.N;
+    const int N = a.N;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+    if (valid) { x0 = a.x[3 * pt]; x1 = a.x[3 * pt + 1]; x2 = a.x[3 * pt + 2]; }
+    const float w = __builtin_ldexpf(1.0f, a.m + a.k0);
+    float pe[3];
+    {
+        const float v0 = x0 * w, v1 = x1 * w, v2 = x2 * w;
+        pe[0] = h ? cosf(v0) : sinf(v0);
+        pe[1] = h ? cosf(v1) : sinf(v1);
+        pe[2] = h ? cosf(v2) : sinf(v2);
+        if (valid)
+            for (int s = 0; s < 3; ++s) a.pe[(size_t)(2 * s + h) * N + pt] = pe[s];
+    }
+    f32x16 H[NT];
+#pragma unroll
+    for (int ot = 0; ot < NT; ++ot) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) H[ot][r] = a.b_in[32 * ot + frow(r, h)];
+        const float *wr = a.w_in + (32 * ot + j) * 6;
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+            H[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[2 * s + h], pe[s], H[ot], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) H[ot][r] = fmaxf(H[ot][r], 0.0f);
+    }
+    auto save = [&](int layer, const f32x16 *T) {
+        if (!valid) return;
+        float *base = a.H + (size_t)layer * W * N + pt;
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) base[(size_t)(32 * ot + frow(r, h)) * N] = T[ot][r];
+    };
+    save(0, H);
+    for (int hl = 0; hl < a.nhid; ++hl) {
+        const float *Wm = a.w_hid[hl];
+        const float *bm = a.b_hid[hl];
+        f32x16 Hn[NT];
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Hn[ot][r] = bm[32 * ot + frow(r, h)];
+            const float *wr = Wm + (size_t)(32 * ot + j) * W;
+#pragma unroll
+            for (int it = 0; it < NT; ++it)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    Hn[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32 * it + frow(r, h)], H[it][r],
+                                                                  Hn[ot], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) H[ot][r] = fmaxf(Hn[ot][r], 0.0f);
+        save(hl + 1, H);
+    }
+    const bool has_nr = a.w_nr != nullptr;
+    const float *br = j < 3 ? a.w_rot + j * W
+                    : j < 6 ? a.w_trn + (j - 3) * W
+                    : (j == 6 && has_nr) ? a.w_nr : nullptr;
+    f32x16 Bo;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int q = frow(r, h);
+        Bo[r] = q < 3 ? a.b_rot[q] : q < 6 ? a.b_trn[q - 3] : (q == 6 && has_nr) ? a.b_nr[0] : 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < NT; ++it)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            Bo = __builtin_amdgcn_mfma_f32_32x32x2f32(br ? br[32 * it + frow(r, h)] : 0.0f, H[it][r],
+                                                      Bo, 0, 0, 0);
+    const float o0 = Bo[0], o1 = Bo[1], o2 = Bo[2], o3 = Bo[3];
+    const float p0 = __shfl_xor(o0, 32, 64), p1 = __shfl_xor(o1, 32, 64);
+    const float p2 = __shfl_xor(o2, 32, 64), p3 = __shfl_xor(o3, 32, 64);
+    const float rr0 = h ? p0 : o0, rr1 = h ? p1 : o1, rr2 = h ? p2 : o2;
+    const float tt0 = h ? p3 : o3, tt1 = h ? o0 : p0, tt2 = h ? o1 : p1;
+    const float nrr = h ? o2 : p2;
+    const float t0 = 0.001f * tt0, t1 = 0.001f * tt1, t2 = 0.001f * tt2;
+    const float r0 = 0.001f * rr0, r1 = 0.001f * rr1, r2 = 0.001f * rr2;
+    const float th = sqrtf((r0 * r0 + r1 * r1) + r2 * r2);
+    const float w0 = r0 / th, w1 = r1 / th, w2 = r2 / th;
+    const float K[3][3] = {{0.f, -w2, w1}, {w2, 0.f, -w0}, {-w1, w0, 0.f}};
+    const float sn = sinf(th), cs = 1.0f - cosf(th);
+    float R[3][3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+            const float kk = (K[u][0] * K[0][v] + K[u][1] * K[1][v]) + K[u][2] * K[2][v];
+            R[u][v] = ((u == v ? 1.0f : 0.0f) + sn * K[u][v]) + cs * kk;
+        }
+    const float y0 = ((R[0][0] * x0 + R[0][1] * x1) + R[0][2] * x2) + t0;
+    const float y1 = ((R[1][0] * x0 + R[1][1] * x1) + R[1][2] * x2) + t1;
+    const float y2 = ((R[2][0] * x0 + R[2][1] * x1) + R[2][2] * x2) + t2;
+    float n0 = y0, n1 = y1, n2 = y2, s = 0.0f;
+    if (has_nr) {
+        s = 1.0f / (1.0f + expf(-(0.001f * nrr)));
+        n0 = x0 + s * (y0 - x0);
+        n1 = x1 + s * (y1 - x1);
+        n2 = x2 + s * (y2 - x2);
+    }
+    if (valid && h == 0) {
+        a.x_out[3 * pt] = n0; a.x_out[3 * pt + 1] = n1; a.x_out[3 * pt + 2] = n2;
+        const float v[8] = {r0, r1, r2, y0, y1, y2, s, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a.aux[(size_t)k * N + pt] = v[k];
+    }
+}
+
+// ---- backward of one level: dL/dx' -> branch gradients -> layer deltas -----
+template <int NT>
+__global__ __launch_bounds__(256) void ndp_train_bwd(TrainArgs a) {
+    constexpr int W = 32 * NT;
+    const int l = threadIdx.x & 63, h = l >> 5, j = l & 31;
+    const int pt = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + j;
+    const bool valid = pt < a.N;
+    const int N = a.N;
+    const bool has_nr = a.w_nr != nullptr;
+    // per-point branch gradients (both halves of the wave compute them)
+    float dO[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+        const float x[3] = {a.x[3 * pt], a.x[3 * pt + 1], a.x[3 * pt + 2]};
+        float g[3] = {a.g[3 * pt], a.g[3 * pt + 1], a.g[3 * pt + 2]};
+        float aux[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) aux[k] = a.aux[(size_t)k * N + pt];
+        const float r0 = aux[0], r1 = aux[1], r2 = aux[2];
+        const float y[3] = {aux[3], aux[4], aux[5]};
+        if (has_nr) {
+            // x' = x + s (y - x), s = sigmoid(1e-3 o_n); BCE(s, 0) = -log(1 - s), mean
+            const float s = aux[6];
+            const float ds = ((g[0] * (y[0] - x[0]) + g[1] * (y[1] - x[1])) + g[2] * (y[2] - x[2])) +
+                             (float)a.bce_scale / (1.0f - s);
+            dO[6] = 0.001f * (ds * (s * (1.0f - s)));
+            g[0] *= s; g[1] *= s; g[2] *= s;
+        }
+        // y = R x + t
+        dO[3] = 0.001f * g[0]; dO[4] = 0.001f * g[1]; dO[5] = 0.001f * g[2];
+        const float th = sqrtf((r0 * r0 + r1 * r1) + r2 * r2);
+        const float w[3] = {r0 / th, r1 / th, r2 / th};
+        const float K[3][3] = {{0.f, -w[2], w[1]}, {w[2], 0.f, -w[0]}, {-w[1], w[0], 0.f}};
+        const float sn = sinf(th), cs0 = cosf(th), cs = 1.0f - cs0;
+        float G[3][3], KK[3][3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = 0; v < 3; ++v) {
+                G[u][v] = g[u] * x[v];
+                KK[u][v] = (K[u][0] * K[0][v] + K[u][1] * K[1][v]) + K[u][2] * K[2][v];
+            }
+        // R = I + sin(th) K + (1 - cos(th)) K^2
+        float dth = 0.0f;
+        float dK[3][3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = 0; v < 3; ++v) {
+                dth += G[u][v] * (cs0 * K[u][v] + sn * KK[u][v]);
+                // d<G, K K>/dK = G K^T + K^T G
+                float gkt = 0.0f, ktg = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    gkt += G[u][q] * K[v][q];
+                    ktg += K[q][u] * G[q][v];
+                }
+                dK[u][v] = sn * G[u][v] + cs * (gkt + ktg);
+            }
+        const float gw[3] = {dK[2][1] - dK[1][2], dK[0][2] - dK[2][0], dK[1][0] - dK[0][1]};
+        const float gww = (gw[0] * w[0] + gw[1] * w[1]) + gw[2] * w[2];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dO[c] = 0.001f * ((gw[c] - gww * w[c]) / th + dth * w[c]);
+        if (h == 0)
+            for (int k = 0; k < 8; ++k) a.dO[(size_t)k * N + pt] = dO[k];
+    }
+    // delta of the last hidden activation: W_b^T dO (K = 8 branch rows, 4 k-steps)
+    const int L = a.nhid;
+    auto load_act = [&](int layer, int ot, int r) -> float {
+        return valid ? a.H[((size_t)layer * W + 32 * ot + frow(r, h)) * N + pt] : 0.0f;
+    };
+    auto branch_w = [&](int q, int col) -> float {  // W_b[q][col], q = branch row 0..7
+        if (q < 3) return a.w_rot[q * W + col];
+        if (q < 6) return a.w_trn[(q - 3) * W + col];
+        if (q == 6 && has_nr) return a.w_nr[col];
+        return 0.0f;
+    };
+    f32x16 Dt[NT];
+#pragma unroll
+    for (int ot = 0; ot < NT; ++ot) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Dt[ot][r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)  // k = 2s + h: B[k][j] = dO[k] of point j
+            Dt[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(branch_w(2 * s + h, 32 * ot + j),
+                                                          h ? dO[2 * s + 1] : dO[2 * s], Dt[ot], 0, 0, 0);
+    }
+    // rows of the transposed product: A[i][k] = W[k][i] -> lane j gives W[k][32 ot + j]
+    for (int layer = L; layer >= 0; --layer) {
+        // mask by the layer's ReLU: delta of the pre-activation
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Dt[ot][r] = sgn_mask(load_act(layer, ot, r), Dt[ot][r]);
+        if (valid) {
+            float *base = a.D + (size_t)layer * W * N + pt;
+#pragma unroll
+            for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) base[(size_t)(32 * ot + frow(r, h)) * N] = Dt[ot][r];
+        }
+        if (layer == 0) break;
+        const float *Wm = a.w_hid[layer - 1];  // layer l = relu(W_{l-1} H_{l-1} + b)
+        f32x16 Dn[NT];
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Dn[ot][r] = 0.0f;
+#pragma unroll
+            for (int it = 0; it < NT; ++it)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    Dn[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                        Wm[(size_t)(32 * it + frow(r, h)) * W + 32 * ot + j], Dt[it][r], Dn[ot], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot) Dt[ot] = Dn[ot];
+    }
+}
+
+// ---- weight gradients: dW[o][i] = sum_p D[o][p] X[i][p] (split-K) ------------
+struct WgradJob {
+    const float *D;   // [FO][N]
+    const float *X;   // [FI][N]
+    int FO, FI;       // actual rows (<= 128)
+    float *part;      // [nchunk][FO][FI] then [nchunk][FO] bias partials
+};
+struct WgradArgs {
+    WgradJob job[8];
+    int N, chunk;     // points per chunk (multiple of 64)
+};
+
+constexpr int kWgT = 64;  // points per LDS stage
+
+__global__ __launch_bounds__(256) void ndp_wgrad(WgradArgs a) {
+    __shared__ float Ds[128][kWgT + 1], Xs[128][kWgT + 1];
+    const WgradJob jb = a.job[blockIdx.y];
+    const int c = blockIdx.x, nchunk = gridDim.x;
+    const int p0 = c * a.chunk, p1 = min(a.N, p0 + a.chunk);
+    const int tid = threadIdx.x, wid = tid >> 6, l = tid & 63, h = l >> 5, jj = l & 31;
+    const int nto = (jb.FO + 31) >> 5, nti = (jb.FI + 31) >> 5, ntile = nto * nti;
+    f32x16 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
+    float bsum = 0.0f;  // bias partial of output row tid (tid < FO)
+    for (int pb = p0; pb < p1; pb += kWgT) {
+        const int np = min(kWgT, p1 - pb);
+        __syncthreads();
+        for (int e = tid; e < 128 * kWgT; e += 256) {
+            const int row = e / kWgT, col = e - row * kWgT;
+            const bool in = col < np;
+            Ds[row][col] = (row < jb.FO && in) ? jb.D[(size_t)row * a.N + pb + col] : 0.0f;
+            Xs[row][col] = (row < jb.FI && in) ? jb.X[(size_t)row * a.N + pb + col] : 0.0f;
+        }
+        __syncthreads();
+        if (tid < jb.FO)
+            for (int k = 0; k < np; ++k) bsum += Ds[tid][k];
+        // wave wid takes tiles wid, wid + 4, ... (<= 4 per wave at 128 x 128)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = wid + 4 * q;
+            if (t >= ntile) break;
+            const int to = t / nti, ti = t - to * nti;
+            for (int s = 0; s < kWgT / 2; ++s) {
+                const int k = 2 * s + h;
+                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[32 * to + jj][k], Xs[32 * ti + jj][k],
+                                                              acc[q], 0, 0, 0);
+            }
+        }
+    }
+    // D[o][i]: lane (jj, h) holds rows frow(r, h) of column jj
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int t = wid + 4 * q;
+        if (t >= ntile) break;
+        const int to = t / nti, ti = t - to * nti;
+        const int col = 32 * ti + jj;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 32 * to + frow(r, h);
+            if (row < jb.FO && col < jb.FI)
+                jb.part[((size_t)c * jb.FO + row) * jb.FI + col] = acc[q][r];
+        }
+    }
+    if (tid < jb.FO)
+        jb.part[(size_t)nchunk * jb.FO * jb.FI + (size_t)c * jb.FO + tid] = bsum;
+}
+
+struct ReduceJob {
+    const float *part;
+    int FO, FI;
+    float *gw, *gb;   // [FO][FI], [FO]
+};
+struct ReduceArgs {
+    ReduceJob job[8];
+    int nchunk;
+};
+
+__global__ __launch_bounds__(256) void ndp_wgrad_reduce(ReduceArgs a) {
+    const ReduceJob jb = a.job[blockIdx.y];
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int nw = jb.FO * jb.FI;
+    if (e < nw) {
+        float s = 0.0f;
+        for (int c = 0; c < a.nchunk; ++c) s += jb.part[(size_t)c * nw + e];
+        jb.gw[e] = s;
+    } else if (e < nw + jb.FO) {
+        const int o = e - nw;
+        float s = 0.0f;
+        for (int c = 0; c < a.nchunk; ++c) s += jb.part[(size_t)a.nchunk * nw + (size_t)c * jb.FO + o];
+        jb.gb[o] = s;
+    }
+}
+
+}  // namespace
+}  // namespace pcr
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+static int fill_train(const pcr_ndp_train *t, pcr::TrainArgs &a) {
+    PCR_REQUIRE(t, PCR_ERR_ARG, "ndp_train: null descriptor");
+    PCR_REQUIRE(t->N >= 0 && t->width == 128, PCR_ERR_ARG, "ndp_train: width %d (only 128)", t->width);
+    PCR_REQUIRE(t->depth >= 1 && t->depth - 1 <= pcr::kMaxHid, PCR_ERR_ARG, "ndp_train: depth %d", t->depth);
+    const pcr_ndp_level &L = t->level;
+    PCR_REQUIRE(L.w_in && L.b_in && L.w_rot && L.b_rot && L.w_trn && L.b_trn && (!L.w_nr || L.b_nr),
+                PCR_ERR_ARG, "ndp_train: null weight");
+    a = pcr::TrainArgs{};
+    a.x = t->x; a.N = t->N; a.W = t->width; a.nhid = t->depth - 1; a.m = L.m; a.k0 = t->k0;
+    a.w_in = L.w_in; a.b_in = L.b_in;
+    for (int k = 0; k < a.nhid; ++k) {
+        PCR_REQUIRE(t->w_hid[k] && t->b_hid[k], PCR_ERR_ARG, "ndp_train: null hidden layer %d", k);
+        a.w_hid[k] = t->w_hid[k];
+        a.b_hid[k] = t->b_hid[k];
+    }
+    a.w_rot = L.w_rot; a.b_rot = L.b_rot; a.w_trn = L.w_trn; a.b_trn = L.b_trn;
+    a.w_nr = L.w_nr; a.b_nr = L.b_nr;
+    a.pe = t->pe; a.H = t->H; a.aux = t->aux; a.x_out = t->x_out;
+    a.g = t->g; a.bce_scale = t->bce_scale; a.dO = t->dO; a.D = t->D;
+    return PCR_OK;
+}
+
+extern "C" int pcr_ndp_train_forward(const pcr_ndp_train *t, pcr_stream_t stream) {
+    pcr::clear_error();
+    pcr::TrainArgs a;
+    int rc = fill_train(t, a);
+    if (rc != PCR_OK) return rc;
+    if (a.N == 0) return PCR_OK;
+    PCR_REQUIRE(a.x && a.pe && a.H && a.aux && a.x_out, PCR_ERR_ARG, "ndp_train_forward: null buffer");
+    hipLaunchKernelGGL(pcr::ndp_train_fwd<4>, dim3((a.N + 127) / 128), dim3(256), 0,
+                       pcr::as_stream(stream), a);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+extern "C" int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32_t chunk,
+                                      float *const *grads, pcr_stream_t stream) {
+    pcr::clear_error();
+    pcr::TrainArgs a;
+    int rc = fill_train(t, a);
+    if (rc != PCR_OK) return rc;
+    if (a.N == 0) return PCR_OK;
+    PCR_REQUIRE(a.g && a.dO && a.D && part && grads, PCR_ERR_ARG, "ndp_train_backward: null buffer");
+    PCR_REQUIRE(chunk >= 64 && chunk % 64 == 0, PCR_ERR_ARG, "ndp_train_backward: chunk %d", chunk);
+    hipStream_t s = pcr::as_stream(stream);
+    hipLaunchKernelGGL(pcr::ndp_train_bwd<4>, dim3((a.N + 127) / 128), dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    // jobs: input layer (W x 6 over pe), hidden layers, branches (7 x W over H_last)
+    const int W = a.W, N = a.N, nchunk = (N + chunk - 1) / chunk;
+    pcr::WgradArgs wa{};
+    pcr::ReduceArgs ra{};
+    wa.N = N; wa.chunk = chunk; ra.nchunk = nchunk;
+    int nj = 0;
+    size_t off = 0;
+    auto add = [&](const float *D, const float *X, int FO, int FI, float *gw, float *gb) {
+        wa.job[nj] = pcr::WgradJob{D, X, FO, FI, part + off};
+        ra.job[nj] = pcr::ReduceJob{part + off, FO, FI, gw, gb};
+        off += (size_t)nchunk * ((size_t)FO * FI + FO);
+        ++nj;
+    };
+    // grads: [0] w_in [1] b_in, then per hidden layer (w, b), then w_branch (8 x W rows
+    // rot 0-2, trn 3-5, nr 6), b_branch (8)
+    add(a.D, a.pe, W, 6, grads[0], grads[1]);
+    for (int k = 0; k < a.nhid; ++k)
+        add(a.D + (size_t)(k + 1) * W * N, a.H + (size_t)k * W * N, W, W, grads[2 + 2 * k],
+            grads[3 + 2 * k]);
+    add(a.dO, a.H + (size_t)a.nhid * W * N, 7, W, grads[2 + 2 * a.nhid], grads[3 + 2 * a.nhid]);
+    hipLaunchKernelGGL(pcr::ndp_wgrad, dim3(nchunk, nj), dim3(256), 0, s, wa);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(pcr::ndp_wgrad_reduce, dim3((W * W + W + 255) / 256, nj), dim3(256), 0, s, ra);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+extern "C" int64_t pcr_ndp_train_partial_floats(int32_t N, int32_t width, int32_t depth, int32_t chunk) {
+    if (N <= 0 || chunk <= 0) return 0;
+    const int64_t nchunk = (N + chunk - 1) / chunk, W = width;
+    return nchunk * ((W * 6 + W) + (int64_t)(depth - 1) * (W * W + W) + (7 * W + 7));
+}

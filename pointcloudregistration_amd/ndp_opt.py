@@ -242,7 +242,139 @@ class _Level:
             g.replay()
 
 
-def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, use_graph=True):
+class _NdpLevelC(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("w_in", "b_in", "w_hid", "b_hid", "w_rot", "b_rot",
+                                               "w_trn", "b_trn", "w_nr", "b_nr")] + \
+        [("m", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class _TrainC(ctypes.Structure):
+    """pcr_ndp_train (include/pcr_api.h)."""
+    _fields_ = [("x", ctypes.c_void_p), ("N", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("depth", ctypes.c_int32), ("k0", ctypes.c_int32), ("level", _NdpLevelC),
+                ("w_hid", ctypes.c_void_p * 4), ("b_hid", ctypes.c_void_p * 4),
+                ("pe", ctypes.c_void_p), ("H", ctypes.c_void_p), ("aux", ctypes.c_void_p),
+                ("x_out", ctypes.c_void_p), ("g", ctypes.c_void_p), ("bce_scale", ctypes.c_double),
+                ("dO", ctypes.c_void_p), ("D", ctypes.c_void_p)]
+
+
+class _LevelFused(_Level):
+    """One level with the warp forward/backward and the weight gradients on libpcr
+    kernels (csrc/ndp_train.hip) instead of torch autograd; same loss, same
+    early-stop rule and Adam (pcr_ndp_control / pcr_adam_masked)."""
+
+    CHUNK = 128
+
+    def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig):
+        sd = dict(layer.named_parameters())
+        self.W = sd["input.0.weight"].shape[0]
+        self.nhid = sum(1 for k in sd if k.startswith("mlp.pts_linears.") and k.endswith(".weight"))
+        if self.W != 128 or self.nhid > 4:
+            raise NotImplementedError("fused NDP training: width 128, depth <= 5")
+        super().__init__(layer, s_sample, t_sample, inds, level, cfg)
+        dev, N, W, d = s_sample.device, s_sample.shape[0], self.W, self.nhid + 1
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.N = N
+        self.pe = torch.zeros(6, N, **f32)
+        self.H = torch.zeros(d, W, N, **f32)
+        self.aux = torch.zeros(8, N, **f32)
+        self.dO = torch.zeros(8, N, **f32)
+        self.D = torch.zeros(d, W, N, **f32)
+        self.gx = torch.zeros(N, 3, **f32)
+        self.xo = torch.zeros(N, 3, **f32)
+        nparts = _lib.load().pcr_ndp_train_partial_floats(N, W, d, self.CHUNK)
+        self.part = torch.zeros(max(int(nparts), 1), **f32)
+        # gradient buffers in the kernel's order; the Adam table must see the same
+        # storage, so the branch parameters' grads are row views of one buffer
+        self.gw_b = torch.zeros(7, W, **f32)
+        self.gb_b = torch.zeros(7, **f32)
+        names = [n for n, _ in layer.named_parameters()]
+        view = {"rot_brach.weight": self.gw_b[0:3], "rot_brach.bias": self.gb_b[0:3],
+                "trn_branch.weight": self.gw_b[3:6], "trn_branch.bias": self.gb_b[3:6],
+                "nr_branch.weight": self.gw_b[6:7], "nr_branch.bias": self.gb_b[6:7]}
+        own = {n: torch.zeros_like(p) for n, p in layer.named_parameters() if n not in view}
+        order = ["input.0.weight", "input.0.bias"]
+        for k in range(self.nhid):
+            order += [f"mlp.pts_linears.{k}.weight", f"mlp.pts_linears.{k}.bias"]
+        kernel_grads = [own[n] for n in order] + [self.gw_b, self.gb_b]
+        self.grad_ptrs = (ctypes.c_void_p * len(kernel_grads))(*[g.data_ptr() for g in kernel_grads])
+        self._keep = kernel_grads
+        self.grads = [view[n] if n in view else own[n] for n in names]
+        self._rebuild_table()
+        t = _TrainC()
+        t.x, t.N, t.width, t.depth, t.k0 = s_sample.data_ptr(), N, W, d, int(layer.k0)
+        lv = _NdpLevelC()
+        lv.w_in, lv.b_in = sd["input.0.weight"].data_ptr(), sd["input.0.bias"].data_ptr()
+        lv.w_rot, lv.b_rot = sd["rot_brach.weight"].data_ptr(), sd["rot_brach.bias"].data_ptr()
+        lv.w_trn, lv.b_trn = sd["trn_branch.weight"].data_ptr(), sd["trn_branch.bias"].data_ptr()
+        self.has_nr = "nr_branch.weight" in sd
+        if self.has_nr:
+            lv.w_nr, lv.b_nr = sd["nr_branch.weight"].data_ptr(), sd["nr_branch.bias"].data_ptr()
+        lv.m = int(layer.m)
+        t.level = lv
+        for k in range(self.nhid):
+            t.w_hid[k] = sd[f"mlp.pts_linears.{k}.weight"].data_ptr()
+            t.b_hid[k] = sd[f"mlp.pts_linears.{k}.bias"].data_ptr()
+        t.pe, t.H, t.aux, t.x_out = (self.pe.data_ptr(), self.H.data_ptr(), self.aux.data_ptr(),
+                                     self.xo.data_ptr())
+        t.g = self.gx.data_ptr()
+        self.bce_on = level > 0 and cfg.w_reg > 0 and self.has_nr
+        t.bce_scale = (cfg.w_reg / N) if self.bce_on else 0.0
+        t.dO, t.D = self.dO.data_ptr(), self.D.data_ptr()
+        self.desc = t
+        K, M = inds.shape[0], t_sample.shape[0]
+        self.K, self.M = K, M
+        self.d1 = torch.zeros(1, K, **f32)
+        self.d2 = torch.zeros(1, M, **f32)
+        self.i1 = torch.zeros(1, K, dtype=torch.int32, device=dev)
+        self.i2 = torch.zeros(1, M, dtype=torch.int32, device=dev)
+        self.gsub = torch.zeros(1, K, 3, **f32)
+        self.gt = torch.zeros(1, M, 3, **f32)
+        self.t3 = t_sample[None].contiguous()
+
+    def _rebuild_table(self):
+        tab = (_AdamTensor * len(self.params))()
+        for k, (p, g, m, v) in enumerate(zip(self.params, self.grads, self.m, self.v)):
+            tab[k] = _AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), 0)
+        raw = np.frombuffer(bytes(tab), dtype=np.uint8).copy()
+        self.table = torch.from_numpy(raw).to(self.s.device)
+
+    def step(self):
+        from .nndistance import nnd_backward_cuda, nnd_forward_cuda
+        cfg = self.cfg
+        st = _lib.stream_handle(self.s.device)
+        desc = ctypes.byref(self.desc)
+        _lib.call("pcr_ndp_train_forward", desc, st)
+        xs = self.xo.index_select(0, self.inds)[None].contiguous()
+        nnd_forward_cuda(xs, self.t3, self.d1, self.d2, self.i1, self.i2)
+        trunc = 1e9
+        c1 = torch.where(self.d1 >= trunc, torch.zeros_like(self.d1), self.d1)
+        c2 = torch.where(self.d2 >= trunc, torch.zeros_like(self.d2), self.d2)
+        loss = c1.sum() / self.K + c2.sum() / self.M
+        gd1 = torch.where(self.d1 >= trunc, torch.zeros_like(self.d1),
+                          torch.full_like(self.d1, 1.0 / self.K))
+        gd2 = torch.where(self.d2 >= trunc, torch.zeros_like(self.d2),
+                          torch.full_like(self.d2, 1.0 / self.M))
+        nnd_backward_cuda(xs, self.t3, self.gsub, self.gt, gd1, gd2, self.i1, self.i2)
+        self.gx.zero_()
+        self.gx.index_add_(0, self.inds, self.gsub[0])
+        if self.bce_on:
+            sv = self.aux[6]
+            loss = loss + cfg.w_reg * torch.mean(-torch.clamp(torch.log(1 - sv), min=-100.0))
+        _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
+                  ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
+        self.loss.copy_(loss)
+        self.log.index_copy_(0, torch.clamp(self.ctr, max=self.cfg.iters), self.loss.reshape(1))
+        self.ctr += 1
+        self.warped.copy_(self.xo)
+        _lib.call("pcr_ndp_control", _lib.ptr(self.loss), _lib.ptr(self.state),
+                  float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4, st)
+        _lib.call("pcr_adam_masked", _lib.ptr(self.table), len(self.params), self.max_numel,
+                  _lib.ptr(self.state), float(cfg.lr), 0.9, 0.999, 1e-8, st)
+
+
+def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, use_graph=True,
+                                 fused=True):
     """Returns (warped_pcd (N, 3) cuda f32, hist (levels + 1, N_s, 3) numpy, iter_cnt) like
     the reference, plus ``info`` per level {steps, evaluated, last_loss}.  ``NDP`` may be
     the reference's Deformation_Pyramid (SE3 / axis_angle) or this module's mirror;
@@ -264,7 +396,9 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
     hist, info = [], []
     for level in range(NDP.n_hierarchy):
         NDP.gradient_setup(optimized_level=level)
-        lv = _Level(NDP.pyramid[level], s_sample, t_sample, ind, level, cfg)
+        layer = NDP.pyramid[level]
+        use_fused = fused and layer.input[0].weight.shape[0] == 128
+        lv = (_LevelFused if use_fused else _Level)(layer, s_sample, t_sample, ind, level, cfg)
         lv.run(use_graph)
         st = lv.state.cpu().numpy()
         info.append({"steps": int(st[3]), "evaluated": int(st[6]), "last_loss": float(st[4]),

@@ -1,0 +1,82 @@
+"""GPU: the fused NDP level step (csrc/ndp_train.hip) against torch autograd of
+the same layer (the reference's NDPLayer restated in ndp_opt.NDPLayer, whose
+warp matches the reference's own to 1e-6: test_ndp_opt_cpu.py).
+
+Tolerance: forward x' to 2e-6 absolute (f32, different summation order of the
+MFMA chains vs hipBLASLt); gradients to 2e-4 of each tensor's largest entry (f32
+sums over 3000 points in different orders)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from pointcloudregistration_amd import _lib, ndp_opt
+
+pytestmark = pytest.mark.gpu
+
+
+def _layer(level, seed, scale=3.0):
+    torch.manual_seed(seed)
+    L = ndp_opt.NDPLayer(3, 128, -8, level + 1, nonrigidity_est=level > 0).cuda()
+    with torch.no_grad():
+        for p in L.parameters():
+            if p.dim() > 1:
+                p.mul_(scale)  # far from the identity warp of a fresh init
+            else:
+                p.uniform_(-0.2, 0.2)
+    return L
+
+
+@pytest.mark.parametrize("level", [0, 1, 5])
+def test_fused_forward_and_gradients_match_autograd(level):
+    rng = np.random.default_rng(level)
+    N = 3000
+    x = torch.from_numpy(rng.uniform(-0.8, 0.8, (N, 3)).astype(np.float32)).cuda()
+    t = torch.from_numpy(rng.uniform(-0.8, 0.8, (500, 3)).astype(np.float32)).cuda()
+    inds = torch.arange(0, N, 3, device="cuda")
+    L = _layer(level, 10 + level)
+    cfg = ndp_opt.NDPConfig(w_reg=0.05)
+    lv = ndp_opt._LevelFused(L, x, t, inds, level, cfg)
+    st = _lib.stream_handle()
+    _lib.call("pcr_ndp_train_forward", ctypes.byref(lv.desc), st)
+    xo, nr = L(x)
+    assert torch.allclose(lv.xo, xo.detach(), atol=2e-6, rtol=0)
+    if nr is not None:
+        assert torch.allclose(lv.aux[6], nr.detach(), atol=2e-6, rtol=0)
+    g = torch.from_numpy(rng.standard_normal((N, 3)).astype(np.float32)).cuda()
+    lv.gx.copy_(g)
+    _lib.call("pcr_ndp_train_backward", ctypes.byref(lv.desc), _lib.ptr(lv.part), lv.CHUNK,
+              ctypes.cast(lv.grad_ptrs, ctypes.c_void_p), st)
+    loss = (xo * g).sum()
+    if lv.bce_on:
+        loss = loss + cfg.w_reg * torch.mean(-torch.log(1 - nr))
+    want = torch.autograd.grad(loss, lv.params)
+    torch.cuda.synchronize()
+    for (name, _), got, w in zip(L.named_parameters(), lv.grads, want):
+        tol = 2e-4 * float(w.abs().max()) + 1e-12
+        assert torch.allclose(got, w, atol=tol, rtol=0), (name, float((got - w).abs().max()), tol)
+
+
+def test_fused_optimisation_close_to_autograd_path():
+    """The whole level loop: fused kernels vs the autograd path (same graph-captured
+    control + Adam): losses to 1e-4 relative, warped points to 1e-4."""
+    rng = np.random.default_rng(3)
+    n = 2500
+    u = rng.standard_normal((n, 3))
+    src = (u / np.linalg.norm(u, axis=1, keepdims=True) * 0.6).astype(np.float32)
+    w = rng.standard_normal((2000, 3))
+    tgt = (w / np.linalg.norm(w, axis=1, keepdims=True) * 0.6 + 0.05).astype(np.float32)
+    inds = np.sort(rng.choice(n, 2000, replace=False))
+    cfg = dict(iters=10, m=3)
+
+    def run(fused):
+        torch.manual_seed(0)
+        P = ndp_opt.DeformationPyramid(3, 128, torch.device("cuda"), -8, 3, True)
+        return ndp_opt.optimize_deformation_pyramid(torch.from_numpy(src).cuda(),
+                                                    torch.from_numpy(tgt).cuda(), inds, cfg,
+                                                    NDP=P, fused=fused)
+    a, b = run(True), run(False)
+    for x, y in zip(a[3], b[3]):
+        np.testing.assert_allclose(x["losses"], y["losses"], rtol=1e-4)
+    assert torch.allclose(a[0], b[0], atol=1e-4)
