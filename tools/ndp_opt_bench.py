@@ -17,6 +17,9 @@ w = rng.standard_normal((n, 3))
 w = w / np.linalg.norm(w, axis=1, keepdims=True)
 tgt = (w + 0.05 * np.sin(3 * w[:, [1, 2, 0]])).astype(np.float32)
 inds = np.sort(rng.choice(n, 5000, replace=False))
+if os.environ.get("BLAS"):
+    torch.backends.cuda.preferred_blas_library(os.environ["BLAS"])
+    print("blas", torch.backends.cuda.preferred_blas_library())
 cfg = ndp_opt.NDPConfig(max_break_count=10**6, m=int(os.environ.get("LEVELS", "9")))
 S, G = torch.from_numpy(src).cuda(), torch.from_numpy(tgt).cuda()
 for rep in range(2):
