@@ -19,6 +19,7 @@
 // Numerics: d = (dx*dx + dy*dy) + dz*dz, each op rounded (built with
 // -ffp-contract=off), dx = cand.x - query.x as in my_lib.cpp:12-15.
 #include "pcr_internal.h"
+#include "scan.h"
 #include <cstdlib>
 #include <math.h>
 
@@ -219,36 +220,7 @@ __global__ __launch_bounds__(1024) void bw_scan(BwdArgs a) {
     int nsrc, ntgt; const int32_t *tidx; int *cnt, *start, *uns, *srt;
     const int dir = blockIdx.z & 1, bat = blockIdx.z >> 1;
     bw_dir(a, dir, nsrc, ntgt, tidx, cnt, start, uns, srt);
-    __shared__ int warp_tot[16];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    int *c = cnt + (size_t)bat * ntgt;
-    int *s = start + (size_t)bat * (ntgt + 1);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int base = 0; base < ntgt; base += 1024) {
-        const int i = base + threadIdx.x;
-        const int v = (i < ntgt) ? c[i] : 0;
-        int x = v;  // inclusive wave scan
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) warp_tot[wid] = x;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int acc = 0;
-            for (int w = 0; w < 16; ++w) { const int t = warp_tot[w]; warp_tot[w] = acc; acc += t; }
-        }
-        __syncthreads();
-        const int excl = carry + warp_tot[wid] + x - v;
-        if (i < ntgt) { s[i] = excl; c[i] = 0; }
-        __syncthreads();
-        if (threadIdx.x == 1023) carry = excl + v;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) s[ntgt] = carry;
+    pcr::block_exclusive_scan_1024(cnt + (size_t)bat * ntgt, start + (size_t)bat * (ntgt + 1), ntgt, true);
 }
 
 __global__ void bw_fill(BwdArgs a) {

@@ -17,11 +17,12 @@
 // exceeds the best distance (strictly) the answer is final.  Rings are capped
 // at kMaxRing, then the query scans every point (same exact rule).
 //
-// One thread per query, 256-thread blocks over all pairs and both directions,
+// One thread (or LPQ lanes) per query, 256-thread blocks over all pairs and both directions,
 // ordered per XCD (xcd_slot) so each grid (160 KB per 8192-point cloud) is
 // served from one XCD's L2.
 #include "pcr_internal.h"
 #include "scan.h"
+#include <cstdlib>
 
 namespace pcr {
 namespace {
@@ -48,21 +49,22 @@ __device__ __forceinline__ unsigned nhash(int x, int y, int z, int S) {
 
 __device__ __forceinline__ int ccoord(float v, double ic) { return (int)__builtin_floor((double)v * ic); }
 
-__global__ __launch_bounds__(256) void nng_bbox(NgArgs a) {
+__global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
     const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x, n = a.n[s];
     const float *P = a.xyz[s] + (size_t)b * n * 3;
     float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
     int bad = 0;
-    for (int i = t; i < n; i += 256)
+#pragma unroll 4
+    for (int i = t; i < n; i += 1024)
         for (int c = 0; c < 3; ++c) {
             const float v = P[3 * i + c];
             bad |= !__builtin_isfinite(v);
             lo[c] = fminf(lo[c], v);
             hi[c] = fmaxf(hi[c], v);
         }
-    __shared__ float sl[3][4], sh[3][4];
-    __shared__ int sb[4];
+    __shared__ float sl[3][16], sh[3][16];
+    __shared__ int sb[16];
     for (int c = 0; c < 3; ++c)
         for (int o = 32; o; o >>= 1) {
             lo[c] = fminf(lo[c], __shfl_xor(lo[c], o, 64));
@@ -78,12 +80,13 @@ __global__ __launch_bounds__(256) void nng_bbox(NgArgs a) {
     double e[3], m = 0.0, amax = 0.0;
     for (int c = 0; c < 3; ++c) {
         float l = sl[c][0], h = sh[c][0];
-        for (int w = 1; w < 4; ++w) { l = fminf(l, sl[c][w]); h = fmaxf(h, sh[c][w]); }
+        for (int w = 1; w < 16; ++w) { l = fminf(l, sl[c][w]); h = fmaxf(h, sh[c][w]); }
         e[c] = (double)h - (double)l;
         m = fmax(m, e[c]);
         amax = fmax(amax, fmax(fabs((double)l), fabs((double)h)));
     }
-    bad = sb[0] | sb[1] | sb[2] | sb[3];
+    bad = 0;
+    for (int w = 0; w < 16; ++w) bad |= sb[w];
     double cell = 1.0;
     if (m > 0.0) {
         double v = 1.0;
@@ -138,12 +141,22 @@ __device__ __forceinline__ int xcd_slot(int L, int total) {
     return (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + k;
 }
 
+// LPQ lanes per query.  A batch fills the chip with one thread per query; a
+// single pair (the NDP Chamfer, quality metrics: ~25K queries) does not, and its
+// per-query cell walks are long dependent load chains.  With LPQ > 1 the lanes
+// of a query split each ring's (dx, dy) columns (and the fallback scan) and
+// merge their (d, j) minima before the certification test; the minimum of
+// (d, j) pairs does not depend on the merge order, so every LPQ gives the same
+// answer.
+template <int LPQ>
 __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
+    constexpr int QPB = 256 / LPQ;
     const int w = xcd_slot(blockIdx.x, gridDim.x);
     const int grp = w / nchunk, chunk = w - grp * nchunk;
-    const int dir = grp / a.B, b = grp - dir * a.B, qi = chunk * blockDim.x + threadIdx.x;
+    const int dir = grp / a.B, b = grp - dir * a.B;
+    const int sub = threadIdx.x % LPQ, qi = chunk * QPB + threadIdx.x / LPQ;
     const int qs = dir, gs = 1 - dir;  // queries from set dir, candidates from the other set
-    if (qi >= a.n[qs]) return;
+    if (qi >= a.n[qs]) return;  // a query's lanes leave together
     const float *q = a.xyz[qs] + ((size_t)b * a.n[qs] + qi) * 3;
     const float qx = q[0], qy = q[1], qz = q[2];
     const int m = a.n[gs];
@@ -151,13 +164,23 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
     float best = __builtin_inff();
     int bj = 0x7fffffff;
     bool done = false;
+    auto merge = [&]() {
+#pragma unroll
+        for (int o = 1; o < LPQ; o <<= 1) {
+            const float ob = __shfl_xor(best, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+        }
+    };
     if (a.flag[b]) {
         // the reference loop: seed with candidate 0, strict < (my_lib.cpp:11-20)
-        best = d2f(C[0], C[1], C[2], qx, qy, qz);
-        bj = 0;
-        for (int j = 1; j < m; ++j) {
-            const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
-            if (d < best) { best = d; bj = j; }
+        if (sub == 0) {
+            best = d2f(C[0], C[1], C[2], qx, qy, qz);
+            bj = 0;
+            for (int j = 1; j < m; ++j) {
+                const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
+                if (d < best) { best = d; bj = j; }
+            }
         }
         done = true;
     }
@@ -180,16 +203,18 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
             }
         };
         for (int k = 0; k <= kMaxRing && !done; ++k) {
-            for (int dx = -k; dx <= k; ++dx)
-                for (int dy = -k; dy <= k; ++dy) {
-                    const bool face = (dx == -k || dx == k || dy == -k || dy == k);
-                    if (face) {
-                        for (int dz = -k; dz <= k; ++dz) scan_cell(cx + dx, cy + dy, cz + dz);
-                    } else {
-                        scan_cell(cx + dx, cy + dy, cz - k);
-                        scan_cell(cx + dx, cy + dy, cz + k);
-                    }
+            // column c = (dx, dy) of ring k; lane sub takes columns sub, sub + LPQ, ...
+            const int side = 2 * k + 1;
+            for (int c = sub; c < side * side; c += LPQ) {
+                const int cq = c / side, dx = cq - k, dy = c - cq * side - k;
+                if (dx == -k || dx == k || dy == -k || dy == k) {
+                    for (int dz = -k; dz <= k; ++dz) scan_cell(cx + dx, cy + dy, cz + dz);
+                } else {
+                    scan_cell(cx + dx, cy + dy, cz - k);
+                    scan_cell(cx + dx, cy + dy, cz + k);
                 }
+            }
+            merge();
             // distance from q to the faces of the visited (2k+1)^3 block
             const double gx = fmin((double)qx - (double)(cx - k) * cell, (double)(cx + k + 1) * cell - (double)qx);
             const double gy = fmin((double)qy - (double)(cy - k) * cell, (double)(cy + k + 1) * cell - (double)qy);
@@ -198,14 +223,17 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
             if (gmin > 0.0 && gmin * gmin * (1.0 - 8.0 * 5.9604644775390625e-08) > (double)best) done = true;
         }
         if (!done) {  // not certified within kMaxRing rings: every candidate
-            for (int j = 0; j < m; ++j) {
+            for (int j = sub; j < m; j += LPQ) {
                 const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
                 if (d < best || (d == best && j < bj)) { best = d; bj = j; }
             }
+            merge();
         }
     }
-    a.dist[dir][(size_t)b * a.n[qs] + qi] = best;
-    a.idx[dir][(size_t)b * a.n[qs] + qi] = bj;
+    if (sub == 0) {
+        a.dist[dir][(size_t)b * a.n[qs] + qi] = best;
+        a.idx[dir][(size_t)b * a.n[qs] + qi] = bj;
+    }
 }
 
 }  // namespace
@@ -228,7 +256,7 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
     a.start = a.hcnt + hc;
     a.dist[0] = dist1; a.dist[1] = dist2; a.idx[0] = idx1; a.idx[1] = idx2;
     PCR_HIP_CHECK(hipMemsetAsync(a.flag, 0, sizeof(int) * (b + hc), s));
-    hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(1024), 0, s, a);
     PCR_LAUNCH_CHECK();
     const dim3 pg((a.nmax + 255) / 256, b, 2);
     hipLaunchKernelGGL(nng_count, pg, dim3(256), 0, s, a);
@@ -239,8 +267,23 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
     hipLaunchKernelGGL(nng_scatter, pg, dim3(256), 0, s, a);
     PCR_LAUNCH_CHECK();
     prof_begin(s, kProfNndGrid);
-    const int nchunk = (a.nmax + 255) / 256;
-    hipLaunchKernelGGL(nng_query, dim3(2 * b * nchunk), dim3(256), 0, s, a, nchunk);
+    // lanes per query: one thread per query once the launch fills the chip
+    // (PCR_NND_LPQ = 1|2|4|8|16 overrides)
+    const long long nq = (long long)b * (n + m);
+    int lpq = nq >= (1LL << 18) ? 1 : nq >= (1LL << 16) ? 4 : 8;
+    if (const char *e = getenv("PCR_NND_LPQ")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) lpq = v;
+    }
+    const int nchunk = (a.nmax + 256 / lpq - 1) / (256 / lpq);
+    const dim3 qg(2 * b * nchunk), qb(256);
+    switch (lpq) {
+        case 1: hipLaunchKernelGGL(nng_query<1>, qg, qb, 0, s, a, nchunk); break;
+        case 2: hipLaunchKernelGGL(nng_query<2>, qg, qb, 0, s, a, nchunk); break;
+        case 4: hipLaunchKernelGGL(nng_query<4>, qg, qb, 0, s, a, nchunk); break;
+        case 8: hipLaunchKernelGGL(nng_query<8>, qg, qb, 0, s, a, nchunk); break;
+        default: hipLaunchKernelGGL(nng_query<16>, qg, qb, 0, s, a, nchunk); break;
+    }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfNndGrid);
     return PCR_OK;

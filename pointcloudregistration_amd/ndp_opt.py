@@ -238,8 +238,12 @@ class _Level:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.step()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
         for _ in range(iters):
             g.replay()
+        ev[1].record()
+        self.replay_events = ev
 
 
 class _NdpLevelC(ctypes.Structure):
@@ -403,6 +407,9 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
         st = lv.state.cpu().numpy()
         info.append({"steps": int(st[3]), "evaluated": int(st[6]), "last_loss": float(st[4]),
                      "losses": lv.log[:int(st[6])].cpu().numpy()})
+        ev = getattr(lv, "replay_events", None)
+        if ev is not None:
+            info[-1]["replay_ms"] = ev[0].elapsed_time(ev[1])
         hist.append((lv.warped + tgt_mean).cpu().numpy())
         s_sample = lv.warped.clone()
     NDP.gradient_setup(optimized_level=-1)

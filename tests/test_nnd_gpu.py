@@ -174,3 +174,27 @@ def test_nnd_grid_adversarial_vs_oracle(oracle, monkeypatch, kind):
     for k, g, e in zip(("d1", "d2", "i1", "i2", "g1", "g2"), got, (e1, e2, j1, j2, eg1, eg2)):
         assert_bitexact(g, e, f"{kind}/{k}")
 
+
+@pytest.mark.parametrize("lpq", ["1", "2", "4", "8", "16"])
+@pytest.mark.parametrize("kind", ["outliers", "quantised", "identical", "nan", "random"])
+def test_nnd_grid_lanes_per_query_vs_oracle(oracle, monkeypatch, kind, lpq):
+    """Splitting each query's ring columns and fallback scan over LPQ lanes
+    (PCR_NND_LPQ; the size rule picks 8 for one pair, 1 for C4 batches) keeps
+    the exact (d, j) answer, ties and the non-finite reference loop included."""
+    monkeypatch.setenv("PCR_NND_ALGO", "grid")
+    monkeypatch.setenv("PCR_NND_LPQ", lpq)
+    rng = np.random.default_rng(len(kind) + 100)
+    if kind == "random":  # the NDP Chamfer shape: a 5000-point subset vs 20000 targets
+        x1 = (rng.random((1, 5000, 3), dtype=np.float32) * 2 - 1).astype(np.float32)
+        x2 = (rng.random((1, 20000, 3), dtype=np.float32) * 2 - 1).astype(np.float32)
+    else:
+        x1, x2 = _adversarial(kind, rng)
+    gd1 = rng.standard_normal(x1.shape[:2]).astype(np.float32)
+    gd2 = rng.standard_normal(x2.shape[:2]).astype(np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        got = _run_fwd_bwd(x1, x2, gd1, gd2)
+        e1, e2, j1, j2 = oracle.nnd_forward(x1, x2)
+        eg1, eg2 = oracle.nnd_backward(x1, x2, gd1, gd2, j1, j2)
+    for k, g, e in zip(("d1", "d2", "i1", "i2", "g1", "g2"), got, (e1, e2, j1, j2, eg1, eg2)):
+        assert_bitexact(g, e, f"{kind}/lpq{lpq}/{k}")
+
