@@ -370,11 +370,28 @@ typedef struct pcr_ndp_train {
     const float *g;
     double bce_scale;
     float *dO, *D;
+    /* optional Chamfer subset (null = off): inv (N) = k where inds[k] == p for a
+     * duplicate-free inds, else -1; the forward also writes x_out[inds] to xs (K,3)
+     * and the backward takes dL/dx_out of p from gsub[inv[p]] (0 off the subset)
+     * instead of g, i.e. g = index_add(zeros, inds, gsub) without materialising it */
+    const int32_t *inv;
+    float *xs;
+    const float *gsub;
 } pcr_ndp_train;
 int pcr_ndp_train_forward(const pcr_ndp_train *t, pcr_stream_t stream);
 int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32_t chunk,
                            float *const *grads, pcr_stream_t stream);
 int64_t pcr_ndp_train_partial_floats(int32_t N, int32_t width, int32_t depth, int32_t chunk);
+/* pcr_ndp_chamfer_glue: the loss of registration.py:231-244 around the Chamfer
+ *   pass, on the device, in a fixed reduction order:
+ *   loss = sum(d1')/K + sum(d2')/M (+ w_reg * mean(-max(log(1 - s), -100)) when s
+ *   is given), d' = d where d < trunc else 0; gd1 = 1/K and gd2 = 1/M where not
+ *   truncated, else 0 (the dist gradients for pcr_nnd_backward);
+ *   log[min(*ctr, log_last)] = loss; ++*ctr (device int64). */
+int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
+                         const float *s, int32_t N, double w_reg, double trunc,
+                         float *gd1, float *gd2, float *loss, float *log, int64_t *ctr,
+                         int32_t log_last, pcr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,13 +1,15 @@
 // f4: the fused NDP level training step -- one level's warp
-// forward with saved activations, the warp backward, and the weight gradients --
-// as libpcr kernels, so an optimisation iteration of
-// c2p-net/deformationpyramid/model/registration.py:208-262 is
-//   ndp_train_fwd -> nnd Chamfer fwd/bwd (a1/a2) -> ndp_train_bwd -> ndp_wgrad
-//   -> ndp_wgrad_reduce -> pcr_ndp_control -> pcr_adam_masked
+// forward with saved activations, the warp backward, the weight gradients and
+// the loss around the Chamfer pass -- as libpcr kernels, so an optimisation
+// iteration of c2p-net/deformationpyramid/model/registration.py:208-262 is
+//   ndp_train_fwd -> nnd Chamfer fwd (a1) -> ndp_chamfer_glue -> nnd Chamfer
+//   bwd (a2) -> ndp_train_bwd -> ndp_wgrad -> ndp_wgrad_reduce
+//   -> pcr_ndp_control -> pcr_adam_masked
 // with no PyTorch autograd on the path.  Semantics: NDPLayer.forward
 // (nets.py:111-140, motion SE3, rotation axis_angle, rigid_body.py:89-119) in
 // f32, its gradient by the chain rule written out below, nn.Linear weight
-// gradients dW = sum_p delta_p (x) a_p, bias gradients sum_p delta_p.
+// gradients dW = sum_p delta_p (x) a_p, bias gradients sum_p delta_p, and the
+// loss of :231-244 (truncated Chamfer means + w_reg * mean BCE(s, 0)).
 //
 // Layouts (N points of the level):
 //   activations H_l, deltas D_l, positional encoding, branch data: FEATURE-major
@@ -16,21 +18,29 @@
 //   GEMMs (K = points) read contiguous rows.
 //   aux [8][N]: r (3, = 1e-3 o_r), y = R x + t (3), s (nonrigidity), 0.
 //   dO [8][N]: dL/d(branch pre-activation): rot (3), trn (3), nr (1), 0.
-// MFMA mapping: as ndp.hip -- one wave owns 32 points, a 32-feature tile is 16
-// accumulator registers (feature frow(r, h) of point j); a layer is a chain of
-// exact-f32 v_mfma_f32_32x32x2_f32 whose B operand is the previous tile.  The
-// backward products use the transposed weights (A[i][k] = W[k][i], lanes read
+// MFMA mapping (ndp_tile.h): a 32-feature x 32-point tile is 16 accumulator
+// registers, a layer a chain of exact-f32 v_mfma_f32_32x32x2_f32 whose B operand
+// is the previous layer's tile; a workgroup of 4 waves owns 32 points, wave w
+// feature tile w of every layer, the tiles exchanged through LDS (a 20k-point
+// level runs 2,500 waves, not the 625 of one wave per 32 points).  The backward
+// products use the transposed weights (A[i][k] = W[k][i], lanes read
 // consecutive columns: coalesced).  Weight gradients are split-K GEMMs over
 // 128-point chunks with per-chunk partials reduced in chunk order
 // (deterministic).
 #include "pcr_internal.h"
+#include "ndp_tile.h"
 
 namespace pcr {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using ndpt::chain;
+using ndpt::f32x16;
+using ndpt::frow;
+using ndpt::publish;
+using ndpt::TileX;
 
 constexpr int kMaxHid = 4;
+constexpr int kNT = 4;  // width 128: 4 feature tiles, 4 waves per workgroup
 
 struct TrainArgs {
     const float *x;                 // (N, 3) level input
@@ -47,75 +57,70 @@ struct TrainArgs {
     double bce_scale;               // w_reg / N when the level has the nonrigidity branch, else 0
     float *dO;                      // [8][N]
     float *D;                       // [nhid + 1][W][N]: dL/d(pre-activation) of layer l
+    // Chamfer subset (optional): inv[p] = k when inds[k] == p (inds unique), else -1;
+    // the forward also writes x'[inds] to xs (K, 3), and the backward reads dL/dx'
+    // of point p from gsub[inv[p]] (zero off the subset) instead of g
+    const int32_t *inv;
+    float *xs;
+    const float *gsub;
 };
-
-__device__ __forceinline__ int frow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ float sgn_mask(float a, float d) { return a > 0.0f ? d : 0.0f; }
 
 // ---- forward of one level, saving what the backward needs -------------------
-template <int NT>
-__global__ __launch_bounds__(256) void ndp_train_fwd(TrainArgs a) {
-    constexpr int W = 32 * NT;
-    const int l = threadIdx.x & 63, h = l >> 5, j = l & 31;
-    const int pt = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + j;
+__global__ __launch_bounds__(64 * kNT) void ndp_train_fwd(TrainArgs a) {
+    constexpr int W = 32 * kNT;
+    __shared__ TileX X[kNT];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5, j = l & 31;
+    const int pt = blockIdx.x * 32 + j;
     const bool valid = pt < a.N;
     const int N = a.N;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
     if (valid) { x0 = a.x[3 * pt]; x1 = a.x[3 * pt + 1]; x2 = a.x[3 * pt + 2]; }
-    const float w = __builtin_ldexpf(1.0f, a.m + a.k0);
+    const float wf = __builtin_ldexpf(1.0f, a.m + a.k0);
     float pe[3];
     {
-        const float v0 = x0 * w, v1 = x1 * w, v2 = x2 * w;
+        const float v0 = x0 * wf, v1 = x1 * wf, v2 = x2 * wf;
         pe[0] = h ? cosf(v0) : sinf(v0);
         pe[1] = h ? cosf(v1) : sinf(v1);
         pe[2] = h ? cosf(v2) : sinf(v2);
-        if (valid)
+        if (valid && w == 0)
             for (int s = 0; s < 3; ++s) a.pe[(size_t)(2 * s + h) * N + pt] = pe[s];
     }
-    f32x16 H[NT];
+    f32x16 H;
 #pragma unroll
-    for (int ot = 0; ot < NT; ++ot) {
+    for (int r = 0; r < 16; ++r) H[r] = a.b_in[32 * w + frow(r, h)];
+    {
+        const float *wr = a.w_in + (32 * w + j) * 6;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) H[ot][r] = a.b_in[32 * ot + frow(r, h)];
-        const float *wr = a.w_in + (32 * ot + j) * 6;
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-            H[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[2 * s + h], pe[s], H[ot], 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) H[ot][r] = fmaxf(H[ot][r], 0.0f);
+        for (int s = 0; s < 3; ++s) H = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[2 * s + h], pe[s], H, 0, 0, 0);
     }
-    auto save = [&](int layer, const f32x16 *T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) H[r] = fmaxf(H[r], 0.0f);
+    auto save = [&](int layer) {
         if (!valid) return;
-        float *base = a.H + (size_t)layer * W * N + pt;
+        float *base = a.H + ((size_t)layer * W + 32 * w) * N + pt;
 #pragma unroll
-        for (int ot = 0; ot < NT; ++ot)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) base[(size_t)(32 * ot + frow(r, h)) * N] = T[ot][r];
+        for (int r = 0; r < 16; ++r) base[(size_t)frow(r, h) * N] = H[r];
     };
-    save(0, H);
+    save(0);
     for (int hl = 0; hl < a.nhid; ++hl) {
-        const float *Wm = a.w_hid[hl];
+        publish(X[w], l, H);
+        __syncthreads();
+        const float *wr = a.w_hid[hl] + (size_t)(32 * w + j) * W;
         const float *bm = a.b_hid[hl];
-        f32x16 Hn[NT];
+        f32x16 Hn;
 #pragma unroll
-        for (int ot = 0; ot < NT; ++ot) {
+        for (int r = 0; r < 16; ++r) Hn[r] = bm[32 * w + frow(r, h)];
+        Hn = chain<kNT>(X, l, [&](int it, int r) { return wr[32 * it + frow(r, h)]; }, Hn);
+        __syncthreads();
 #pragma unroll
-            for (int r = 0; r < 16; ++r) Hn[ot][r] = bm[32 * ot + frow(r, h)];
-            const float *wr = Wm + (size_t)(32 * ot + j) * W;
-#pragma unroll
-            for (int it = 0; it < NT; ++it)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    Hn[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32 * it + frow(r, h)], H[it][r],
-                                                                  Hn[ot], 0, 0, 0);
-        }
-#pragma unroll
-        for (int ot = 0; ot < NT; ++ot)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) H[ot][r] = fmaxf(Hn[ot][r], 0.0f);
-        save(hl + 1, H);
+        for (int r = 0; r < 16; ++r) H[r] = fmaxf(Hn[r], 0.0f);
+        save(hl + 1);
     }
+    publish(X[w], l, H);
+    __syncthreads();
+    if (w != 0) return;  // branch head and warp: wave 0 (no barrier follows)
     const bool has_nr = a.w_nr != nullptr;
     const float *br = j < 3 ? a.w_rot + j * W
                     : j < 6 ? a.w_trn + (j - 3) * W
@@ -126,12 +131,7 @@ __global__ __launch_bounds__(256) void ndp_train_fwd(TrainArgs a) {
         const int q = frow(r, h);
         Bo[r] = q < 3 ? a.b_rot[q] : q < 6 ? a.b_trn[q - 3] : (q == 6 && has_nr) ? a.b_nr[0] : 0.0f;
     }
-#pragma unroll
-    for (int it = 0; it < NT; ++it)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            Bo = __builtin_amdgcn_mfma_f32_32x32x2f32(br ? br[32 * it + frow(r, h)] : 0.0f, H[it][r],
-                                                      Bo, 0, 0, 0);
+    Bo = chain<kNT>(X, l, [&](int it, int r) { return br ? br[32 * it + frow(r, h)] : 0.0f; }, Bo);
     const float o0 = Bo[0], o1 = Bo[1], o2 = Bo[2], o3 = Bo[3];
     const float p0 = __shfl_xor(o0, 32, 64), p1 = __shfl_xor(o1, 32, 64);
     const float p2 = __shfl_xor(o2, 32, 64), p3 = __shfl_xor(o3, 32, 64);
@@ -167,23 +167,35 @@ __global__ __launch_bounds__(256) void ndp_train_fwd(TrainArgs a) {
         const float v[8] = {r0, r1, r2, y0, y1, y2, s, 0.0f};
 #pragma unroll
         for (int k = 0; k < 8; ++k) a.aux[(size_t)k * N + pt] = v[k];
+        if (a.xs) {
+            const int k = a.inv[pt];
+            if (k >= 0) { a.xs[3 * k] = n0; a.xs[3 * k + 1] = n1; a.xs[3 * k + 2] = n2; }
+        }
     }
 }
 
 // ---- backward of one level: dL/dx' -> branch gradients -> layer deltas -----
-template <int NT>
-__global__ __launch_bounds__(256) void ndp_train_bwd(TrainArgs a) {
-    constexpr int W = 32 * NT;
-    const int l = threadIdx.x & 63, h = l >> 5, j = l & 31;
-    const int pt = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + j;
+__global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
+    constexpr int W = 32 * kNT;
+    __shared__ TileX X[kNT];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5, j = l & 31;
+    const int pt = blockIdx.x * 32 + j;
     const bool valid = pt < a.N;
     const int N = a.N;
     const bool has_nr = a.w_nr != nullptr;
-    // per-point branch gradients (both halves of the wave compute them)
+    // per-point branch gradients (every lane of every wave computes them)
     float dO[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (valid) {
         const float x[3] = {a.x[3 * pt], a.x[3 * pt + 1], a.x[3 * pt + 2]};
-        float g[3] = {a.g[3 * pt], a.g[3 * pt + 1], a.g[3 * pt + 2]};
+        float g[3];
+        if (a.inv) {
+            const int k = a.inv[pt];
+            g[0] = k >= 0 ? a.gsub[3 * k] : 0.0f;
+            g[1] = k >= 0 ? a.gsub[3 * k + 1] : 0.0f;
+            g[2] = k >= 0 ? a.gsub[3 * k + 2] : 0.0f;
+        } else {
+            g[0] = a.g[3 * pt]; g[1] = a.g[3 * pt + 1]; g[2] = a.g[3 * pt + 2];
+        }
         float aux[7];
 #pragma unroll
         for (int k = 0; k < 7; ++k) aux[k] = a.aux[(size_t)k * N + pt];
@@ -232,13 +244,13 @@ __global__ __launch_bounds__(256) void ndp_train_bwd(TrainArgs a) {
         const float gww = (gw[0] * w[0] + gw[1] * w[1]) + gw[2] * w[2];
 #pragma unroll
         for (int c = 0; c < 3; ++c) dO[c] = 0.001f * ((gw[c] - gww * w[c]) / th + dth * w[c]);
-        if (h == 0)
+        if (h == 0 && threadIdx.x < 64)  // wave 0 (w is the rotation axis here)
             for (int k = 0; k < 8; ++k) a.dO[(size_t)k * N + pt] = dO[k];
     }
     // delta of the last hidden activation: W_b^T dO (K = 8 branch rows, 4 k-steps)
     const int L = a.nhid;
-    auto load_act = [&](int layer, int ot, int r) -> float {
-        return valid ? a.H[((size_t)layer * W + 32 * ot + frow(r, h)) * N + pt] : 0.0f;
+    auto load_act = [&](int layer, int r) -> float {
+        return valid ? a.H[((size_t)layer * W + 32 * w + frow(r, h)) * N + pt] : 0.0f;
     };
     auto branch_w = [&](int q, int col) -> float {  // W_b[q][col], q = branch row 0..7
         if (q < 3) return a.w_rot[q * W + col];
@@ -246,46 +258,34 @@ __global__ __launch_bounds__(256) void ndp_train_bwd(TrainArgs a) {
         if (q == 6 && has_nr) return a.w_nr[col];
         return 0.0f;
     };
-    f32x16 Dt[NT];
+    f32x16 Dt;
 #pragma unroll
-    for (int ot = 0; ot < NT; ++ot) {
+    for (int r = 0; r < 16; ++r) Dt[r] = 0.0f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) Dt[ot][r] = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s)  // k = 2s + h: B[k][j] = dO[k] of point j
-            Dt[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(branch_w(2 * s + h, 32 * ot + j),
-                                                          h ? dO[2 * s + 1] : dO[2 * s], Dt[ot], 0, 0, 0);
-    }
-    // rows of the transposed product: A[i][k] = W[k][i] -> lane j gives W[k][32 ot + j]
+    for (int s = 0; s < 4; ++s)  // k = 2s + h: B[k][j] = dO[k] of point j
+        Dt = __builtin_amdgcn_mfma_f32_32x32x2f32(branch_w(2 * s + h, 32 * w + j),
+                                                  h ? dO[2 * s + 1] : dO[2 * s], Dt, 0, 0, 0);
+    // rows of the transposed product: A[i][k] = W[k][i] -> lane j gives W[k][32 w + j]
     for (int layer = L; layer >= 0; --layer) {
         // mask by the layer's ReLU: delta of the pre-activation
 #pragma unroll
-        for (int ot = 0; ot < NT; ++ot)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) Dt[ot][r] = sgn_mask(load_act(layer, ot, r), Dt[ot][r]);
+        for (int r = 0; r < 16; ++r) Dt[r] = sgn_mask(load_act(layer, r), Dt[r]);
         if (valid) {
-            float *base = a.D + (size_t)layer * W * N + pt;
+            float *base = a.D + ((size_t)layer * W + 32 * w) * N + pt;
 #pragma unroll
-            for (int ot = 0; ot < NT; ++ot)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) base[(size_t)(32 * ot + frow(r, h)) * N] = Dt[ot][r];
+            for (int r = 0; r < 16; ++r) base[(size_t)frow(r, h) * N] = Dt[r];
         }
         if (layer == 0) break;
+        publish(X[w], l, Dt);
+        __syncthreads();
         const float *Wm = a.w_hid[layer - 1];  // layer l = relu(W_{l-1} H_{l-1} + b)
-        f32x16 Dn[NT];
+        f32x16 Dn;
 #pragma unroll
-        for (int ot = 0; ot < NT; ++ot) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) Dn[ot][r] = 0.0f;
-#pragma unroll
-            for (int it = 0; it < NT; ++it)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    Dn[ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                        Wm[(size_t)(32 * it + frow(r, h)) * W + 32 * ot + j], Dt[it][r], Dn[ot], 0, 0, 0);
-        }
-#pragma unroll
-        for (int ot = 0; ot < NT; ++ot) Dt[ot] = Dn[ot];
+        for (int r = 0; r < 16; ++r) Dn[r] = 0.0f;
+        Dn = chain<kNT>(X, l, [&](int it, int r) {
+            return Wm[(size_t)(32 * it + frow(r, h)) * W + 32 * w + j]; }, Dn);
+        __syncthreads();
+        Dt = Dn;
     }
 }
 
@@ -303,56 +303,50 @@ struct WgradArgs {
 
 constexpr int kWgT = 64;  // points per LDS stage
 
-__global__ __launch_bounds__(256) void ndp_wgrad(WgradArgs a) {
+// 16 waves: wave t owns output tile t of the job (a 128 x 128 weight is 4 x 4
+// tiles); the chains and the bias sums keep their point order
+__global__ __launch_bounds__(1024) void ndp_wgrad(WgradArgs a) {
     __shared__ float Ds[128][kWgT + 1], Xs[128][kWgT + 1];
     const WgradJob jb = a.job[blockIdx.y];
     const int c = blockIdx.x, nchunk = gridDim.x;
     const int p0 = c * a.chunk, p1 = min(a.N, p0 + a.chunk);
     const int tid = threadIdx.x, wid = tid >> 6, l = tid & 63, h = l >> 5, jj = l & 31;
-    const int nto = (jb.FO + 31) >> 5, nti = (jb.FI + 31) >> 5, ntile = nto * nti;
-    f32x16 acc[4];
+    const int nti = (jb.FI + 31) >> 5, ntile = ((jb.FO + 31) >> 5) * nti;
+    const bool own = wid < ntile;
+    const int to = own ? wid / nti : 0, ti = own ? wid - to * nti : 0;
+    f32x16 acc;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
     float bsum = 0.0f;  // bias partial of output row tid (tid < FO)
     for (int pb = p0; pb < p1; pb += kWgT) {
         const int np = min(kWgT, p1 - pb);
         __syncthreads();
-        for (int e = tid; e < 128 * kWgT; e += 256) {
+        for (int e = tid; e < 128 * kWgT; e += 1024) {
             const int row = e / kWgT, col = e - row * kWgT;
             const bool in = col < np;
             Ds[row][col] = (row < jb.FO && in) ? jb.D[(size_t)row * a.N + pb + col] : 0.0f;
             Xs[row][col] = (row < jb.FI && in) ? jb.X[(size_t)row * a.N + pb + col] : 0.0f;
         }
         __syncthreads();
-        if (tid < jb.FO)
+        if (tid < jb.FO) {
+#pragma unroll 8
             for (int k = 0; k < np; ++k) bsum += Ds[tid][k];
-        // wave wid takes tiles wid, wid + 4, ... (<= 4 per wave at 128 x 128)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int t = wid + 4 * q;
-            if (t >= ntile) break;
-            const int to = t / nti, ti = t - to * nti;
+        }
+        if (own)
             for (int s = 0; s < kWgT / 2; ++s) {
                 const int k = 2 * s + h;
-                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[32 * to + jj][k], Xs[32 * ti + jj][k],
-                                                              acc[q], 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[32 * to + jj][k], Xs[32 * ti + jj][k], acc,
+                                                           0, 0, 0);
             }
-        }
     }
     // D[o][i]: lane (jj, h) holds rows frow(r, h) of column jj
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int t = wid + 4 * q;
-        if (t >= ntile) break;
-        const int to = t / nti, ti = t - to * nti;
+    if (own) {
         const int col = 32 * ti + jj;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = 32 * to + frow(r, h);
             if (row < jb.FO && col < jb.FI)
-                jb.part[((size_t)c * jb.FO + row) * jb.FI + col] = acc[q][r];
+                jb.part[((size_t)c * jb.FO + row) * jb.FI + col] = acc[r];
         }
     }
     if (tid < jb.FO)
@@ -375,14 +369,68 @@ __global__ __launch_bounds__(256) void ndp_wgrad_reduce(ReduceArgs a) {
     const int nw = jb.FO * jb.FI;
     if (e < nw) {
         float s = 0.0f;
+#pragma unroll 8
         for (int c = 0; c < a.nchunk; ++c) s += jb.part[(size_t)c * nw + e];
         jb.gw[e] = s;
     } else if (e < nw + jb.FO) {
         const int o = e - nw;
         float s = 0.0f;
+#pragma unroll 8
         for (int c = 0; c < a.nchunk; ++c) s += jb.part[(size_t)a.nchunk * nw + (size_t)c * jb.FO + o];
         jb.gb[o] = s;
     }
+}
+
+// ---- the level loss around the Chamfer pass (registration.py:231-244): the
+// truncated Chamfer means with their gradients dL/dd1 = 1/K, dL/dd2 = 1/M
+// (0 where truncated), + w_reg * mean(-max(log(1 - s), -100)), and the loss
+// log entry; one workgroup, fixed reduction order ------------------------------
+struct GlueArgs {
+    const float *d1, *d2, *s;  // (K), (M), nonrigidity (N) or null (no BCE term)
+    int K, M, N, log_last;
+    float trunc, w_reg, g1, g2;
+    float *gd1, *gd2, *loss, *log;
+    long long *ctr;
+};
+
+__global__ __launch_bounds__(1024) void ndp_chamfer_glue(GlueArgs a) {
+    __shared__ float red[3][16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    for (int i = t; i < a.K; i += 1024) {
+        const float d = a.d1[i];
+        const bool in = !(d >= a.trunc);  // torch.where(d >= trunc, 0, d): NaN stays
+        s1 += in ? d : 0.0f;
+        a.gd1[i] = in ? a.g1 : 0.0f;
+    }
+    for (int i = t; i < a.M; i += 1024) {
+        const float d = a.d2[i];
+        const bool in = !(d >= a.trunc);
+        s2 += in ? d : 0.0f;
+        a.gd2[i] = in ? a.g2 : 0.0f;
+    }
+    if (a.s)
+        for (int i = t; i < a.N; i += 1024) {
+            const float v = logf(1.0f - a.s[i]);
+            s3 += v < -100.0f ? -100.0f : v;  // clamp(min=-100), NaN stays
+        }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+        s3 += __shfl_xor(s3, o, 64);
+    }
+    if (lane == 0) { red[0][wv] = s1; red[1][wv] = s2; red[2][wv] = s3; }
+    __syncthreads();
+    if (t != 0) return;
+    float S1 = 0.0f, S2 = 0.0f, S3 = 0.0f;
+    for (int w = 0; w < 16; ++w) { S1 += red[0][w]; S2 += red[1][w]; S3 += red[2][w]; }
+    float L = S1 / (float)a.K + S2 / (float)a.M;
+    if (a.s) L = L + a.w_reg * (-S3 / (float)a.N);
+    *a.loss = L;
+    const long long c = *a.ctr;
+    a.log[c < a.log_last ? c : a.log_last] = L;
+    *a.ctr = c + 1;
 }
 
 }  // namespace
@@ -410,6 +458,7 @@ static int fill_train(const pcr_ndp_train *t, pcr::TrainArgs &a) {
     a.w_nr = L.w_nr; a.b_nr = L.b_nr;
     a.pe = t->pe; a.H = t->H; a.aux = t->aux; a.x_out = t->x_out;
     a.g = t->g; a.bce_scale = t->bce_scale; a.dO = t->dO; a.D = t->D;
+    a.inv = t->inv; a.xs = t->xs; a.gsub = t->gsub;
     return PCR_OK;
 }
 
@@ -420,7 +469,8 @@ extern "C" int pcr_ndp_train_forward(const pcr_ndp_train *t, pcr_stream_t stream
     if (rc != PCR_OK) return rc;
     if (a.N == 0) return PCR_OK;
     PCR_REQUIRE(a.x && a.pe && a.H && a.aux && a.x_out, PCR_ERR_ARG, "ndp_train_forward: null buffer");
-    hipLaunchKernelGGL(pcr::ndp_train_fwd<4>, dim3((a.N + 127) / 128), dim3(256), 0,
+    PCR_REQUIRE(!a.xs || a.inv, PCR_ERR_ARG, "ndp_train_forward: xs without inv");
+    hipLaunchKernelGGL(pcr::ndp_train_fwd, dim3((a.N + 31) / 32), dim3(64 * pcr::kNT), 0,
                        pcr::as_stream(stream), a);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
@@ -433,10 +483,11 @@ extern "C" int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32
     int rc = fill_train(t, a);
     if (rc != PCR_OK) return rc;
     if (a.N == 0) return PCR_OK;
-    PCR_REQUIRE(a.g && a.dO && a.D && part && grads, PCR_ERR_ARG, "ndp_train_backward: null buffer");
+    PCR_REQUIRE((a.inv ? a.gsub != nullptr : a.g != nullptr) && a.dO && a.D && part && grads, PCR_ERR_ARG,
+                "ndp_train_backward: null buffer");
     PCR_REQUIRE(chunk >= 64 && chunk % 64 == 0, PCR_ERR_ARG, "ndp_train_backward: chunk %d", chunk);
     hipStream_t s = pcr::as_stream(stream);
-    hipLaunchKernelGGL(pcr::ndp_train_bwd<4>, dim3((a.N + 127) / 128), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pcr::ndp_train_bwd, dim3((a.N + 31) / 32), dim3(64 * pcr::kNT), 0, s, a);
     PCR_LAUNCH_CHECK();
     // jobs: input layer (W x 6 over pe), hidden layers, branches (7 x W over H_last)
     const int W = a.W, N = a.N, nchunk = (N + chunk - 1) / chunk;
@@ -458,7 +509,7 @@ extern "C" int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32
         add(a.D + (size_t)(k + 1) * W * N, a.H + (size_t)k * W * N, W, W, grads[2 + 2 * k],
             grads[3 + 2 * k]);
     add(a.dO, a.H + (size_t)a.nhid * W * N, 7, W, grads[2 + 2 * a.nhid], grads[3 + 2 * a.nhid]);
-    hipLaunchKernelGGL(pcr::ndp_wgrad, dim3(nchunk, nj), dim3(256), 0, s, wa);
+    hipLaunchKernelGGL(pcr::ndp_wgrad, dim3(nchunk, nj), dim3(1024), 0, s, wa);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(pcr::ndp_wgrad_reduce, dim3((W * W + W + 255) / 256, nj), dim3(256), 0, s, ra);
     PCR_LAUNCH_CHECK();
@@ -469,4 +520,20 @@ extern "C" int64_t pcr_ndp_train_partial_floats(int32_t N, int32_t width, int32_
     if (N <= 0 || chunk <= 0) return 0;
     const int64_t nchunk = (N + chunk - 1) / chunk, W = width;
     return nchunk * ((W * 6 + W) + (int64_t)(depth - 1) * (W * W + W) + (7 * W + 7));
+}
+
+extern "C" int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
+                                    const float *s, int32_t N, double w_reg, double trunc,
+                                    float *gd1, float *gd2, float *loss, float *log, int64_t *ctr,
+                                    int32_t log_last, pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(K >= 0 && M >= 0 && N >= 0 && log_last >= 0, PCR_ERR_ARG, "ndp_chamfer_glue: negative size");
+    PCR_REQUIRE((K == 0 || (d1 && gd1)) && (M == 0 || (d2 && gd2)) && loss && log && ctr, PCR_ERR_ARG,
+                "ndp_chamfer_glue: null buffer");
+    pcr::GlueArgs g{d1, d2, s, K, M, N, log_last, (float)trunc, (float)w_reg,
+                    (float)(1.0 / (double)K), (float)(1.0 / (double)M), gd1, gd2, loss, log,
+                    (long long *)ctr};
+    hipLaunchKernelGGL(pcr::ndp_chamfer_glue, dim3(1), dim3(1024), 0, pcr::as_stream(stream), g);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
 }

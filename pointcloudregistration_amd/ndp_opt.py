@@ -259,7 +259,8 @@ class _TrainC(ctypes.Structure):
                 ("w_hid", ctypes.c_void_p * 4), ("b_hid", ctypes.c_void_p * 4),
                 ("pe", ctypes.c_void_p), ("H", ctypes.c_void_p), ("aux", ctypes.c_void_p),
                 ("x_out", ctypes.c_void_p), ("g", ctypes.c_void_p), ("bce_scale", ctypes.c_double),
-                ("dO", ctypes.c_void_p), ("D", ctypes.c_void_p)]
+                ("dO", ctypes.c_void_p), ("D", ctypes.c_void_p),
+                ("inv", ctypes.c_void_p), ("xs", ctypes.c_void_p), ("gsub", ctypes.c_void_p)]
 
 
 class _LevelFused(_Level):
@@ -285,7 +286,7 @@ class _LevelFused(_Level):
         self.dO = torch.zeros(8, N, **f32)
         self.D = torch.zeros(d, W, N, **f32)
         self.gx = torch.zeros(N, 3, **f32)
-        self.xo = torch.zeros(N, 3, **f32)
+        self.xo = self.warped  # the forward writes the level output in place
         nparts = _lib.load().pcr_ndp_train_partial_floats(N, W, d, self.CHUNK)
         self.part = torch.zeros(max(int(nparts), 1), **f32)
         # gradient buffers in the kernel's order; the Adam table must see the same
@@ -325,16 +326,26 @@ class _LevelFused(_Level):
         self.bce_on = level > 0 and cfg.w_reg > 0 and self.has_nr
         t.bce_scale = (cfg.w_reg / N) if self.bce_on else 0.0
         t.dO, t.D = self.dO.data_ptr(), self.D.data_ptr()
-        self.desc = t
         K, M = inds.shape[0], t_sample.shape[0]
         self.K, self.M = K, M
         self.d1 = torch.zeros(1, K, **f32)
         self.d2 = torch.zeros(1, M, **f32)
+        self.gd1 = torch.zeros(1, K, **f32)
+        self.gd2 = torch.zeros(1, M, **f32)
         self.i1 = torch.zeros(1, K, dtype=torch.int32, device=dev)
         self.i2 = torch.zeros(1, M, dtype=torch.int32, device=dev)
         self.gsub = torch.zeros(1, K, 3, **f32)
         self.gt = torch.zeros(1, M, 3, **f32)
         self.t3 = t_sample[None].contiguous()
+        # duplicate-free subset: the forward writes x'[inds] and the backward reads
+        # dL/dx' of the subset through inv (no gather / index_add launches)
+        self.use_inv = int(torch.unique(inds).numel()) == K
+        if self.use_inv:
+            self.inv = torch.full((N,), -1, dtype=torch.int32, device=dev)
+            self.inv[inds] = torch.arange(K, dtype=torch.int32, device=dev)
+            self.xs = torch.zeros(1, K, 3, **f32)
+            t.inv, t.xs, t.gsub = self.inv.data_ptr(), self.xs.data_ptr(), self.gsub.data_ptr()
+        self.desc = t
 
     def _rebuild_table(self):
         tab = (_AdamTensor * len(self.params))()
@@ -349,28 +360,19 @@ class _LevelFused(_Level):
         st = _lib.stream_handle(self.s.device)
         desc = ctypes.byref(self.desc)
         _lib.call("pcr_ndp_train_forward", desc, st)
-        xs = self.xo.index_select(0, self.inds)[None].contiguous()
+        xs = self.xs if self.use_inv else self.xo.index_select(0, self.inds)[None].contiguous()
         nnd_forward_cuda(xs, self.t3, self.d1, self.d2, self.i1, self.i2)
-        trunc = 1e9
-        c1 = torch.where(self.d1 >= trunc, torch.zeros_like(self.d1), self.d1)
-        c2 = torch.where(self.d2 >= trunc, torch.zeros_like(self.d2), self.d2)
-        loss = c1.sum() / self.K + c2.sum() / self.M
-        gd1 = torch.where(self.d1 >= trunc, torch.zeros_like(self.d1),
-                          torch.full_like(self.d1, 1.0 / self.K))
-        gd2 = torch.where(self.d2 >= trunc, torch.zeros_like(self.d2),
-                          torch.full_like(self.d2, 1.0 / self.M))
-        nnd_backward_cuda(xs, self.t3, self.gsub, self.gt, gd1, gd2, self.i1, self.i2)
-        self.gx.zero_()
-        self.gx.index_add_(0, self.inds, self.gsub[0])
-        if self.bce_on:
-            sv = self.aux[6]
-            loss = loss + cfg.w_reg * torch.mean(-torch.clamp(torch.log(1 - sv), min=-100.0))
+        # loss (truncated Chamfer means + BCE), dL/dd1, dL/dd2, the log entry, the counter
+        _lib.call("pcr_ndp_chamfer_glue", _lib.ptr(self.d1), self.K, _lib.ptr(self.d2), self.M,
+                  _lib.ptr(self.aux[6] if self.bce_on else None), self.N, float(cfg.w_reg), 1e9,
+                  _lib.ptr(self.gd1), _lib.ptr(self.gd2), _lib.ptr(self.loss), _lib.ptr(self.log),
+                  _lib.ptr(self.ctr), int(cfg.iters), st)
+        nnd_backward_cuda(xs, self.t3, self.gsub, self.gt, self.gd1, self.gd2, self.i1, self.i2)
+        if not self.use_inv:
+            self.gx.zero_()
+            self.gx.index_add_(0, self.inds, self.gsub[0])
         _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
                   ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
-        self.loss.copy_(loss)
-        self.log.index_copy_(0, torch.clamp(self.ctr, max=self.cfg.iters), self.loss.reshape(1))
-        self.ctr += 1
-        self.warped.copy_(self.xo)
         _lib.call("pcr_ndp_control", _lib.ptr(self.loss), _lib.ptr(self.state),
                   float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4, st)
         _lib.call("pcr_adam_masked", _lib.ptr(self.table), len(self.params), self.max_numel,

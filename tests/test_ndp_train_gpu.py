@@ -45,6 +45,7 @@ def test_fused_forward_and_gradients_match_autograd(level):
     if nr is not None:
         assert torch.allclose(lv.aux[6], nr.detach(), atol=2e-6, rtol=0)
     g = torch.from_numpy(rng.standard_normal((N, 3)).astype(np.float32)).cuda()
+    lv.desc.inv = lv.desc.xs = lv.desc.gsub = None  # dL/dx' from gx (subset path: below)
     lv.gx.copy_(g)
     _lib.call("pcr_ndp_train_backward", ctypes.byref(lv.desc), _lib.ptr(lv.part), lv.CHUNK,
               ctypes.cast(lv.grad_ptrs, ctypes.c_void_p), st)
@@ -56,6 +57,60 @@ def test_fused_forward_and_gradients_match_autograd(level):
     for (name, _), got, w in zip(L.named_parameters(), lv.grads, want):
         tol = 2e-4 * float(w.abs().max()) + 1e-12
         assert torch.allclose(got, w, atol=tol, rtol=0), (name, float((got - w).abs().max()), tol)
+
+
+def test_subset_path_matches_explicit_gather_scatter():
+    """inv/xs/gsub (the forward writes x'[inds], the backward reads dL/dx' of the
+    subset) == index_select + index_add_ into a full gradient, bit for bit."""
+    rng = np.random.default_rng(7)
+    N, K = 3000, 1000
+    x = torch.from_numpy(rng.uniform(-0.8, 0.8, (N, 3)).astype(np.float32)).cuda()
+    t = torch.from_numpy(rng.uniform(-0.8, 0.8, (500, 3)).astype(np.float32)).cuda()
+    inds = torch.from_numpy(np.sort(rng.choice(N, K, replace=False))).cuda()
+    L = _layer(2, 17)
+    lv = ndp_opt._LevelFused(L, x, t, inds, 2, ndp_opt.NDPConfig(w_reg=0.05))
+    assert lv.use_inv
+    st = _lib.stream_handle()
+    _lib.call("pcr_ndp_train_forward", ctypes.byref(lv.desc), st)
+    assert torch.equal(lv.xs[0], lv.xo[inds])
+    gs = torch.from_numpy(rng.standard_normal((K, 3)).astype(np.float32)).cuda()
+    lv.gsub[0].copy_(gs)
+    args = (_lib.ptr(lv.part), lv.CHUNK, ctypes.cast(lv.grad_ptrs, ctypes.c_void_p), st)
+    _lib.call("pcr_ndp_train_backward", ctypes.byref(lv.desc), *args)
+    got = [g.clone() for g in lv.grads]
+    lv.desc.inv = lv.desc.xs = lv.desc.gsub = None
+    lv.gx.zero_()
+    lv.gx.index_add_(0, inds, gs)
+    _lib.call("pcr_ndp_train_backward", ctypes.byref(lv.desc), *args)
+    torch.cuda.synchronize()
+    for a, b in zip(got, lv.grads):
+        assert torch.equal(a, b)
+
+
+def test_chamfer_glue_matches_torch_loss():
+    """pcr_ndp_chamfer_glue == the loss of registration.py:231-244 as torch
+    computes it (sum order differs: 1e-6 relative), gradients and log exact."""
+    rng = np.random.default_rng(5)
+    K, M, N = 1100, 1300, 2000
+    d1 = torch.from_numpy(rng.random((1, K)).astype(np.float32) * 0.1).cuda()
+    d2 = torch.from_numpy(rng.random((1, M)).astype(np.float32) * 0.1).cuda()
+    d1[0, 7] = 2e9  # truncated
+    s = torch.from_numpy(rng.random(N).astype(np.float32) * 0.9).cuda()
+    s[3] = 1.0  # log(0) -> clamped to -100
+    gd1, gd2 = torch.empty_like(d1), torch.empty_like(d2)
+    loss = torch.zeros((), device="cuda")
+    log = torch.zeros(4, device="cuda")
+    ctr = torch.tensor([5], dtype=torch.long, device="cuda")
+    _lib.call("pcr_ndp_chamfer_glue", _lib.ptr(d1), K, _lib.ptr(d2), M, _lib.ptr(s), N, 0.05, 1e9,
+              _lib.ptr(gd1), _lib.ptr(gd2), _lib.ptr(loss), _lib.ptr(log), _lib.ptr(ctr), 3,
+              _lib.stream_handle())
+    c1 = torch.where(d1 >= 1e9, torch.zeros_like(d1), d1)
+    want = c1.sum() / K + d2.sum() / M + 0.05 * torch.mean(-torch.clamp(torch.log(1 - s), min=-100.0))
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(want)) <= 1e-6 * abs(float(want))
+    assert torch.equal(gd1, torch.where(d1 >= 1e9, torch.zeros_like(d1), torch.full_like(d1, 1.0 / K)))
+    assert torch.equal(gd2, torch.full_like(d2, 1.0 / M))
+    assert float(log[3]) == float(loss) and int(ctr) == 6
 
 
 def test_fused_optimisation_close_to_autograd_path():
