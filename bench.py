@@ -375,7 +375,7 @@ def measure_ndp_opt(with_cpu):
     return res
 
 
-TRAFFIC_FILE = "profiles/r01/v10_pmc_traffic.json"
+TRAFFIC_FILE = "profiles/r01/v11_pmc_traffic.json"
 
 
 def _pmc_traffic(kernel):
@@ -390,6 +390,27 @@ def _pmc_traffic(kernel):
         if kernel in k:
             return v.get("fetch_size_bytes", 0.0) + v.get("write_size_bytes", 0.0)
     return None
+
+
+def _chamfer_roofline(prof, P, N):
+    """Second roofline line: the a1 Chamfer kernel of the step (nng_query, one
+    launch = both directions of all P pairs).  Algorithmic bytes per launch: each
+    query point read once (12 B) and its (dist, idx) written (8 B), plus one read
+    of each cloud's grid (float4 points + slot starts).  It is bound by latency
+    (dependent cell walks, L2-resident grids), not HBM: frac shows how far."""
+    ms, n = prof
+    if not n:
+        return None
+    per = ms / n
+    S = 256
+    while S < N:
+        S <<= 1
+    nbytes = 2 * P * N * (12 + 8) + 2 * P * (N * 16 + (S + 1) * 4)
+    gbs = nbytes / (per * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "nng_query<1> (certified grid 1-NN)", "achieved": gbs,
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+            "traffic": _pmc_traffic("nng_query"), "bytes_per_launch": nbytes,
+            "kernel_ms_per_launch": per, "launches": n}
 
 
 def main():
@@ -415,7 +436,7 @@ def main():
         step()
     torch.cuda.synchronize()
     _lib.profile_enable(True)
-    for pid in range(7):
+    for pid in range(8):
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
     barrier(world)
@@ -431,7 +452,7 @@ def main():
             (("feature_screen", _lib.PROF_FEAT_SCREEN), ("nnd_fwd", _lib.PROF_NND_FWD),
              ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
              ("icp", _lib.PROF_ICP), ("feat_rescan", _lib.PROF_FEAT_RESCAN),
-             ("feat_pack", _lib.PROF_FEAT_PACK))}
+             ("feat_pack", _lib.PROF_FEAT_PACK), ("nnd_grid_query", _lib.PROF_NND_GRID))}
     _lib.profile_enable(False)
     rescan_rows = _lib.featnn_rescan_rows(reset=True)
 
@@ -488,6 +509,7 @@ def main():
                      "executed_mfma_tflops": executed,
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS},
+        "roofline_chamfer": _chamfer_roofline(prof["nnd_grid_query"], P, N),
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
         "featnn_rescan_rows_per_step": [r / args.steps for r in rescan_rows],
         "stages_ms": stages,

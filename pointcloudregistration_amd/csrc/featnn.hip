@@ -1215,14 +1215,11 @@ __global__ __launch_bounds__(512) void featnn_dual5(DualArgs5 a) {
                     mm2 = vmed3(m1, o1, t2);
                     m1 = vmin(m1, o1);
                 }
-                const unsigned code = __float_as_uint(m1) & 255u;
-                const int r = code & 15;
-                const int mi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 +
-                               (r & 3) + 8 * (r >> 2);
+                // no row index stored: featnn_colmerge5 decodes it from m1's
+                // code bits (a third fewer column-partial bytes written and read)
                 const size_t o = cpoff + (size_t)ct * 32 + col;
                 a.cp1[o] = m1;
                 a.cp2[o] = mm2;
-                a.cpi[o] = mi;
             }
         }
     }
@@ -1383,14 +1380,11 @@ __global__ __launch_bounds__(512) void featnn_dual6(DualArgs5 a) {
                     mm2 = vmed3(m1, o1, t2);
                     m1 = vmin(m1, o1);
                 }
-                const unsigned code = __float_as_uint(m1) & 255u;
-                const int r = code & 15;
-                const int mi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 +
-                               (r & 3) + 8 * (r >> 2);
+                // no row index stored: featnn_colmerge5 decodes it from m1's
+                // code bits (a third fewer column-partial bytes written and read)
                 const size_t o = cpoff + (size_t)ct * 32 + col;
                 a.cp1[o] = m1;
                 a.cp2[o] = mm2;
-                a.cpi[o] = mi;
             }
         }
     };
@@ -1587,14 +1581,11 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
                     mm2 = vmed3(m1, o1, t2);
                     m1 = vmin(m1, o1);
                 }
-                const unsigned code = __float_as_uint(m1) & 255u;
-                const int r = code & 15;
-                const int mi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 +
-                               (r & 3) + 8 * (r >> 2);
+                // no row index stored: featnn_colmerge5 decodes it from m1's
+                // code bits (a third fewer column-partial bytes written and read)
                 const size_t o = cpoff + (size_t)ct * 32 + col;
                 a.cp1[o] = m1;
                 a.cp2[o] = mm2;
-                a.cpi[o] = mi;
             }
         }
     }
@@ -1643,7 +1634,13 @@ __global__ void featnn_colmerge5(DualArgs5 a, int32_t *nn21, int *list21, int *c
     int i1 = 0;
     for (int rb = 0; rb < nrb_used; ++rb) {
         const size_t o = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32 + j;
-        top2_merge(b1, i1, b2, a.cp1[o], a.cpi[o], a.cp2[o]);
+        // row index of the partial's winner from its code bits (wave, half,
+        // register), as the screen kernels packed them
+        const float v1 = a.cp1[o];
+        const unsigned code = __float_as_uint(v1) & 255u;
+        const int r = code & 15;
+        const int vi = rb * 256 + (int)(code >> 5) * 32 + (int)((code >> 4) & 1) * 4 + (r & 3) + 8 * (r >> 2);
+        top2_merge(b1, i1, b2, v1, vi, a.cp2[o]);
     }
     nn21[(size_t)p * a.Mmax + j] = i1;
     const double F = (double)__uint_as_float(a.fmax[p]);

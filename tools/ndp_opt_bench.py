@@ -27,6 +27,9 @@ for rep in range(2):
     P = ndp_opt.DeformationPyramid(3, 128, torch.device("cuda"), -8, cfg.m, True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ndp_opt.optimize_deformation_pyramid(S, G, inds, cfg, NDP=P, use_graph=os.environ.get("GRAPH", "1") == "1")
+    out = ndp_opt.optimize_deformation_pyramid(S, G, inds, cfg, NDP=P,
+                                               use_graph=os.environ.get("GRAPH", "1") == "1",
+                                               fused=os.environ.get("FUSED", "1") == "1")
     torch.cuda.synchronize()
-    print(rep, (time.perf_counter() - t0) * 1e3, "ms")
+    rp = [round(i.get("replay_ms", 0.0), 2) for i in out[3]]
+    print(rep, (time.perf_counter() - t0) * 1e3, "ms; replay ms per level", rp, "sum", round(sum(rp), 2))
