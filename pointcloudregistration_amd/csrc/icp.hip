@@ -143,7 +143,32 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
             // --- Umeyama over correspondences: means
             if (tid < 256) {
                 double v[6] = {0, 0, 0, 0, 0, 0};
-                for (int i = tid; i < n; i += 256) {
+                // four entries of this lane's sequence are loaded before they are
+                // added in sequence order: the same sums, overlapped gathers
+                int i = tid;
+                for (; i + 768 < n; i += 1024) {
+                    int jj[4];
+                    double a3[4][3], b3[4][3];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) jj[u] = cj[i + 256 * u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int ii = i + 256 * u, j = jj[u] < 0 ? 0 : jj[u];
+                        a3[u][0] = P3[3 * ii]; a3[u][1] = P3[3 * ii + 1]; a3[u][2] = P3[3 * ii + 2];
+                        b3[u][0] = (double)G[3 * j]; b3[u][1] = (double)G[3 * j + 1]; b3[u][2] = (double)G[3 * j + 2];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (jj[u] >= 0) {
+                            v[0] = v[0] + a3[u][0];
+                            v[1] = v[1] + a3[u][1];
+                            v[2] = v[2] + a3[u][2];
+                            v[3] = v[3] + b3[u][0];
+                            v[4] = v[4] + b3[u][1];
+                            v[5] = v[5] + b3[u][2];
+                        }
+                }
+                for (; i < n; i += 256) {
                     const int j = cj[i];
                     if (j < 0) continue;
                     v[0] = v[0] + P3[3 * i];
@@ -164,15 +189,33 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
             // --- cross covariance
             if (tid < 256) {
                 double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-                for (int i = tid; i < n; i += 256) {
-                    const int j = cj[i];
-                    if (j < 0) continue;
-                    const double s0 = P3[3 * i] - ms0, s1 = P3[3 * i + 1] - ms1, s2 = P3[3 * i + 2] - ms2;
-                    const double t0 = (double)G[3 * j] - mt0, t1 = (double)G[3 * j + 1] - mt1,
-                                 t2 = (double)G[3 * j + 2] - mt2;
+                auto add = [&](double s0, double s1, double s2, double t0, double t1, double t2) {
                     v[0] = v[0] + s0 * t0; v[1] = v[1] + s0 * t1; v[2] = v[2] + s0 * t2;
                     v[3] = v[3] + s1 * t0; v[4] = v[4] + s1 * t1; v[5] = v[5] + s1 * t2;
                     v[6] = v[6] + s2 * t0; v[7] = v[7] + s2 * t1; v[8] = v[8] + s2 * t2;
+                };
+                int i = tid;
+                for (; i + 768 < n; i += 1024) {  // as above: loads first, sums in order
+                    int jj[4];
+                    double a3[4][3], b3[4][3];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) jj[u] = cj[i + 256 * u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int ii = i + 256 * u, j = jj[u] < 0 ? 0 : jj[u];
+                        a3[u][0] = P3[3 * ii] - ms0; a3[u][1] = P3[3 * ii + 1] - ms1; a3[u][2] = P3[3 * ii + 2] - ms2;
+                        b3[u][0] = (double)G[3 * j] - mt0; b3[u][1] = (double)G[3 * j + 1] - mt1;
+                        b3[u][2] = (double)G[3 * j + 2] - mt2;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (jj[u] >= 0) add(a3[u][0], a3[u][1], a3[u][2], b3[u][0], b3[u][1], b3[u][2]);
+                }
+                for (; i < n; i += 256) {
+                    const int j = cj[i];
+                    if (j < 0) continue;
+                    add(P3[3 * i] - ms0, P3[3 * i + 1] - ms1, P3[3 * i + 2] - ms2, (double)G[3 * j] - mt0,
+                        (double)G[3 * j + 1] - mt1, (double)G[3 * j + 2] - mt2);
                 }
                 for (int k = 0; k < 9; ++k) red[tid][k] = v[k];
             }
