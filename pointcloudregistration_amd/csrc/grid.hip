@@ -87,11 +87,16 @@ __global__ __launch_bounds__(1024) void grid_build_lds(BuildArgs a) {
     }
 }
 
-// Spatial order of a cloud: points sorted by the Morton code of their grid
-// cell (10 bits per axis relative to the cloud's minimum cell), one
-// 1024-thread workgroup per cloud, bitonic sort of (key << 16 | index) in
-// LDS.  Sweeps that walk a cloud in this order give each wave neighbouring
-// queries: the same hash cells, similar candidate counts, coherent LDS reads.
+// Spatial order of a cloud: points bucketed by the Morton code of their grid
+// cell, 5 bits per axis relative to the cloud's minimum cell (cells merged in
+// powers of two until the cloud's extent fits 32), by a counting sort in LDS --
+// one 1024-thread workgroup per cloud: count, scan, scatter (the bitonic sort
+// of full 30-bit codes it replaces took 128 us per C4 call).  Sweeps that walk
+// a cloud in this order give each wave neighbouring queries: the same hash
+// cells, similar candidate counts, coherent LDS reads.  Order within a bucket is
+// atomic order; it changes timing only (every sweep's result is independent of
+// the order: fixed-point or integer sums, per-point outputs, and an early stop
+// that only fires on hypotheses that cannot win).
 __device__ __forceinline__ unsigned spread10(unsigned v) {
     v &= 1023u;
     v = (v | (v << 16)) & 0x030000FFu;
@@ -101,60 +106,54 @@ __device__ __forceinline__ unsigned spread10(unsigned v) {
     return v;
 }
 
-__global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, const int32_t *n,
-                                                             int Nmax, double inv_cell, int np2max,
-                                                             int32_t *order) {
-    extern __shared__ unsigned long long keys[];
-    __shared__ int smin[3][16];
+constexpr int kOrdBits = 5, kOrdBuckets = 1 << (3 * kOrdBits);
+
+__global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, const int32_t *n, int Nmax,
+                                                             double inv_cell, int32_t *order) {
+    extern __shared__ int bk[];  // kOrdBuckets + 1: counts -> starts -> cursors
+    __shared__ int smin[3][16], smax[3][16];
     const int p = blockIdx.x, t = threadIdx.x;
-    const int cnt = count_of(n, p, Nmax);
+    const int m = count_of(n, p, Nmax);
     const float *P = pts + (size_t)p * Nmax * 3;
     int32_t *o = order + (size_t)p * Nmax;
-    int np2 = 1;
-    while (np2 < cnt) np2 <<= 1;
-    if (np2 > np2max) {  // too large for the LDS sort: identity order
-        for (int i = t; i < Nmax; i += 1024) o[i] = i;
-        return;
-    }
-    int mn[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
-    for (int i = t; i < cnt; i += 1024)
-        for (int c = 0; c < 3; ++c) mn[c] = min(mn[c], (int)__builtin_floor((double)P[3 * i + c] * inv_cell));
-    for (int c = 0; c < 3; ++c) {
-        for (int off = 32; off; off >>= 1) mn[c] = min(mn[c], __shfl_xor(mn[c], off, 64));
-        if ((t & 63) == 0) smin[c][t >> 6] = mn[c];
-    }
-    __syncthreads();
-    int base[3];
-    for (int c = 0; c < 3; ++c) {
-        int v = smin[c][0];
-        for (int w = 1; w < 16; ++w) v = min(v, smin[c][w]);
-        base[c] = v;
-    }
-    for (int i = t; i < np2; i += 1024) {
-        unsigned long long k = ~0ull;
-        if (i < cnt) {
-            unsigned m = 0;
-            for (int c = 0; c < 3; ++c) {
-                const int q = (int)__builtin_floor((double)P[3 * i + c] * inv_cell) - base[c];
-                m |= spread10((unsigned)min(max(q, 0), 1023)) << c;
-            }
-            k = ((unsigned long long)m << 16) | (unsigned)i;
+    int mn[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff}, mx[3] = {-0x7fffffff, -0x7fffffff, -0x7fffffff};
+    for (int i = t; i < m; i += 1024)
+        for (int c = 0; c < 3; ++c) {
+            const int q = (int)__builtin_floor((double)P[3 * i + c] * inv_cell);
+            mn[c] = min(mn[c], q);
+            mx[c] = max(mx[c], q);
         }
-        keys[i] = k;
-    }
-    __syncthreads();
-    for (int size = 2; size <= np2; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = t; i < np2; i += 1024) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const unsigned long long a = keys[i], b = keys[j];
-                    if ((a > b) == ((i & size) == 0)) { keys[i] = b; keys[j] = a; }
-                }
-            }
-            __syncthreads();
+    for (int c = 0; c < 3; ++c) {
+        for (int off = 32; off; off >>= 1) {
+            mn[c] = min(mn[c], __shfl_xor(mn[c], off, 64));
+            mx[c] = max(mx[c], __shfl_xor(mx[c], off, 64));
         }
-    for (int i = t; i < Nmax; i += 1024) o[i] = i < cnt ? (int32_t)(keys[i] & 0xFFFFu) : i;
+        if ((t & 63) == 0) { smin[c][t >> 6] = mn[c]; smax[c][t >> 6] = mx[c]; }
+    }
+    for (int i = t; i < kOrdBuckets; i += 1024) bk[i] = 0;
+    __syncthreads();
+    int base[3], ext = 0;
+    for (int c = 0; c < 3; ++c) {
+        int lo = smin[c][0], hi = smax[c][0];
+        for (int w = 1; w < 16; ++w) { lo = min(lo, smin[c][w]); hi = max(hi, smax[c][w]); }
+        base[c] = lo;
+        ext = max(ext, (int)min((long long)hi - lo, (long long)0x3fffffff));
+    }
+    int shift = 0;
+    while ((ext >> shift) >= (1 << kOrdBits)) ++shift;
+    auto key = [&](int i) -> unsigned {
+        unsigned k = 0;
+        for (int c = 0; c < 3; ++c) {
+            const int q = ((int)__builtin_floor((double)P[3 * i + c] * inv_cell) - base[c]) >> shift;
+            k |= spread10((unsigned)min(max(q, 0), (1 << kOrdBits) - 1)) << c;
+        }
+        return k;
+    };
+    for (int i = t; i < m; i += 1024) atomicAdd(&bk[key(i)], 1);
+    __syncthreads();
+    block_exclusive_scan_1024(bk, bk, kOrdBuckets, false);
+    for (int i = t; i < m; i += 1024) o[atomicAdd(&bk[key(i)], 1)] = i;
+    for (int i = m + t; i < Nmax; i += 1024) o[i] = i;
 }
 
 }  // namespace
@@ -163,12 +162,10 @@ int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double ce
                   int ws_slot, const int32_t **order) {
     int32_t *o = (int32_t *)workspace(ws_slot, sizeof(int32_t) * (size_t)P * Nmax + 64);
     PCR_REQUIRE(o, PCR_ERR_NOMEM, "spatial_order: %s", pcr_last_error());
-    const int np2max = Nmax <= 65536 ? 16384 : 0;  // 128 KiB of keys; indices fit 16 bits
-    const size_t sm = sizeof(unsigned long long) * (size_t)(np2max > 0 ? np2max : 1);
+    const size_t sm = sizeof(int) * (size_t)(kOrdBuckets + 1);
     PCR_HIP_CHECK(hipFuncSetAttribute((const void *)spatial_order_kernel,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    hipLaunchKernelGGL(spatial_order_kernel, dim3(P), dim3(1024), sm, s, pts, n, Nmax, 1.0 / cell,
-                       np2max, o);
+    hipLaunchKernelGGL(spatial_order_kernel, dim3(P), dim3(1024), sm, s, pts, n, Nmax, 1.0 / cell, o);
     PCR_LAUNCH_CHECK();
     *order = o;
     return PCR_OK;
