@@ -375,7 +375,7 @@ def measure_ndp_opt(with_cpu):
     return res
 
 
-TRAFFIC_FILE = "profiles/r01/v11_pmc_traffic.json"
+TRAFFIC_FILE = "profiles/r01/v12_pmc_traffic.json"
 
 
 def _pmc_traffic(kernel):
