@@ -2,14 +2,19 @@
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--points NPTS]
 
-Workload = BASELINE.json configs[3]: P synthetic TOF/PC-style
-cloud pairs of NPTS points with D=32 descriptors per GPU rank (weak scaling: rank
-r owns pairs r*P .. r*P+P-1, generated locally), inputs resident in HBM.
-One step = the whole pair pipeline over the batch (pointcloudregistration_amd/
+Workload = BASELINE.json configs[3]: a job of P (default 256)
+synthetic TOF/PC-style cloud pairs of NPTS points with D=32 descriptors, split
+over the ranks as SURVEY §8e prescribes (rank r owns a contiguous shard of
+~P/N pairs, generated locally; strong scaling), inputs resident in HBM.
+One step = the whole pair pipeline over the shard (pointcloudregistration_amd/
 pipeline.py): exact mutual feature NN -> RANSAC (RANSAC.py parameters) -> ICP
 -> nnd Chamfer quality, then the RCCL all-gather of the per-pair records.
-Multi-GPU: one process per GPU (torchrun), barrier + synchronize around the timed
-loop, max over ranks; value = all pairs processed / that time.
+Multi-GPU: one process per GPU -- under torchrun, or started by this script
+itself when --gpus N > 1 is given without a launcher -- barrier + synchronize
+around the timed loop, max over ranks; value = all pairs of the job / that time.
+Beside it: the PCIe-inclusive rate (host-resident inputs, `host_resident`), weak
+scaling at N > 1 (P pairs on every rank), the pair-parallel CPU baseline and the
+C2 / a4 / a10 / f1 / f4 side measurements at N = 1.
 """
 from __future__ import annotations
 
@@ -37,15 +42,31 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=256)
+    ap.add_argument("--pairs", type=int, default=256,
+                    help="pairs in the WHOLE job (SURVEY 8e: 256 split over the ranks)")
     ap.add_argument("--points", type=int, default=8192)
     ap.add_argument("--dim", type=int, default=32)
     ap.add_argument("--feat-noise", type=float, default=1.0)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-resident", action="store_true",
+                    help="skip the PCIe-inclusive (host-resident inputs) measurement")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the a4 (LRF) / a10 (NDP warp) side measurements")
+                    help="skip the C2 / a4 / a10 / f1 / f4 side measurements")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` without a launcher: start N rank processes BEFORE
+    this process touches the GPU, relay rank 0's JSON line, exit non-zero if any
+    rank fails (multigpu.launch_local_ranks).  Under torchrun the env already names
+    the rank and this is not used."""
+    from pointcloudregistration_amd.multigpu import launch_local_ranks
+    rc, out0 = launch_local_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                  args.gpus)
+    sys.stdout.write(out0)
+    sys.stdout.flush()
+    return rc
 
 
 def dist_setup():
@@ -74,35 +95,67 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def cpu_baseline(batch, params, budget_s):
+CPU_WORKER_CAP = 16  # the GPU box's host share per GPU (os.cpu_count() shows the whole machine)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(batch, params, budget_s, pair_ids):
     """The oracle's C restatement of the same per-pair pipeline (oracle/pcr_oracle.c:
-    featnn both ways -> mutual corres -> sequential RANSAC -> ICP -> nnd Chamfer) on
-    the first pairs of this rank's workload, for ~budget_s seconds.  featnn uses
-    OpenMP (OMP_NUM_THREADS threads); the rest is single-threaded like the reference."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    rp, ip = params.ransac, params.icp
-    done, t0, Ts = 0, time.perf_counter(), []
-    while (time.perf_counter() - t0 < budget_s or done == 0) and done < batch.src.shape[0]:
-        p = done
-        nn12 = oracle.featnn(batch.src_feat[p], batch.tgt_feat[p])
-        nn21 = oracle.featnn(batch.tgt_feat[p], batch.src_feat[p])
-        co = oracle.corres(nn12, nn21, rp.mutual_filter, rp.ransac_n)
-        r = oracle.ransac(batch.src[p], batch.tgt[p], co, rp.max_correspondence_distance,
-                          rp.ransac_n, rp.edge_length_ratio, None, rp.max_iteration,
-                          rp.confidence, rp.seed, p)
-        ic = oracle.icp(batch.src[p], batch.tgt[p], ip.max_correspondence_distance, init=r["T"])
-        T = ic["T"]
-        aligned = (batch.src[p].astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
-        oracle.nnd_forward(aligned[None], batch.tgt[p][None])
-        Ts.append((r["T"], T))
-        done += 1
-    el = time.perf_counter() - t0
-    return ({"value": done / el, "unit": "pairs/s", "cores": threads, "kind": "port",
+    featnn both ways -> mutual corres -> sequential RANSAC -> ICP -> nnd Chamfer),
+    pair-parallel: one single-threaded worker process per host core
+    (oracle/cpu_pipeline.py), each taking pairs w, w+W, ... of the workload for
+    ~budget_s seconds.  Runs before this process touches the GPU (the workers are
+    plain child processes).  value = sum over workers of pairs / own elapsed."""
+    import shutil
+    import subprocess
+    import tempfile
+    aff = len(os.sched_getaffinity(0))
+    W = max(1, min(aff, CPU_WORKER_CAP))
+    k = min(batch.src.shape[0], 8 * W)
+    tmp = tempfile.mkdtemp(prefix="pcr_cpu_")
+    try:
+        inp = os.path.join(tmp, "in")
+        os.mkdir(inp)
+        arrays = dict(src=batch.src[:k], tgt=batch.tgt[:k], src_feat=batch.src_feat[:k],
+                      tgt_feat=batch.tgt_feat[:k], pair_ids=np.asarray(pair_ids[:k], np.int32),
+                      ransac_d=np.float64(params.ransac.max_correspondence_distance),
+                      icp_d=np.float64(params.icp.max_correspondence_distance),
+                      seed=np.int64(params.ransac.seed))
+        for name, arr in arrays.items():
+            np.save(os.path.join(inp, name + ".npy"), arr)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        worker = os.path.join(ROOT, "oracle", "cpu_pipeline.py")
+        procs = [subprocess.Popen([sys.executable, worker, inp, os.path.join(tmp, f"o{w}.npz"),
+                                   str(w), str(W), str(budget_s)], env=env) for w in range(W)]
+        rcs = [p.wait() for p in procs]
+        if any(rcs):
+            raise RuntimeError(f"cpu baseline workers failed: {rcs}")
+        rate, done, Ts = 0.0, 0, {}
+        for w in range(W):
+            z = np.load(os.path.join(tmp, f"o{w}.npz"))
+            n = len(z["pairs"])
+            rate += n / float(z["elapsed"])
+            done += n
+            for i, p in enumerate(z["pairs"]):
+                Ts[int(p)] = (z["T_ransac"][i], z["T_icp"][i])
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return ({"value": rate, "unit": "pairs/s", "cores": W, "affinity_cpus": aff,
+             "cpu_model": _cpu_model(), "kind": "port",
              "sample": f"{done} of the workload's pairs ({batch.src.shape[1]} pts, D="
-                       f"{batch.src_feat.shape[2]}) through the oracle pipeline in {el:.1f}s; "
-                       f"feature-NN on {threads} OpenMP threads, RANSAC/ICP/Chamfer 1 thread"},
+                       f"{batch.src_feat.shape[2]}) through the oracle pipeline (featnn x2, "
+                       f"mutual corres, RANSAC, ICP, Chamfer), {W} single-threaded worker "
+                       f"processes for ~{budget_s:.0f} s each; value = sum of per-worker rates"},
             Ts)
 
 
@@ -375,21 +428,117 @@ def measure_ndp_opt(with_cpu):
     return res
 
 
-TRAFFIC_FILE = "profiles/r01/v12_pmc_traffic.json"
+def measure_c2(with_cpu):
+    """C2 (BASELINE configs[1]): dip/torch-nndistance Chamfer forward on 2 x 4096
+    random points (test.py:8-9 shape, U[0,1)^3, default_rng(0)), the drop-in's
+    default path (certified grid) and the brute-force kernel, beside the
+    reference's own CPU extension (dip/torch-nndistance/src/my_lib.cpp:28-60,
+    compiled unmodified into oracle/_ref by oracle/build_ref.sh) on one core."""
+    from pointcloudregistration_amd import nndistance as nd
+    rng = np.random.default_rng(0)
+    N = 4096
+    x1 = rng.random((1, N, 3), dtype=np.float32)
+    x2 = rng.random((1, N, 3), dtype=np.float32)
+    t1, t2 = torch.from_numpy(x1).cuda(), torch.from_numpy(x2).cuda()
+    d1, d2 = torch.empty(1, N, device="cuda"), torch.empty(1, N, device="cuda")
+    i1 = torch.empty(1, N, dtype=torch.int32, device="cuda")
+    i2 = torch.empty(1, N, dtype=torch.int32, device="cuda")
+    res = {"workload": "C2: nnd forward, B=1, 4096 x 4096 (both directions), U[0,1)^3"}
+    outs = {}
+    old = os.environ.get("PCR_NND_ALGO")
+    try:
+        for algo in ("grid", "brute"):
+            os.environ["PCR_NND_ALGO"] = algo
+            ms = _events_ms(lambda: nd.nnd_forward_cuda(t1, t2, d1, d2, i1, i2), 50)
+            outs[algo] = [x.cpu().numpy() for x in (d1, d2, i1, i2)]
+            res[f"gpu_ms_{algo}"] = ms
+    finally:
+        if old is None:
+            os.environ.pop("PCR_NND_ALGO", None)
+        else:
+            os.environ["PCR_NND_ALGO"] = old
+    evals = 2.0 * N * N
+    res["pair_evals_per_s_brute"] = evals / (res["gpu_ms_brute"] * 1e-3)
+    # brute force: 8 flops per pair evaluation (3 sub, 3 mul, 2 add; no FMA: bit-exact form)
+    tf = evals * 8 / (res["gpu_ms_brute"] * 1e-3) / 1e12
+    res["roofline_brute"] = {"bound": "valu-f32", "achieved": tf, "peak": PEAK_F32_MFMA_TFLOPS,
+                             "unit": "TFLOP/s", "frac": tf / PEAK_F32_MFMA_TFLOPS,
+                             "note": "one launch of 1 pair: 32 KB of inputs, far from filling "
+                                     "256 CUs; 8 flops/pair-eval, no FMA contraction"}
+    res["grid_equals_brute"] = all(np.array_equal(a, b) for a, b in zip(outs["grid"], outs["brute"]))
+    if with_cpu:
+        ref = None
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle", "_ref"))
+            import torch_nndistance_ref as ref  # the reference's my_lib.cpp, compiled here
+        except ImportError:
+            ref = None
+        c1, c2 = torch.from_numpy(x1), torch.from_numpy(x2)
+        e1, e2 = torch.zeros(1, N), torch.zeros(1, N)
+        j1, j2 = torch.zeros(1, N, dtype=torch.int32), torch.zeros(1, N, dtype=torch.int32)
+        reps = 3
+        if ref is not None:
+            ref.nnd_forward(c1, c2, e1, e2, j1, j2)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ref.nnd_forward(c1, c2, e1, e2, j1, j2)
+            cpu_ms = (time.perf_counter() - t0) * 1e3 / reps
+            kind, got = "reference", [e1.numpy(), e2.numpy(), j1.numpy(), j2.numpy()]
+        else:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                got = list(O.nnd_forward(x1, x2))
+            cpu_ms = (time.perf_counter() - t0) * 1e3 / reps
+            kind = "port"
+        res["cpu_baseline"] = {"ms": cpu_ms, "cores": 1, "kind": kind,
+                               "sample": "the same 4096 x 4096 forward, "
+                                         + ("oracle/_ref torch_nndistance_ref.nnd_forward "
+                                            "(reference my_lib.cpp)" if kind == "reference"
+                                            else "oracle nnd_forward (C restatement)")}
+        res["gpu_vs_cpu_bitexact"] = all(np.array_equal(a, b) for a, b in zip(outs["grid"], got))
+        res["speedup_vs_cpu"] = cpu_ms / res["gpu_ms_grid"]
+    return res
+
+
+TRAFFIC_DIR = "profiles"
+
+
+def _traffic_file():
+    """Newest committed PMC traffic summary (profiles/rNN/vMM_pmc_traffic.json)."""
+    import glob
+    import re
+    best, key = None, None
+    for f in glob.glob(os.path.join(ROOT, TRAFFIC_DIR, "r*", "*pmc_traffic.json")):
+        m = re.search(r"r(\d+)[/\\]v(\d+)_pmc_traffic\.json$", f)
+        if m:
+            k = (int(m.group(1)), int(m.group(2)))
+            if key is None or k > key:
+                best, key = f, k
+    return best
 
 
 def _pmc_traffic(kernel):
-    """HBM bytes per launch (fetch + write) of `kernel` from the committed PMC summary
-    (tools/pmc_traffic.sh on this bench), or None when absent."""
+    """HBM bytes per launch (fetch + write) of `kernel` from the newest committed PMC
+    summary (tools/pmc_traffic.sh on this bench), or None when absent."""
+    f = _traffic_file()
+    if f is None:
+        return None
     try:
-        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
-            ks = json.load(f)["kernels"]
+        with open(f) as fh:
+            ks = json.load(fh)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
     for k, v in ks.items():
         if kernel in k:
             return v.get("fetch_size_bytes", 0.0) + v.get("write_size_bytes", 0.0)
     return None
+
+
+def _traffic_source():
+    f = _traffic_file()
+    return os.path.relpath(f, ROOT) if f else None
 
 
 def _chamfer_roofline(prof, P, N):
@@ -413,24 +562,171 @@ def _chamfer_roofline(prof, P, N):
             "kernel_ms_per_launch": per, "launches": n}
 
 
+def grid_candidates(src, tgt, T, d):
+    """Mean candidates c_bar examined per radius-d grid query of src (through T)
+    against tgt: a host replay of grid.h's walk (cells 2.01 d, the <=2x2x2 cells
+    of the 1.001 d box that the cell-gap test keeps; hash collisions ignored)."""
+    cell = 2.01 * d
+    thr = float(np.float32(d * d))
+    kt = np.floor(tgt.astype(np.float64) / cell).astype(np.int64)
+    key = lambda c: (c[..., 0] * 1_000_003 + c[..., 1]) * 1_000_033 + c[..., 2]  # noqa: E731
+    uk, cnt = np.unique(key(kt), return_counts=True)
+    p = src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]
+    lo = np.floor((p - 1.001 * d) / cell).astype(np.int64)
+    hi = np.floor((p + 1.001 * d) / cell).astype(np.int64)
+    total = np.zeros(p.shape[0])
+    for dx in (0, 1):
+        for dy in (0, 1):
+            for dz in (0, 1):
+                c = lo + np.array([dx, dy, dz])
+                ok = np.all(c <= hi, axis=1)
+                gap = np.maximum(np.maximum(c * cell - p, p - (c + 1) * cell), 0.0)
+                ok &= (gap * gap).sum(1) <= thr
+                k = key(c)
+                pos = np.clip(np.searchsorted(uk, k), 0, len(uk) - 1)
+                hit = ok & (uk[pos] == k)
+                total += np.where(hit, cnt[pos], 0)
+    return float(total.mean())
+
+
+def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
+    """HBM roofline line of a grid-sweep kernel (RANSAC verification a7 / ICP a8)
+    with SURVEY 8d's algorithmic bytes per sweep of N source points:
+    N*12 (points) + N*c_bar*12 (candidate targets) + N/8 (inlier mask bits)."""
+    ms, n = prof
+    if not n:
+        return None
+    per = ms / n
+    per_sweep = N * 12 + N * cbar * 12 + N / 8
+    nbytes = sweeps * per_sweep
+    gbs = nbytes / (per * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": kernel, "achieved": gbs, "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": _pmc_traffic(kernel),
+            "bytes_per_launch": nbytes, "sweeps_per_launch": sweeps, "c_bar": cbar,
+            "kernel_ms_per_launch": per, "launches": n,
+            "note": f"{name}: candidate gathers are served from the pair's LDS copy of its "
+                    "target grid, so HBM sees far less than these algorithmic bytes"}
+
+
+def run_timed(step, steps, warmup, world):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize;
+    returns the max over ranks of the wall time (s) and the last step's result."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    return max_over_ranks(time.perf_counter() - t0, world), out
+
+
+def measure_host_resident(batch, params, pair_ids, steps, warmup, world, total_pairs):
+    """SURVEY 8d's end-to-end C4 definition: inputs resident on the HOST (pinned),
+    each step = H2D of the rank's xyz + descriptors, the pipeline, the records
+    all-gather and their D2H.  Double-buffered: the copy of batch k+1 runs on its
+    own HIP stream while batch k computes, so the rate is that of a stream of
+    batches (min of PCIe and compute throughput)."""
+    from pointcloudregistration_amd.multigpu import gather_records
+    from pointcloudregistration_amd.pipeline import PairPipeline
+    host = [torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
+            for x in (batch.src, batch.tgt, batch.src_feat, batch.tgt_feat)]
+    bufs = [[torch.empty(h.shape, dtype=h.dtype, device="cuda") for h in host] for _ in range(2)]
+    pipes = [PairPipeline(*bufs[k], params, pair_ids=pair_ids) for k in range(2)]
+    P = batch.src.shape[0]
+    rows = -(-total_pairs // world)
+    rec_host = torch.empty((rows * world, 40), dtype=torch.float64).pin_memory()
+    copy_s = torch.cuda.Stream()
+    comp = torch.cuda.current_stream()
+    copied = [torch.cuda.Event() for _ in range(2)]
+    freed = [torch.cuda.Event() for _ in range(2)]
+    h2d_bytes = sum(h.numel() * h.element_size() for h in host)
+
+    def issue_copy(k):
+        b = k % 2
+        with torch.cuda.stream(copy_s):
+            if k >= 2:
+                copy_s.wait_event(freed[b])
+            for d, h in zip(bufs[b], host):
+                d.copy_(h, non_blocking=True)
+            copied[b].record(copy_s)
+
+    def run(n):
+        issue_copy(0)
+        for k in range(n):
+            if k + 1 < n:
+                issue_copy(k + 1)
+            b = k % 2
+            comp.wait_event(copied[b])
+            pipes[b].run()
+            rec = gather_records(pipes[b].records(), world, rows)
+            freed[b].record(comp)
+            rec_host.copy_(rec, non_blocking=True)
+
+    run(max(warmup, 1))
+    torch.cuda.synchronize()
+    # the copy alone, for the PCIe rate
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(copy_s):
+        e0.record(copy_s)
+        for d, h in zip(bufs[0], host):
+            d.copy_(h, non_blocking=True)
+        e1.record(copy_s)
+    torch.cuda.synchronize()
+    h2d_ms = e0.elapsed_time(e1)
+    wall, _ = run_timed(lambda: run(steps), 1, 0, world)
+    return {"value": total_pairs * steps / wall, "unit": "pairs/s",
+            "ms_per_step": wall / steps * 1e3, "h2d_bytes_per_step_per_rank": h2d_bytes,
+            "h2d_ms_per_step": h2d_ms, "h2d_gbs": h2d_bytes / (h2d_ms * 1e-3) / 1e9,
+            "note": "pinned host inputs -> HBM on a copy stream overlapped with the previous "
+                    "batch's pipeline; records all-gathered and copied back to the host"}
+
+
 def main():
     args = parse()
-    rank, world, local = dist_setup()
-    from pointcloudregistration_amd import _lib, synth
-    from pointcloudregistration_amd.multigpu import gather_records, weak_shard
-    from pointcloudregistration_amd.pipeline import PairPipeline, default_params
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+              f"torchrun --nproc-per-node {args.gpus} or without a launcher", file=sys.stderr)
+        sys.exit(2)
+    from pointcloudregistration_amd import synth
+    from pointcloudregistration_amd.multigpu import gather_records, shard
+    from pointcloudregistration_amd.pipeline import default_params
 
-    first, P = weak_shard(args.pairs, rank)
+    # SURVEY 8e: the job's `pairs` pairs split over the ranks (strong scaling);
+    # every rank generates its own shard on the host
+    first, P = shard(args.pairs, world, rank)
+    if P == 0:
+        print(f"bench: rank {rank} has no pairs ({args.pairs} over {world})", file=sys.stderr)
+        sys.exit(2)
     N, D = args.points, args.dim
     batch = synth.make_batch(P, n=N, m=N, d=D, base_seed=1000, first_pair=first,
                              feat_noise=args.feat_noise)
     params = default_params(seed=0)
+    pair_ids = np.arange(first, first + P, dtype=np.int32)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(batch, params, args.cpu_budget, pair_ids)  # before any GPU call
+
+    rank, world, local = dist_setup()
+    from pointcloudregistration_amd import _lib
+    from pointcloudregistration_amd.pipeline import PairPipeline
     pipe = PairPipeline(batch.src, batch.tgt, batch.src_feat, batch.tgt_feat, params,
-                        pair_ids=np.arange(first, first + P, dtype=np.int32))
+                        pair_ids=pair_ids)
+
+    rows = -(-args.pairs // world)   # equal-size record blocks for the all-gather
 
     def step():
         pipe.run()
-        return gather_records(pipe.records(), world)
+        return gather_records(pipe.records(), world, rows)
 
     for _ in range(args.warmup):
         step()
@@ -439,15 +735,7 @@ def main():
     for pid in range(8):
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rec = step()
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    wall = max_over_ranks(time.perf_counter() - t0, world)
+    wall, rec = run_timed(step, args.steps, 0, world)
     prof = {name: _lib.profile_read(pid) for name, pid in
             (("feature_screen", _lib.PROF_FEAT_SCREEN), ("nnd_fwd", _lib.PROF_NND_FWD),
              ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
@@ -474,11 +762,22 @@ def main():
     executed = achieved * kexec / D
 
     recs = rec.cpu().numpy()
-    mine = recs[rank * P:(rank + 1) * P]
+    mine = recs[rank * rows:rank * rows + P]
     T_icp = mine[:, 16:32].reshape(P, 4, 4)
     rre, rte = synth.rre_rte(T_icp[:, :3, :3], T_icp[:, :3, 3], batch.R, batch.t)
 
-    total_pairs = P * world * args.steps
+    # sweep rooflines (a7 RANSAC verification, a8 ICP): sweeps per launch from the
+    # kernels' own counters, c_bar from a host replay on 4 sampled pairs
+    rr, ir, _, _ = pipe.last
+    validated = int(rr.stats[:, 1].sum().item())
+    icp_sweeps = int((ir.stats[:, 0] + 1).sum().item())
+    samp = list(range(min(4, P)))
+    cb_r = float(np.mean([grid_candidates(batch.src[p], batch.tgt[p], mine[p, 0:16].reshape(4, 4),
+                                          params.ransac.max_correspondence_distance) for p in samp]))
+    cb_i = float(np.mean([grid_candidates(batch.src[p], batch.tgt[p], T_icp[p],
+                                          params.icp.max_correspondence_distance) for p in samp]))
+
+    total_pairs = args.pairs * args.steps   # every pair of the job, once per step
     out = {
         "metric": "TOF/PC pairs/sec (8192 pts)",
         "value": total_pairs / wall,
@@ -488,21 +787,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32 xyz/features; f64 RANSAC/ICP; f16x3-split MFMA screen (certified bound) "
                  "+ f64 exact re-rank",
         "data": f"synthetic: procedural surface pairs, ROPNet-style augmentation, D={D} "
                 f"descriptors (noise {args.feat_noise}), generated per rank (seeds 1000+pair)",
         "config": {"workload": "C4: batch of augmented TOF/PC pairs (featNN+RANSAC+ICP+Chamfer)",
-                   "pairs_per_gpu": P, "points": N, "feature_dim": D,
+                   "pairs_total": args.pairs, "pairs_per_gpu": P, "points": N, "feature_dim": D,
                    "ransac": "d=0.04 mutual n=3 edge0.9 dist0.04 (100000,0.999)",
-                   "icp": "d=0.02 (1e-6,1e-6,30)", "parallelism": f"pair-sharded x{world}"},
+                   "icp": "d=0.02 (1e-6,1e-6,30)", "parallelism": f"pair-sharded x{world}",
+                   "inputs": "resident in HBM (see host_resident for the PCIe-inclusive rate)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_F16_MFMA_TFLOPS,
                      "traffic": _pmc_traffic("featnn_dual7"),
-                     "traffic_source": TRAFFIC_FILE + " (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
-                                       "passes of this bench; FETCH_SIZE x2 per the gfx950 note)",
+                     "traffic_source": f"{_traffic_source()} (rocprofv3 --pmc FETCH_SIZE, "
+                                       "WRITE_SIZE passes of this bench; FETCH_SIZE x2 per the "
+                                       "gfx950 note)",
                      "kernel": "featnn_dual7 (v_mfma_f32_32x32x16_f16, f16x3 split, top-2 epilogue)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,
@@ -510,33 +811,60 @@ def main():
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS},
         "roofline_chamfer": _chamfer_roofline(prof["nnd_grid_query"], P, N),
+        "roofline_ransac": _sweep_roofline("a7 RANSAC verification", "ransac_pair_kernel",
+                                           prof["ransac_validate"], validated, N, cb_r),
+        "roofline_icp": _sweep_roofline("a8 ICP", "icp_kernel", prof["icp"], icp_sweeps, N, cb_i),
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
         "featnn_rescan_rows_per_step": [r / args.steps for r in rescan_rows],
         "stages_ms": stages,
         "accuracy": {"rre_deg_median": float(np.median(rre)), "rre_deg_max": float(np.max(rre)),
                      "rte_median": float(np.median(rte)), "rte_max": float(np.max(rte)),
                      "ransac_iters_mean": float(mine[:, 37].mean()),
+                     "ransac_validations_mean": validated / P,
                      "mutual_corres_mean": float(mine[:, 39].mean())},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, Ts = cpu_baseline(batch, params, args.cpu_budget)
+    if not args.no_host_resident:
+        del pipe
+        torch.cuda.empty_cache()
+        out["host_resident"] = measure_host_resident(batch, params, pair_ids, args.steps,
+                                                     args.warmup, world, args.pairs)
+    if world > 1:
+        # secondary: weak scaling, `pairs` pairs on EVERY rank
+        wfirst = rank * args.pairs
+        wb = synth.make_batch(args.pairs, n=N, m=N, d=D, base_seed=1000, first_pair=wfirst,
+                              feat_noise=args.feat_noise)
+        wpipe = PairPipeline(wb.src, wb.tgt, wb.src_feat, wb.tgt_feat, params,
+                             pair_ids=np.arange(wfirst, wfirst + args.pairs, dtype=np.int32))
+
+        def wstep():
+            wpipe.run()
+            return gather_records(wpipe.records(), world, args.pairs)
+        wwall, _ = run_timed(wstep, args.steps, args.warmup, world)
+        out["weak_scaling"] = {"value": args.pairs * world * args.steps / wwall,
+                               "unit": "pairs/s", "pairs_per_gpu": args.pairs,
+                               "ms_per_step": wwall / args.steps * 1e3}
+    if cpu is not None:
+        cb, Ts = cpu
         out["cpu_baseline"] = cb
-        k = len(Ts)
-        T_r = mine[:k, 0:16].reshape(k, 4, 4)
-        same_r = all(np.array_equal(T_r[i], Ts[i][0]) for i in range(k))
-        same_i = all(np.array_equal(T_icp[i], Ts[i][1]) for i in range(k))
-        d_rre, d_rte = synth.rre_rte(T_icp[:k, :3, :3], T_icp[:k, :3, 3],
-                                     np.stack([t[1][:3, :3] for t in Ts]),
-                                     np.stack([t[1][:3, 3] for t in Ts]))
+        ks = sorted(Ts)
+        k = len(ks)
+        T_r = mine[ks, 0:16].reshape(k, 4, 4)
+        same_r = all(np.array_equal(T_r[i], Ts[p][0]) for i, p in enumerate(ks))
+        same_i = all(np.array_equal(T_icp[p], Ts[p][1]) for p in ks)
+        d_rre, d_rte = synth.rre_rte(T_icp[ks, :3, :3], T_icp[ks, :3, 3],
+                                     np.stack([Ts[p][1][:3, :3] for p in ks]),
+                                     np.stack([Ts[p][1][:3, 3] for p in ks]))
         out["accuracy"]["vs_cpu_ref"] = {"pairs": k, "T_ransac_bitexact": bool(same_r),
                                          "T_icp_bitexact": bool(same_i),
                                          "rre_deg_max": float(np.max(d_rre)),
                                          "rte_max": float(np.max(d_rte))}
     if rank == 0 and world == 1 and not args.no_secondary:
-        out["secondary"] = {"a4_lrf": measure_lrf(not args.no_cpu_baseline),
-                            "a10_ndp_warp": measure_ndp(not args.no_cpu_baseline),
-                            "f1_fpfh": measure_fpfh(not args.no_cpu_baseline),
-                            "f4_ndp_opt": measure_ndp_opt(not args.no_cpu_baseline)}
+        wc = not args.no_cpu_baseline
+        out["secondary"] = {"c2_nnd": measure_c2(wc),
+                            "a4_lrf": measure_lrf(wc),
+                            "a10_ndp_warp": measure_ndp(wc),
+                            "f1_fpfh": measure_fpfh(wc),
+                            "f4_ndp_opt": measure_ndp_opt(wc)}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -13,6 +13,16 @@
  * returns a thread-local message for the last failure.  (The reference CUDA
  * launcher prints and returns 0 / 1, nnd_cuda.cu:155-161; the Python layer
  * maps PCR_OK -> 1 and raises on failure.)
+ *
+ * Concurrency contract: scratch buffers come from a library-owned workspace
+ * with one set of slots PER DEVICE (not per stream).  Calls for one device must
+ * therefore be ordered: issue them on one stream at a time (or order the streams
+ * with events), from any host thread.  Two libpcr calls running concurrently on
+ * two streams of the same device would share scratch.  A slot that grows keeps
+ * its previous buffer alive (HIP graphs captured earlier may still point at it);
+ * pcr_workspace_release() frees every workspace buffer of the current device
+ * after a device synchronize -- call it only when no captured graph that
+ * contains libpcr kernels will be replayed again.
  */
 #ifndef PCR_API_H
 #define PCR_API_H
@@ -31,6 +41,7 @@ typedef void *pcr_stream_t; /* hipStream_t */
 
 const char *pcr_last_error(void);
 int pcr_version(void);
+int pcr_workspace_release(void);
 
 /* Optional per-kernel timing with HIP events recorded on the launch stream
  * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,

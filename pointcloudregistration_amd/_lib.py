@@ -102,6 +102,8 @@ def load():
         lib.pcr_last_error.restype = ctypes.c_char_p
         lib.pcr_last_error.argtypes = []
         lib.pcr_version.restype = ctypes.c_int
+        lib.pcr_workspace_release.restype = ctypes.c_int
+        lib.pcr_workspace_release.argtypes = []
         lib.pcr_profile_enable.restype = None
         lib.pcr_profile_enable.argtypes = [_i32]
         lib.pcr_profile_read.restype = ctypes.c_int
@@ -119,7 +121,7 @@ def load():
 
 
 def exported_symbols():
-    return ["pcr_last_error", "pcr_version", "pcr_profile_enable", "pcr_profile_read",
+    return ["pcr_last_error", "pcr_version", "pcr_workspace_release", "pcr_profile_enable", "pcr_profile_read",
             "pcr_featnn_rescan_rows", "pcr_ndp_train_partial_floats"] + list(SIGNATURES)
 
 

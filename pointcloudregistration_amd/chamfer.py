@@ -35,6 +35,16 @@ def compute_truncated_chamfer_distance(x, y, trunc=1e9, batch_reduction="mean",
     if batch_reduction not in (None, "mean", "sum"):
         raise ValueError('batch_reduction must be one of ["mean", "sum"] or None')
     N, P1, P2 = x.shape[0], x.shape[1], y.shape[1]
+    if weights is not None:  # loss.py:127-139
+        if weights.size(0) != N:
+            raise ValueError("weights must be of shape (N,).")
+        if not (weights >= 0).all():
+            raise ValueError("weights cannot be negative.")
+        if weights.sum() == 0.0:
+            w = weights.view(N, 1)
+            if batch_reduction in ("mean", "sum"):
+                return ((x.sum((1, 2)) * w).sum() * 0.0, (x.sum((1, 2)) * w).sum() * 0.0)
+            return ((x.sum((1, 2)) * w) * 0.0, (x.sum((1, 2)) * w) * 0.0)
     dist1, dist2 = nnd(x.float().contiguous(), y.float().contiguous())
     cham_x = torch.where(dist1 >= trunc, torch.zeros_like(dist1), dist1)
     cham_y = torch.where(dist2 >= trunc, torch.zeros_like(dist2), dist2)

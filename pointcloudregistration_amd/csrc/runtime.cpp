@@ -28,7 +28,9 @@ constexpr int kMaxDevices = 64;
 constexpr int kMaxSlots = 32;
 std::mutex g_mu;
 Slot g_slots[kMaxDevices][kMaxSlots];
-std::vector<void *> g_retired;  // superseded buffers, freed never (process lifetime)
+// superseded buffers: kept until pcr_workspace_release (a graph captured before a
+// slot grew still points at its old buffer)
+std::vector<std::pair<int, void *>> g_retired;
 }  // namespace
 
 void *workspace(int slot, size_t bytes) {
@@ -50,7 +52,7 @@ void *workspace(int slot, size_t bytes) {
         set_error("workspace: hipMalloc(%zu) failed", want);
         return nullptr;
     }
-    if (s.ptr) g_retired.push_back(s.ptr);
+    if (s.ptr) g_retired.emplace_back(dev, s.ptr);
     s.ptr = p;
     s.bytes = want;
     return p;
@@ -123,6 +125,32 @@ extern "C" int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, in
     if (total_ms) *total_ms = pcr::g_total_ms[id];
     if (count) *count = pcr::g_count[id];
     if (reset) { pcr::g_total_ms[id] = 0.0; pcr::g_count[id] = 0; }
+    return PCR_OK;
+}
+
+extern "C" int pcr_workspace_release(void) {
+    pcr::clear_error();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= pcr::kMaxDevices) {
+        pcr::set_error("workspace_release: no current device");
+        return PCR_ERR_HIP;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) {
+        pcr::set_error("workspace_release: device synchronize failed");
+        return PCR_ERR_HIP;
+    }
+    std::lock_guard<std::mutex> lk(pcr::g_mu);
+    for (auto &s : pcr::g_slots[dev]) {
+        if (s.ptr) (void)hipFree(s.ptr);
+        s.ptr = nullptr;
+        s.bytes = 0;
+    }
+    std::vector<std::pair<int, void *>> keep;
+    for (auto &r : pcr::g_retired) {
+        if (r.first == dev) (void)hipFree(r.second);
+        else keep.push_back(r);
+    }
+    pcr::g_retired.swap(keep);
     return PCR_OK;
 }
 

@@ -8,6 +8,11 @@ RCCL over xGMI with the "nccl" backend on ROCm, gloo on CPU for tests.
 """
 from __future__ import annotations
 
+import os
+import socket
+import subprocess
+import sys
+
 import torch
 import torch.distributed as dist
 
@@ -25,8 +30,17 @@ def weak_shard(pairs_per_rank: int, rank: int):
     return rank * pairs_per_rank, pairs_per_rank
 
 
-def gather_records(rec: torch.Tensor, world: int):
-    """All-gather equal-size (P, W) record blocks; returns (world*P, W) on every rank."""
+def gather_records(rec: torch.Tensor, world: int, rows: int | None = None):
+    """All-gather the ranks' (P_r, W) record blocks; returns (world*rows, W) on every
+    rank, rank r's records at rows [r*rows, r*rows + P_r) (zero padding after them).
+    `rows` >= every P_r (default: this rank's P, i.e. equal shards)."""
+    rows = rec.shape[0] if rows is None else int(rows)
+    if rows < rec.shape[0]:
+        raise ValueError(f"rows={rows} < this rank's {rec.shape[0]} records")
+    if rows > rec.shape[0]:
+        pad = torch.zeros((rows - rec.shape[0],) + tuple(rec.shape[1:]), dtype=rec.dtype,
+                          device=rec.device)
+        rec = torch.cat([rec, pad], 0)
     if world == 1:
         return rec
     rec = rec.contiguous()
@@ -38,3 +52,38 @@ def gather_records(rec: torch.Tensor, world: int):
     parts = [torch.empty_like(rec) for _ in range(world)]
     dist.all_gather(parts, rec)
     return torch.cat(parts, 0)
+
+
+def launch_local_ranks(cmd, world: int, timeout=None):
+    """Start `world` copies of `cmd` as rank processes of one node (RANK, LOCAL_RANK,
+    WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT): what
+    torchrun --nproc-per-node would do, for a parent that must not touch the GPU
+    itself.  Returns (exit code, rank 0's stdout): 0 only if every rank exited 0.
+    A failed rank 0 leaves the others blocked in a collective, so they are ended."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    try:
+        for r in range(world):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                       LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port))
+            procs.append(subprocess.Popen(cmd, env=env,
+                                          stdout=subprocess.PIPE if r == 0 else None))
+        out0 = procs[0].communicate(timeout=timeout)[0] or b""
+        rcs = [procs[0].returncode]
+        for p in procs[1:]:
+            if rcs[0] != 0 and p.poll() is None:
+                p.kill()
+            rcs.append(p.wait(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    rc = 0 if all(c == 0 for c in rcs) else 1
+    if rc:
+        print(f"launch_local_ranks: rank exit codes {rcs}", file=sys.stderr)
+    return rc, out0.decode("utf-8", "replace")

@@ -344,11 +344,15 @@ def _points(pc):
 
 
 def _feature_rows(f):
-    data = f.data if hasattr(f, "data") else f
-    if isinstance(data, torch.Tensor):
-        return data.t() if hasattr(f, "data") else data
-    data = np.asarray(data)
-    return data.T if hasattr(f, "data") else data   # Open3D Feature.data is (dim, num)
+    """(num, dim) rows of a feature argument: an Open3D-style Feature (``.data`` is
+    (dim, num)) is transposed; a raw (N, D) ndarray or tensor passes through (both
+    have a ``.data`` attribute of their own, so the test is on the type)."""
+    if isinstance(f, (np.ndarray, torch.Tensor)):
+        return f
+    if hasattr(f, "data"):
+        data = f.data
+        return data.t() if isinstance(data, torch.Tensor) else np.asarray(data).T
+    return np.asarray(f)
 
 
 def _ransac_params_from_o3d(max_corr, estimation_method, ransac_n, checkers, criteria, mutual,
