@@ -93,6 +93,8 @@ def _setup_sigs():
     L.oracle_corres.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
     L.oracle_philox.argtypes = [c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     L.oracle_horn_rotation.argtypes = [c.c_void_p, c.c_void_p]
+    L.oracle_xs_sum.restype = c.c_double
+    L.oracle_xs_sum.argtypes = [c.c_void_p, c.c_int]
     L.oracle_lrf_count.restype = c.c_int
     L.oracle_lrf_count.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_double]
     L.oracle_lrf.restype = c.c_int
@@ -123,6 +125,12 @@ def philox(seed, pair, itr, block=0):
     out = np.zeros(4, np.uint32)
     L().oracle_philox(seed, pair, itr, block, _p(out))
     return out
+
+
+def xs_sum(v):
+    """Exact fixed-point sum of f64 terms rounded once (the ICP Umeyama sums)."""
+    v = _f64(v).reshape(-1)
+    return float(L().oracle_xs_sum(_p(v), v.shape[0]))
 
 
 def horn_rotation(S):

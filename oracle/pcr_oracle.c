@@ -677,8 +677,9 @@ int oracle_ransac(const float *srcf, int n, const float *tgtf, int m, const int3
 /* a8: point-to-point ICP, restating Open3D 0.13 RegistrationICP as called   */
 /* from DataPreparation/RANSAC.py:61-63 (ICPConvergenceCriteria defaults:   */
 /* 1e-6, 1e-6, 30).  Correspondences: radius-limited 1-NN; update = Umeyama  */
-/* over all correspondences (deterministic 256-lane sums, lane = source     */
-/* index mod 256); T <- update*T; points transformed in place (f64).        */
+/* over all correspondences (1024 f64 lane partials, lane = source index    */
+/* mod 1024, added exactly: xs_*); T <- update*T; points transformed in     */
+/* place (f64).                                                             */
 /* ------------------------------------------------------------------------- */
 static void mat4_mul(const double A[16], const double B[16], double C[16])
 {
@@ -696,28 +697,114 @@ static int is_identity16(const double T[16])
     return 1;
 }
 
+/* Exact, order-independent sums (the ICP Umeyama step adds its 1024 lane    */
+/* partials with them).  Every term (an f64 value)                           */
+/* is taken to a signed 128-bit fixed-point integer with LSB 2^-80           */
+/* (truncated toward zero below it; |term| saturates at 2^47), the integers  */
+/* are added (associative: any split over lanes, waves or workgroups gives   */
+/* the same total), and the total is rounded once to the nearest f64 (ties   */
+/* to even).  The GPU kernel (csrc/xsum.h) does the same arithmetic, so ICP  */
+/* results do not depend on how a pair's lanes are spread over workgroups.  */
+typedef __int128 xs_t;
+#define XS_FRAC 80
+
+static xs_t xs_term(double x)
+{
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    const int e = (int)((b >> 52) & 0x7ff);
+    if (e == 0x7ff) return 0;                       /* non-finite: contributes 0 */
+    const uint64_t f = b & 0x000fffffffffffffull;
+    const uint64_t mant = e ? (f | 0x0010000000000000ull) : f;
+    int s = (e ? e : 1) - 1075 + XS_FRAC;           /* value = mant * 2^(s - 80) */
+    unsigned __int128 M = mant;
+    if (s >= 0) {
+        if (s > 74) { M = ((unsigned __int128)1 << 127) - 1; }   /* saturate */
+        else M <<= s;
+    } else {
+        M = (-s >= 64) ? 0 : (M >> (-s));
+    }
+    const xs_t v = (xs_t)M;
+    return (b >> 63) ? -v : v;
+}
+
+static double xs_to_double(xs_t v)
+{
+    const int neg = v < 0;
+    unsigned __int128 u = neg ? (unsigned __int128)(-(v + 1)) + 1u : (unsigned __int128)v;
+    if (u == 0) return 0.0;
+    const uint64_t hi = (uint64_t)(u >> 64), lo = (uint64_t)u;
+    const int msb = hi ? 127 - __builtin_clzll(hi) : 63 - __builtin_clzll(lo);
+    uint64_t m;
+    int sh = 0;
+    if (msb <= 52) {
+        m = (uint64_t)u;
+    } else {
+        sh = msb - 52;
+        m = (uint64_t)(u >> sh);
+        const unsigned __int128 rem = u & (((unsigned __int128)1 << sh) - 1u);
+        const unsigned __int128 half = (unsigned __int128)1 << (sh - 1);
+        if (rem > half || (rem == half && (m & 1u))) {
+            m += 1u;
+            if (m == (1ull << 53)) { m >>= 1; sh += 1; }
+        }
+    }
+    /* m * 2^(sh - 80): m < 2^53 is exact in f64, the power of two is exact */
+    const int k = sh - XS_FRAC;
+    uint64_t pb = (uint64_t)(k + 1023) << 52;
+    double p2;
+    memcpy(&p2, &pb, 8);
+    const double r = (double)m * p2;
+    return neg ? -r : r;
+}
+
+double oracle_xs_sum(const double *v, int n)
+{
+    xs_t a = 0;
+    for (int i = 0; i < n; i++) a += xs_term(v[i]);
+    return xs_to_double(a);
+}
+
+/* Umeyama over the correspondences of an ICP iteration.  Sums: 1024 lane      */
+/* partials (lane = source index mod 1024, f64 in increasing index), then the  */
+/* exact fixed-point sum of the lane partials (xs_* above), rounded once.      */
+#define ICP_LANES 1024
+static void lane_sums(const double *P, const double *Tg, const int32_t *cj, int n,
+                      const double *ms, const double *mt, int nq, double *out)
+{
+    /* nq = 6: source xyz, target xyz; nq = 9: centred products (a, b) */
+    xs_t tot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int l = 0; l < ICP_LANES; l++) {
+        double part[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = l; i < n; i += ICP_LANES) {
+            if (cj[i] < 0) continue;
+            const double *p = P + 3 * i, *t = Tg + 3 * cj[i];
+            if (nq == 6) {
+                for (int c = 0; c < 3; c++) { part[c] = part[c] + p[c]; part[3 + c] = part[3 + c] + t[c]; }
+            } else {
+                for (int a = 0; a < 3; a++)
+                    for (int b = 0; b < 3; b++)
+                        part[3 * a + b] = part[3 * a + b] + (p[a] - ms[a]) * (t[b] - mt[b]);
+            }
+        }
+        for (int q = 0; q < nq; q++) tot[q] += xs_term(part[q]);
+    }
+    for (int q = 0; q < nq; q++) out[q] = xs_to_double(tot[q]);
+}
+
 static void umeyama_masked(const double *P, const double *Tg, const int32_t *cj, int n, double T[12])
 {
-    unsigned char *mask = (unsigned char *)malloc((size_t)n);
-    double *v = (double *)malloc(sizeof(double) * (size_t)n);
     int K = 0;
-    for (int i = 0; i < n; i++) { mask[i] = cj[i] >= 0; K += mask[i]; }
+    for (int i = 0; i < n; i++) K += cj[i] >= 0;
     const double one_over_n = 1.0 / (double)K;
-    double ms[3], mt[3];
+    double sums[6], ms[3], mt[3];
+    lane_sums(P, Tg, cj, n, NULL, NULL, 6, sums);
     for (int c = 0; c < 3; c++) {
-        for (int i = 0; i < n; i++) v[i] = mask[i] ? P[3 * i + c] : 0.0;
-        ms[c] = det_sum(v, mask, n) * one_over_n;
-        for (int i = 0; i < n; i++) v[i] = mask[i] ? Tg[3 * cj[i] + c] : 0.0;
-        mt[c] = det_sum(v, mask, n) * one_over_n;
+        ms[c] = sums[c] * one_over_n;
+        mt[c] = sums[3 + c] * one_over_n;
     }
     double S[9];
-    for (int a = 0; a < 3; a++)
-        for (int b = 0; b < 3; b++) {
-            for (int i = 0; i < n; i++)
-                v[i] = mask[i] ? (P[3 * i + a] - ms[a]) * (Tg[3 * cj[i] + b] - mt[b]) : 0.0;
-            S[3 * a + b] = det_sum(v, mask, n);
-        }
-    free(mask); free(v);
+    lane_sums(P, Tg, cj, n, ms, mt, 9, S);
     double R[9];
     oracle_horn_rotation(S, R);
     for (int a = 0; a < 3; a++) {

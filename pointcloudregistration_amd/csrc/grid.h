@@ -50,9 +50,10 @@ __device__ __forceinline__ double cell_gap(double p, int c, double cell) {
 // d2 < thr <= r^2 (1 + 2^-23)); candidates are taken two at a time so their
 // LDS loads overlap.  The update order (slot order, strict < then lower index
 // on ties) makes the result independent of both.
-template <typename IdxT>
+// kSlot: also report the winner's slot (its coordinates are g.x/y/z[slot])
+template <typename IdxT, bool kSlot = false>
 __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double thr, double px,
-                                          double py, double pz, double &d2out) {
+                                          double py, double pz, double &d2out, int *slot = nullptr) {
     // The build assigns cells by floor(v / cell); here floor(v * inv_cell) over
     // [p - 1.001 r, p + 1.001 r]: the 0.1 % margin exceeds the rounding
     // difference, so every point within r of p lies in a visited cell.
@@ -62,12 +63,12 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
     const int z0 = (int)__builtin_floor((pz - rr) * ic), z1 = (int)__builtin_floor((pz + rr) * ic);
     const double lim = thr * (1.0 + 1e-9);
     double best = __builtin_inf();
-    int bj = -1;
+    int bj = -1, bs = -1;
     auto take = [&](int s) {
         const double d2 = dist2(px, py, pz, (double)g.x[s], (double)g.y[s], (double)g.z[s]);
         if (d2 < thr) {
             const int j = (int)g.idx[s];
-            if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; }
+            if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; if constexpr (kSlot) bs = s; }
         }
     };
     for (int x = x0; x <= x1; ++x) {
@@ -89,11 +90,11 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
                     const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
                     if (da < thr) {
                         const int j = (int)g.idx[s];
-                        if (da < best || (da == best && j < bj)) { best = da; bj = j; }
+                        if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = s; }
                     }
                     if (db < thr) {
                         const int j = (int)g.idx[s + 1];
-                        if (db < best || (db == best && j < bj)) { best = db; bj = j; }
+                        if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = s + 1; }
                     }
                 }
                 if (s < s1) take(s);
@@ -101,6 +102,7 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
         }
     }
     d2out = best;
+    if constexpr (kSlot) *slot = bs;
     return bj;
 }
 

@@ -2,18 +2,43 @@
 // DataPreparation/RANSAC.py:61-63 and dip/preprocess_correspondences.py:48,83).
 // Contract: oracle_icp (pcr_oracle.c).
 //
-// MI355X design: one 1024-thread workgroup per pair runs the whole ICP loop
-// (no host round trips).  Per iteration: 1024 threads query the target hash grid
-// for every (in-place transformed, f64) source point; Umeyama over the
-// correspondences uses the deterministic 256-lane reduction (lane = source index
-// mod 256, fixed halving tree), so the update is bit-reproducible; thread 0
-// solves Horn and composes T <- U*T; convergence is decided in-kernel.
+// MI355X design: the whole ICP loop of a pair runs inside one launch (no host
+// round trips), on one 1024-thread workgroup per pair -- or on G workgroups per
+// pair meeting at a per-pair barrier (cooperative launch, coop.h) when the batch
+// has fewer pairs than the chip has CUs.  Each workgroup holds the pair's target
+// hash grid in LDS.
+//  * The f64 working copy (transformed in place every iteration, as Open3D's
+//    Transform does) and the correspondences (target xyz + index, one float4)
+//    are stored by source index; the sweep takes 64-query chunks of the spatial
+//    (Morton-of-cell) order from a counter.
+//  * Per iteration: every point is queried in the grid (radius-limited 1-NN),
+//    then the Umeyama means and cross-covariance are summed in 1024 fixed lanes
+//    (lane l: indices l, l + 1024, ... in f64, in order) whose partials are added
+//    EXACTLY (xsum.h) -- so the result is the same whatever the number of
+//    workgroups a pair's lanes are spread over; Horn's quaternion solve and the
+//    T <- U*T update run redundantly in every workgroup on the same totals.
 #include "pcr_internal.h"
+#include "coop.h"
 #include "geom.h"
 #include "grid.h"
+#include "xsum.h"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 namespace pcr {
 namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+constexpr int kLanes = 1024;  // Umeyama sum lanes (oracle ICP_LANES): independent of G
+
+// one workgroup's partial of a reduction (G > 1): HBM slot per (pair, parity, g)
+struct XPart {
+    xs_t s[9];
+    unsigned long long acc;
+    int cnt, pad;
+};
 
 struct IArgs {
     const float *src, *tgt;
@@ -23,65 +48,161 @@ struct IArgs {
     double d, thr, rel_fit, rel_rmse;
     int max_iter;
     GridBatch grid;
-    double *P3;   // P x Nmax x 3 workspace
-    int *cj;      // P x Nmax workspace
+    double *P3;          // P x Nmax x 3 working copy by source index
+    float4 *tq;          // P x Nmax correspondence per source point: target xyz, index bits
     double *T_out, *fit_out;
     int32_t *stats;
-    int32_t *corr_tgt;  // optional (P, Nmax): final correspondence per source point
+    int32_t *corr_tgt;   // optional (P, Nmax): final correspondence per source point
     const int32_t *order;  // (P, Nmax) spatial order of the source points, or null
+    int G;
+    XPart *part;         // (P, 2, G) when G > 1
+    unsigned *bar;       // (P, 2) when G > 1
+    int *chunk;          // (P) sweep chunk counters, when G > 1
+    unsigned long long *timing;  // debug (PCR_ICP_TIMING): per pair, phase clocks
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
     return n ? min(max(n[p], 0), mx) : mx;
 }
 
-// fixed halving tree over red[0..256) x nv values (all 1024 threads call)
-__device__ inline void tree256(double (*red)[9], int nv) {
-    for (int s = 128; s >= 1; s >>= 1) {
-        if ((int)threadIdx.x < s)
-            for (int v = 0; v < nv; ++v) red[threadIdx.x][v] = red[threadIdx.x][v] + red[threadIdx.x + s][v];
-        __syncthreads();
+struct IShared {  // LDS header; the grid copy (if any) follows
+    xs_t ws[kWaves][9];
+    unsigned long long wacc[kWaves];
+    int wcnt[kWaves];
+    xs_t tot[9];
+    unsigned long long acc;
+    int cnt;
+    double T[16];     // the running transformation (init, then U * T per iteration)
+    double U[12];     // this iteration's update
+    int nred;         // reductions done (parity of the HBM partial slots)
+    int chunk;        // next 64-position chunk of the current sweep (G = 1)
+};
+
+// wave-level sum of NQ fixed-point values; lane 0 parks them in sh.ws[wave][q0..]
+template <int NQ>
+__device__ __forceinline__ void wave_park(IShared &sh, const xs_t *v, int q0) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        xs_t x = v[q];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x += xs_shfl_xor(x, o);
+        if (lane == 0) sh.ws[wid][q0 + q] = x;
     }
 }
 
-struct IShared {  // LDS header; the grid copy (if any) follows
-    double red[256][9];
-    double T[16], U[12];
-    unsigned long long s_acc[16];
-    int s_cnt[16];
-    double s_fit, s_rmse;
-    int s_count;
-    int chunk;  // next 64-query chunk of the current sweep
-};
+// the same for f64 lane partials, converted one at a time (few live registers)
+template <int NQ>
+__device__ __forceinline__ void wave_park_f64(IShared &sh, const double *v, int q0) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll 1
+    for (int q = 0; q < NQ; ++q) {
+        double d = v[0];
+#pragma unroll
+        for (int t = 1; t < NQ; ++t) d = (q == t) ? v[t] : d;
+        xs_t x = xs_term(d);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x += xs_shfl_xor(x, o);
+        if (lane == 0) sh.ws[wid][q0 + q] = x;
+    }
+}
+
+// sum the NV parked values + (cnt, acc) over the pair's workgroups; result in
+// sh.tot / sh.cnt / sh.acc (all threads call; ends with a barrier)
+template <int NV>
+__device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int cnt,
+                            unsigned long long acc) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        acc += __shfl_xor(acc, o, 64);
+    }
+    if (lane == 0) {
+        sh.wcnt[wid] = cnt;
+        sh.wacc[wid] = acc;
+    }
+    __syncthreads();
+    if (tid < NV + 2) {  // thread q sums quantity q (NV: count, NV+1: error sum)
+        xs_t s = 0;
+        unsigned long long A = 0;
+        int C = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            if (tid < NV) s += sh.ws[w][tid];
+            else if (tid == NV) C += sh.wcnt[w];
+            else A += sh.wacc[w];
+        }
+        if (a.G > 1) {
+            XPart &me = a.part[((size_t)p * 2 + (sh.nred & 1)) * a.G + g];
+            if (tid < NV) me.s[tid] = s;
+            else if (tid == NV) me.cnt = C;
+            else me.acc = A;
+        } else {
+            if (tid < NV) sh.tot[tid] = s;
+            else if (tid == NV) sh.cnt = C;
+            else sh.acc = A;
+        }
+    }
+    if (a.G > 1) {
+        pair_barrier(a.bar + 2 * (size_t)p, a.G);
+        if (tid < NV + 2) {
+            const XPart *all = a.part + ((size_t)p * 2 + (sh.nred & 1)) * a.G;
+            xs_t s = 0;
+            unsigned long long A = 0;
+            int C = 0;
+            for (int h = 0; h < a.G; ++h) {
+                if (tid < NV) s += all[h].s[tid];
+                else if (tid == NV) C += all[h].cnt;
+                else A += all[h].acc;
+            }
+            if (tid < NV) sh.tot[tid] = s;
+            else if (tid == NV) sh.cnt = C;
+            else sh.acc = A;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) sh.nred += 1;  // read only by threads < NV + 2 after the next barrier
+}
 
 template <bool kLds>
-__global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
+__global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     IShared &sh = *reinterpret_cast<IShared *>(dsm);
-    double (*red)[9] = sh.red;
-    double *T = sh.T, *U = sh.U;
-    const int p = blockIdx.x;
+    const int G = a.G;
+    const int p = blockIdx.x / G, g = blockIdx.x - p * G;
     const int n = cnt_of(a.n_src, p, a.Nmax);
     const int m = cnt_of(a.n_tgt, p, a.Mmax);
-    const int tid = threadIdx.x;
-    double *P3 = a.P3 + (size_t)p * a.Nmax * 3;
-    int *cj = a.cj + (size_t)p * a.Nmax;
+    const int tid = threadIdx.x, lane = tid & 63;
     const float *S = a.src + (size_t)p * a.Nmax * 3;
-    const float *G = a.tgt + (size_t)p * a.Mmax * 3;
-    if (tid < 16) T[tid] = a.init[(size_t)p * 16 + tid];
-    if (tid == 0) sh.chunk = 0;
+    const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
+    // working copy (f64 xyz) and correspondence (target xyz + index in one
+    // float4), both by source INDEX, AoS: one cache line per point in the sweep
+    double *P3 = a.P3 + (size_t)p * a.Nmax * 3;
+    float4 *TQ = a.tq + (size_t)p * a.Nmax;
+    if (tid < 16) sh.T[tid] = a.init[(size_t)p * 16 + tid];
+    if (tid == 0) { sh.nred = 0; sh.chunk = 0; }
     __syncthreads();
     const bool valid = a.d > 0.0 && n > 0 && m > 0;
     bool ident = true;
-    for (int k = 0; k < 16; ++k) ident = ident && (T[k] == ((k % 5 == 0) ? 1.0 : 0.0));
-    for (int i = tid; i < n; i += 1024) {
-        double x = (double)S[3 * i], y = (double)S[3 * i + 1], z = (double)S[3 * i + 2];
-        if (!ident) {
-            double ox, oy, oz;
-            xform12(T, x, y, z, ox, oy, oz);
-            x = ox; y = oy; z = oz;
+    for (int k = 0; k < 16; ++k) ident = ident && (sh.T[k] == ((k % 5 == 0) ? 1.0 : 0.0));
+    const int stride = G * kThreads, base = g * kThreads + tid;
+    // Umeyama lanes (lane l: source indices l, l + 1024, ... summed in order in
+    // f64): workgroup g owns lanes [g*LG, (g+1)*LG), one per thread
+    const int LG = kLanes / G;
+    const int my_lane = tid < LG ? g * LG + tid : -1;
+    if (valid) {  // working copy = init applied to the f32 input (Open3D's Transform)
+        double T0[12];
+        for (int q = 0; q < 12; ++q) T0[q] = sh.T[q];
+        for (int i = base; i < n; i += stride) {
+            double x = (double)S[3 * i], y = (double)S[3 * i + 1], z = (double)S[3 * i + 2];
+            if (!ident) {
+                double ox, oy, oz;
+                xform12(T0, x, y, z, ox, oy, oz);
+                x = ox; y = oy; z = oz;
+            }
+            P3[3 * i] = x; P3[3 * i + 1] = y; P3[3 * i + 2] = z;
         }
-        P3[3 * i] = x; P3[3 * i + 1] = y; P3[3 * i + 2] = z;
+        if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);  // (G = 1: the barrier below)
     }
     GridT<uint16_t> gl{};
     GridView gg{};
@@ -91,139 +212,124 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
     }
     __syncthreads();
     const double scale = fx_scale(a.thr);
+    // debug phase clocks (s_memtime) of workgroup 0's thread 0: only in a build
+    // with -DPCR_ICP_PHASES (the registers they hold cost the normal build)
+#ifdef PCR_ICP_PHASES
+    const bool tmg = a.timing != nullptr && g == 0 && tid == 0;
+#else
+    const bool tmg = false;
+#endif
+    unsigned long long tph[6] = {0, 0, 0, 0, 0, 0}, tlast = tmg ? __builtin_readcyclecounter() : 0ull;
+    const unsigned long long t00 = tlast;
+    auto mark = [&](int ph) {
+        if (tmg) {
+            const unsigned long long t = __builtin_readcyclecounter();
+            tph[ph] += t - tlast;
+            tlast = t;
+        }
+    };
+    auto sync_pair = [&]() {
+        if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);
+        else __syncthreads();
+    };
+    double fit = 0.0, rmse = 0.0, ms[3] = {0, 0, 0}, mt[3] = {0, 0, 0};
+    int count = 0;
+    // correspondences of the current points, their count / error sum and the
+    // Umeyama means
     auto evaluate = [&]() {
         unsigned long long acc = 0;
         int cnt = 0;
-        const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
-        const int nch = (n + 63) >> 6, lane = tid & 63;
-        for (;;) {  // 64-query chunks in spatial order, taken dynamically
-            int c = 0;
-            if (lane == 0) c = atomicAdd(&sh.chunk, 1);
-            c = __shfl(c, 0, 64);
-            if (c >= nch) break;
-            const int k = (c << 6) + lane;
-            if (k < n) {
-                const int i = ord ? ord[k] : k;
-                double d2;
-                int j;
-                if constexpr (kLds) j = grid_query(gl, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
-                else j = grid_query(gg, a.d, a.thr, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], d2);
-                cj[i] = j;
-                if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+        {  // 64-query chunks of the spatial order taken from a counter (dense and
+           // sparse regions cost different time)
+            int *ctr = G > 1 ? a.chunk + p : &sh.chunk;
+            const int nch = (n + 63) >> 6;
+            for (;;) {
+                int c = 0;
+                if (lane == 0) c = G > 1 ? coop_fetch_add(ctr, 1) : atomicAdd(ctr, 1);
+                c = __shfl(c, 0, 64);
+                if (c >= nch) break;
+                const int k = (c << 6) + lane;
+                if (k < n) {
+                    const int i = ord ? ord[k] : k;
+                    const double x = P3[3 * i], y = P3[3 * i + 1], z = P3[3 * i + 2];
+                    double d2;
+                    int q, s;
+                    float qx = 0.f, qy = 0.f, qz = 0.f;
+                    if constexpr (kLds) {
+                        q = grid_query<uint16_t, true>(gl, a.d, a.thr, x, y, z, d2, &s);
+                        if (q >= 0) { qx = gl.x[s]; qy = gl.y[s]; qz = gl.z[s]; }
+                    } else {
+                        q = grid_query<uint32_t, true>(gg, a.d, a.thr, x, y, z, d2, &s);
+                        if (q >= 0) { qx = gg.x[s]; qy = gg.y[s]; qz = gg.z[s]; }
+                    }
+                    TQ[i] = make_float4(qx, qy, qz, __int_as_float(q));
+                    if (q >= 0) {
+                        ++cnt;
+                        acc += (unsigned long long)(d2 * scale);
+                    }
+                }
             }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            acc += __shfl_xor(acc, o, 64);
-            cnt += __shfl_xor(cnt, o, 64);
+        // every correspondence written; the counter is re-armed for the next sweep
+        // (which comes after at least two more barriers)
+        sync_pair();
+        if (tid == 0 && g == 0) {
+            if (G > 1) __hip_atomic_store(a.chunk + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else sh.chunk = 0;
         }
-        if ((tid & 63) == 0) { sh.s_acc[tid >> 6] = acc; sh.s_cnt[tid >> 6] = cnt; }
-        __syncthreads();
-        if (tid == 0) {
-            unsigned long long A = 0;
-            int C = 0;
-            for (int w = 0; w < 16; ++w) { A += sh.s_acc[w]; C += sh.s_cnt[w]; }
-            sh.s_count = C;
-            sh.chunk = 0;  // next sweep (published by the barrier below)
-            if (C > 0) {
-                sh.s_fit = (double)C / (double)n;
-                sh.s_rmse = __builtin_sqrt(((double)A / scale) / (double)C);
-            } else {
-                sh.s_fit = 0.0;
-                sh.s_rmse = 0.0;
+        mark(0);
+        {  // means: each lane's source / target coordinate sums in index order
+            double v[6] = {0, 0, 0, 0, 0, 0};
+            if (my_lane >= 0)
+                for (int i = my_lane; i < n; i += kLanes) {
+                    const float4 t = TQ[i];
+                    if (__float_as_int(t.w) < 0) continue;
+                    v[0] = v[0] + P3[3 * i]; v[1] = v[1] + P3[3 * i + 1]; v[2] = v[2] + P3[3 * i + 2];
+                    v[3] = v[3] + (double)t.x; v[4] = v[4] + (double)t.y; v[5] = v[5] + (double)t.z;
+                }
+            wave_park_f64<6>(sh, v, 0);
+        }
+        pair_reduce<6>(a, sh, p, g, cnt, acc);
+        mark(1);
+        count = sh.cnt;
+        if (count > 0) {
+            fit = (double)count / (double)n;
+            rmse = __builtin_sqrt(((double)sh.acc / scale) / (double)count);
+            const double inv = 1.0 / (double)count;
+            for (int c = 0; c < 3; ++c) {
+                ms[c] = xs_to_double(sh.tot[c]) * inv;
+                mt[c] = xs_to_double(sh.tot[3 + c]) * inv;
             }
+        } else {
+            fit = 0.0;
+            rmse = 0.0;
         }
-        __syncthreads();
+        __syncthreads();  // sh.tot is rewritten by the next reduction
     };
     int it = 0;
     if (valid) {
         evaluate();
         for (it = 0; it < a.max_iter;) {
-            if (sh.s_count == 0) break;
-            // --- Umeyama over correspondences: means
-            if (tid < 256) {
-                double v[6] = {0, 0, 0, 0, 0, 0};
-                // four entries of this lane's sequence are loaded before they are
-                // added in sequence order: the same sums, overlapped gathers
-                int i = tid;
-                for (; i + 768 < n; i += 1024) {
-                    int jj[4];
-                    double a3[4][3], b3[4][3];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) jj[u] = cj[i + 256 * u];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ii = i + 256 * u, j = jj[u] < 0 ? 0 : jj[u];
-                        a3[u][0] = P3[3 * ii]; a3[u][1] = P3[3 * ii + 1]; a3[u][2] = P3[3 * ii + 2];
-                        b3[u][0] = (double)G[3 * j]; b3[u][1] = (double)G[3 * j + 1]; b3[u][2] = (double)G[3 * j + 2];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (jj[u] >= 0) {
-                            v[0] = v[0] + a3[u][0];
-                            v[1] = v[1] + a3[u][1];
-                            v[2] = v[2] + a3[u][2];
-                            v[3] = v[3] + b3[u][0];
-                            v[4] = v[4] + b3[u][1];
-                            v[5] = v[5] + b3[u][2];
-                        }
-                }
-                for (; i < n; i += 256) {
-                    const int j = cj[i];
-                    if (j < 0) continue;
-                    v[0] = v[0] + P3[3 * i];
-                    v[1] = v[1] + P3[3 * i + 1];
-                    v[2] = v[2] + P3[3 * i + 2];
-                    v[3] = v[3] + (double)G[3 * j];
-                    v[4] = v[4] + (double)G[3 * j + 1];
-                    v[5] = v[5] + (double)G[3 * j + 2];
-                }
-                for (int k = 0; k < 6; ++k) red[tid][k] = v[k];
-            }
-            __syncthreads();
-            tree256(red, 6);
-            const double inv = 1.0 / (double)sh.s_count;
-            const double ms0 = red[0][0] * inv, ms1 = red[0][1] * inv, ms2 = red[0][2] * inv;
-            const double mt0 = red[0][3] * inv, mt1 = red[0][4] * inv, mt2 = red[0][5] * inv;
-            __syncthreads();
-            // --- cross covariance
-            if (tid < 256) {
+            if (count == 0) break;
+            {  // --- cross covariance of the centred correspondences, per lane in order
                 double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-                auto add = [&](double s0, double s1, double s2, double t0, double t1, double t2) {
-                    v[0] = v[0] + s0 * t0; v[1] = v[1] + s0 * t1; v[2] = v[2] + s0 * t2;
-                    v[3] = v[3] + s1 * t0; v[4] = v[4] + s1 * t1; v[5] = v[5] + s1 * t2;
-                    v[6] = v[6] + s2 * t0; v[7] = v[7] + s2 * t1; v[8] = v[8] + s2 * t2;
-                };
-                int i = tid;
-                for (; i + 768 < n; i += 1024) {  // as above: loads first, sums in order
-                    int jj[4];
-                    double a3[4][3], b3[4][3];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) jj[u] = cj[i + 256 * u];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ii = i + 256 * u, j = jj[u] < 0 ? 0 : jj[u];
-                        a3[u][0] = P3[3 * ii] - ms0; a3[u][1] = P3[3 * ii + 1] - ms1; a3[u][2] = P3[3 * ii + 2] - ms2;
-                        b3[u][0] = (double)G[3 * j] - mt0; b3[u][1] = (double)G[3 * j + 1] - mt1;
-                        b3[u][2] = (double)G[3 * j + 2] - mt2;
+                if (my_lane >= 0)
+                    for (int i = my_lane; i < n; i += kLanes) {
+                        const float4 t = TQ[i];
+                        if (__float_as_int(t.w) < 0) continue;
+                        const double s0 = P3[3 * i] - ms[0], s1 = P3[3 * i + 1] - ms[1], s2 = P3[3 * i + 2] - ms[2];
+                        const double t0 = (double)t.x - mt[0], t1 = (double)t.y - mt[1], t2 = (double)t.z - mt[2];
+                        v[0] = v[0] + s0 * t0; v[1] = v[1] + s0 * t1; v[2] = v[2] + s0 * t2;
+                        v[3] = v[3] + s1 * t0; v[4] = v[4] + s1 * t1; v[5] = v[5] + s1 * t2;
+                        v[6] = v[6] + s2 * t0; v[7] = v[7] + s2 * t1; v[8] = v[8] + s2 * t2;
                     }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (jj[u] >= 0) add(a3[u][0], a3[u][1], a3[u][2], b3[u][0], b3[u][1], b3[u][2]);
-                }
-                for (; i < n; i += 256) {
-                    const int j = cj[i];
-                    if (j < 0) continue;
-                    add(P3[3 * i] - ms0, P3[3 * i + 1] - ms1, P3[3 * i + 2] - ms2, (double)G[3 * j] - mt0,
-                        (double)G[3 * j + 1] - mt1, (double)G[3 * j + 2] - mt2);
-                }
-                for (int k = 0; k < 9; ++k) red[tid][k] = v[k];
+                wave_park_f64<9>(sh, v, 0);
             }
-            __syncthreads();
-            tree256(red, 9);
+            pair_reduce<9>(a, sh, p, g, 0, 0ull);
+            mark(2);
             if (tid == 0) {
-                double Sm[9], R[9], ms[3] = {ms0, ms1, ms2}, mt[3] = {mt0, mt1, mt2};
-                for (int k = 0; k < 9; ++k) Sm[k] = red[0][k];
+                double Sm[9], R[9], U[12];
+                for (int k = 0; k < 9; ++k) Sm[k] = xs_to_double(sh.tot[k]);
                 horn_rotation(Sm, R);
                 compose_rt(R, ms, mt, U);
                 double Tn[16];
@@ -232,34 +338,52 @@ __global__ __launch_bounds__(1024) void icp_kernel(IArgs a) {
                         const double u0 = r < 3 ? U[4 * r + 0] : 0.0, u1 = r < 3 ? U[4 * r + 1] : 0.0,
                                      u2 = r < 3 ? U[4 * r + 2] : 0.0, u3 = r < 3 ? U[4 * r + 3] : 1.0;
                         Tn[4 * r + c] =
-                            ((u0 * T[c] + u1 * T[4 + c]) + u2 * T[8 + c]) + u3 * T[12 + c];
+                            ((u0 * sh.T[c] + u1 * sh.T[4 + c]) + u2 * sh.T[8 + c]) + u3 * sh.T[12 + c];
                     }
-                for (int k = 0; k < 16; ++k) T[k] = Tn[k];
+                for (int k = 0; k < 16; ++k) sh.T[k] = Tn[k];
+                for (int k = 0; k < 12; ++k) sh.U[k] = U[k];
             }
             __syncthreads();
-            for (int i = tid; i < n; i += 1024) {
-                double ox, oy, oz;
-                xform12(U, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], ox, oy, oz);
-                P3[3 * i] = ox; P3[3 * i + 1] = oy; P3[3 * i + 2] = oz;
+            mark(3);
+            {  // the points transformed in place
+                double U[12];
+                for (int q = 0; q < 12; ++q) U[q] = sh.U[q];
+                for (int i = base; i < n; i += stride) {
+                    double ox, oy, oz;
+                    xform12(U, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], ox, oy, oz);
+                    P3[3 * i] = ox; P3[3 * i + 1] = oy; P3[3 * i + 2] = oz;
+                }
             }
-            __syncthreads();
-            const double pf = sh.s_fit, pr = sh.s_rmse;
-            __syncthreads();
+            // the next sweep reads any point: every new position visible pair-wide
+            sync_pair();
+            mark(4);
+            const double pf = fit, pr = rmse;
             evaluate();
             ++it;
-            if (__builtin_fabs(pf - sh.s_fit) < a.rel_fit && __builtin_fabs(pr - sh.s_rmse) < a.rel_rmse) break;
+            if (__builtin_fabs(pf - fit) < a.rel_fit && __builtin_fabs(pr - rmse) < a.rel_rmse) break;
         }
     }
-    if (a.corr_tgt)
-        for (int i = tid; i < a.Nmax; i += 1024)
-            a.corr_tgt[(size_t)p * a.Nmax + i] = (valid && i < n) ? cj[i] : -1;
-    if (tid == 0) {
-        for (int k = 0; k < 16; ++k) a.T_out[(size_t)p * 16 + k] = T[k];
-        a.fit_out[2 * p] = valid ? sh.s_fit : 0.0;
-        a.fit_out[2 * p + 1] = valid ? sh.s_rmse : 0.0;
-        a.stats[2 * p] = it;
-        a.stats[2 * p + 1] = valid ? sh.s_count : 0;
+    if (a.corr_tgt) {
+        int32_t *ct = a.corr_tgt + (size_t)p * a.Nmax;
+        for (int i = base; i < a.Nmax; i += stride) ct[i] = (valid && i < n) ? __float_as_int(TQ[i].w) : -1;
     }
+    if (g == 0 && tid == 0) {
+        for (int k = 0; k < 16; ++k) a.T_out[(size_t)p * 16 + k] = sh.T[k];
+        a.fit_out[2 * p] = valid ? fit : 0.0;
+        a.fit_out[2 * p + 1] = valid ? rmse : 0.0;
+        a.stats[2 * p] = it;
+        a.stats[2 * p + 1] = valid ? count : 0;
+        if (tmg) {
+            unsigned long long *tt = a.timing + (size_t)p * 8;
+            for (int k = 0; k < 5; ++k) tt[k] = tph[k];
+            tt[5] = __builtin_readcyclecounter() - t00;
+            tt[6] = (unsigned long long)it;
+        }
+    }
+}
+
+const void *icp_fn(bool lds) {
+    return lds ? (const void *)icp_kernel<true> : (const void *)icp_kernel<false>;
 }
 
 }  // namespace
@@ -276,6 +400,8 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     a.rel_fit = prm->relative_fitness;
     a.rel_rmse = prm->relative_rmse;
     a.max_iter = prm->max_iteration;
+    a.P3 = nullptr;
+    a.tq = nullptr;
     if (a.d > 0.0) {
         int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
         if (rc != PCR_OK) return rc;
@@ -288,25 +414,62 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         a.grid.S = 1;
         a.grid.cell = 1.0;
     }
-    char *ws = (char *)workspace(8, (sizeof(double) * 3 + sizeof(int)) * (size_t)P * (Nmax ? Nmax : 1) + 64);
-    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
-    a.P3 = (double *)ws;
-    a.cj = (int *)(ws + sizeof(double) * 3 * (size_t)P * (Nmax ? Nmax : 1));
     a.T_out = T_out; a.fit_out = fit_out; a.stats = stats; a.corr_tgt = corr_tgt;
     const size_t hdr = (sizeof(IShared) + 15) & ~size_t(15);
     const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds_bytes(Mmax, a.grid.S, 160 * 1024 - hdr) : 0;
-    prof_begin(s, kProfIcp);
-    if (gbytes > 0) {
-        PCR_HIP_CHECK(hipFuncSetAttribute((const void *)icp_kernel<true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)(hdr + gbytes)));
-        hipLaunchKernelGGL(icp_kernel<true>, dim3(P), dim3(1024), hdr + gbytes, s, a);
+    const bool lds = gbytes > 0;
+    const size_t sm = lds ? hdr + gbytes : hdr;
+    const void *fn = icp_fn(lds);
+    PCR_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, sm) != hipSuccess) {
+        (void)hipGetLastError();
+        per_cu = 0;
+    }
+    a.G = coop_groups(P, per_cu);
+    // working copy and correspondences, by position
+    const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
+    char *ws = (char *)workspace(8, (sizeof(double) * 3 + sizeof(float4)) * (size_t)P * nm + 64);
+    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
+    a.P3 = (double *)ws;
+    a.tq = (float4 *)(ws + sizeof(double) * 3 * (size_t)P * nm);
+    if (a.G > 1) {
+        char *cw = (char *)workspace(10, (sizeof(XPart) * 2 * (size_t)a.G + sizeof(unsigned) * 3) * (size_t)P + 64);
+        PCR_REQUIRE(cw, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
+        a.part = (XPart *)cw;
+        a.bar = (unsigned *)(cw + sizeof(XPart) * 2 * (size_t)a.G * (size_t)P);
+        a.chunk = (int *)(a.bar + 2 * (size_t)P);
+        PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 3 * (size_t)P, s));
     } else {
-        PCR_HIP_CHECK(hipFuncSetAttribute((const void *)icp_kernel<false>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)hdr));
-        hipLaunchKernelGGL(icp_kernel<false>, dim3(P), dim3(1024), hdr, s, a);
+        a.part = nullptr;
+        a.bar = nullptr;
+        a.chunk = nullptr;
+    }
+    a.timing = nullptr;
+    const bool want_timing = getenv("PCR_ICP_TIMING") != nullptr;
+    if (want_timing) {
+        a.timing = (unsigned long long *)workspace(12, sizeof(unsigned long long) * 8 * (size_t)P);
+        PCR_REQUIRE(a.timing, PCR_ERR_NOMEM, "icp timing: %s", pcr_last_error());
+        PCR_HIP_CHECK(hipMemsetAsync(a.timing, 0, sizeof(unsigned long long) * 8 * (size_t)P, s));
+    }
+    prof_begin(s, kProfIcp);
+    {
+        void *args[] = {&a};
+        PCR_HIP_CHECK(coop_launch(fn, P, a.G, kThreads, args, sm, s));
     }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfIcp);
+    if (want_timing) {  // debug: phase split in shader clocks, mean over pairs, to stderr
+        std::vector<unsigned long long> h(8 * (size_t)P);
+        PCR_HIP_CHECK(hipMemcpyAsync(h.data(), a.timing, h.size() * 8, hipMemcpyDeviceToHost, s));
+        PCR_HIP_CHECK(hipStreamSynchronize(s));
+        double m[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (int q = 0; q < P; ++q)
+            for (int k = 0; k < 7; ++k) m[k] += (double)h[8 * q + k] / P;
+        fprintf(stderr, "icp timing (clocks, mean over %d pairs, G=%d): sweep %.0f means %.0f cov %.0f "
+                "horn %.0f transform %.0f total %.0f iters %.2f\n", P, a.G, m[0], m[1], m[2], m[3], m[4],
+                m[5], m[6]);
+    }
     return PCR_OK;
 }
 

@@ -5,6 +5,8 @@
 #include <mutex>
 #include <vector>
 #include "pcr_internal.h"
+#include "coop.h"
+#include <cstdlib>
 
 namespace pcr {
 
@@ -56,6 +58,30 @@ void *workspace(int slot, size_t bytes) {
     s.ptr = p;
     s.bytes = want;
     return p;
+}
+
+// ---- several workgroups per pair (coop.h) ---------------------------------
+int coop_groups(int P, int per_cu) {
+    if (const char *e = getenv("PCR_COOP_G")) {  // tests: force a split
+        const int g = atoi(e);
+        if (g >= 1 && g <= 16) return g;
+    }
+    int dev = 0, cus = 0;
+    if (per_cu <= 0 || P <= 0 || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    const long cap = (long)per_cu * cus;
+    if ((long)P * 2 > cap) return 1;
+    const long g = cap / P;
+    return (int)(g > 8 ? 8 : g);
+}
+
+hipError_t coop_launch(const void *fn, int P, int G, int threads, void **args, size_t lds,
+                       hipStream_t s) {
+    if (G <= 1) return hipLaunchKernel(fn, dim3(P), dim3(threads), args, lds, s);
+    return hipLaunchCooperativeKernel(fn, dim3(P * G), dim3(threads), args, (unsigned)lds, s);
 }
 
 // ---- optional per-kernel HIP-event timing (pcr_profile_*) -----------------

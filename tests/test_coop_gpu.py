@@ -1,0 +1,107 @@
+"""Several workgroups per pair (coop.h): RANSAC verification sweeps and ICP
+iterations split over G = 1, 2, 4, 8 workgroups of a cooperative launch must give
+the oracle's results bit for bit -- the split only changes who adds which integer
+partial.  PCR_COOP_G forces the split (the library picks G from the batch size:
+G > 1 only when the pairs alone cannot fill the CUs, e.g. 32 pairs per GPU at 8
+GPUs).  Also: ICP past its position checkpoint (> 8 iterations) and clouds with
+more points than a split's threads."""
+import os
+
+import numpy as np
+import pytest
+
+from pointcloudregistration_amd import registration as reg
+from pointcloudregistration_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _bits(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+@pytest.fixture()
+def coop_g():
+    old = os.environ.get("PCR_COOP_G")
+
+    def set_g(g):
+        os.environ["PCR_COOP_G"] = str(g)
+    yield set_g
+    if old is None:
+        os.environ.pop("PCR_COOP_G", None)
+    else:
+        os.environ["PCR_COOP_G"] = old
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_ransac_split_bitexact_vs_oracle(oracle, coop_g, G):
+    P, n = 3, 4096
+    B = synth.make_batch(P, n=n, m=n, d=32, base_seed=2000, feat_noise=1.0)
+    coop_g(G)
+    prm = reg.RansacParams(max_correspondence_distance=0.04, seed=7)
+    res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm,
+                                            pair_ids=np.arange(P, dtype=np.int32) + 9)
+    T, st, ct, mk = _np(res.transformation), _np(res.stats), _np(res.corr_tgt), _np(res.inlier_mask)
+    for p in range(P):
+        co = oracle.corres(oracle.featnn(B.src_feat[p], B.tgt_feat[p]),
+                           oracle.featnn(B.tgt_feat[p], B.src_feat[p]), True, 3)
+        r = oracle.ransac(B.src[p], B.tgt[p], co, 0.04, seed=7, pair_id=9 + p)
+        assert _bits(T[p], r["T"])
+        assert _bits(_np(res.fitness)[p], r["fitness"]) and _bits(_np(res.inlier_rmse)[p], r["inlier_rmse"])
+        assert (st[p, 0], st[p, 1], st[p, 2], st[p, 3]) == (r["iters"], r["validated"], r["best_itr"], 1)
+        cs = r["correspondence_set"]
+        got = np.nonzero(ct[p] >= 0)[0]
+        assert np.array_equal(got, cs[:, 0]) and np.array_equal(ct[p, got], cs[:, 1])
+        bits = np.unpackbits(mk[p].view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(np.nonzero(bits)[0], cs[:, 0]) and st[p, 4] == len(cs)
+
+
+def test_ransac_multi_round_low_inlier_ratio(oracle, coop_g):
+    """Noisy descriptors -> a low inlier ratio -> est_k beyond the first round of
+    1024 hypotheses: the later rounds continue the same sequential loop."""
+    P, n = 2, 2048
+    B = synth.make_batch(P, n=n, m=n, d=32, base_seed=3100, feat_noise=2.2)
+    for G in (1, 4):
+        coop_g(G)
+        prm = reg.RansacParams(max_correspondence_distance=0.04, seed=3, max_iteration=6000)
+        res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm)
+        st = _np(res.stats)
+        for p in range(P):
+            co = oracle.corres(oracle.featnn(B.src_feat[p], B.tgt_feat[p]),
+                               oracle.featnn(B.tgt_feat[p], B.src_feat[p]), True, 3)
+            r = oracle.ransac(B.src[p], B.tgt[p], co, 0.04, seed=3, pair_id=p, max_iteration=6000)
+            assert _bits(_np(res.transformation)[p], r["T"])
+            assert (st[p, 0], st[p, 1], st[p, 2]) == (r["iters"], r["validated"], r["best_itr"])
+        assert st[:, 0].max() > 1024, st[:, 0]
+
+
+@pytest.mark.parametrize("G", [1, 2, 8])
+@pytest.mark.parametrize("n,noise_init,r,relf", [(3000, 0.01, 0.02, 1e-6), (4096, 0.08, 0.1, 0.0),
+                                                 (20000, 0.03, 0.05, 1e-6)])
+def test_icp_split_bitexact_vs_oracle(oracle, coop_g, G, n, noise_init, r, relf):
+    """relative_fitness = 0 runs all 30 iterations (past the position checkpoints
+    at 8, 16 and 24 updates); 20000 points exceed a 512-thread split's threads."""
+    P = 3
+    B = synth.make_batch(P, n=n, m=n, d=8, base_seed=600 + n, feat_noise=1.0)
+    rng = np.random.default_rng(n)
+    init = np.zeros((P, 4, 4))
+    for p in range(P):
+        init[p, :3, :3] = synth.rotation_xyz(*rng.normal(0, noise_init, 3)) @ B.R[p]
+        init[p, :3, 3] = B.t[p] + rng.normal(0, noise_init, 3)
+        init[p, 3, 3] = 1
+    coop_g(G)
+    prm = reg.IcpParams(r, relative_fitness=relf, relative_rmse=relf)
+    res = reg.icp_batch(B.src, B.tgt, init, prm)
+    for p in range(P):
+        o = oracle.icp(B.src[p], B.tgt[p], r, init=init[p], relative_fitness=relf, relative_rmse=relf)
+        assert _bits(_np(res.transformation)[p], o["T"]), p
+        assert _bits(_np(res.fitness)[p], o["fitness"]) and _bits(_np(res.inlier_rmse)[p], o["inlier_rmse"])
+        assert tuple(_np(res.stats)[p]) == (o["iters"], o["n_corr"])
+        assert int((_np(res.corr_tgt)[p] >= 0).sum()) == o["n_corr"]
+    if relf == 0.0:
+        assert _np(res.stats)[:, 0].max() == 30

@@ -104,3 +104,25 @@ def test_oracle_ransac_icp_known_answer(oracle):
     assert np.array_equal(r["T"], r2["T"]) and r["iters"] == r2["iters"]
     r3 = oracle.ransac(src, tgt, co, 0.04, seed=1, pair_id=0)
     assert r3["found"] == 1
+
+
+def test_xs_sum_exact_and_order_independent(oracle):
+    """The ICP Umeyama sums (pcr_oracle.c xs_*): every term on a 2^-80 fixed-point
+    grid, integer sum, one rounding -> equals the exactly rounded rational sum for
+    terms on the grid, and does not depend on the order of the terms."""
+    from fractions import Fraction
+    rng = np.random.default_rng(0)
+    for scale in (1e-3, 1.0, 250.0):
+        v = (rng.standard_normal(8192) * scale)
+        v = np.ldexp(np.round(np.ldexp(v, 60)), -60)   # on the grid: exact terms
+        exact = sum(Fraction(float(x)) for x in v)
+        assert oracle.xs_sum(v) == float(exact)
+        for _ in range(3):
+            assert oracle.xs_sum(rng.permutation(v)) == oracle.xs_sum(v)
+    # cancellation: f64 sequential sums lose it, the exact sum does not
+    v = np.array([1e15, 1.0, -1e15, 2.0 ** -30])
+    assert oracle.xs_sum(v) == 1.0 + 2.0 ** -30
+    assert oracle.xs_sum(np.zeros(5)) == 0.0 and oracle.xs_sum(-v) == -(1.0 + 2.0 ** -30)
+    # ties round to even (f64 spacing at 2^46 is 2^-6; the format holds |sum| < 2^47)
+    assert oracle.xs_sum(np.array([2.0 ** 46, 2.0 ** -7])) == 2.0 ** 46
+    assert oracle.xs_sum(np.array([2.0 ** 46, 3 * 2.0 ** -7])) == 2.0 ** 46 + 2.0 ** -5
