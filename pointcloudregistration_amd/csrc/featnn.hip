@@ -7,19 +7,16 @@
 // (oracle_featnn): argmin_j D_ij, D_ij = sum_k ((double)f_ik - (double)g_jk)^2
 // summed sequentially in f64, lowest index on ties.
 //
-// MI355X design:
-//  1. pack: features -> MFMA operand layout [tile][k-pair s][lane], lane l holds
-//     row 32t+(l&31), dim 2s+(l>>5) (both A and B of v_mfma_f32_32x32x2_f32 use
-//     this map), zero-padded to a multiple of 16 dims; squared norms.
-//  2. screen: each wave owns 32 query rows (A = -2*q kept in VGPRs) and sweeps
-//     every 32-candidate tile: C is seeded with |g_j|^2, 8*KCH f32-in MFMAs give
-//     s_ij = |g_j|^2 - 2 q_i.g_j as an exact k-ordered fmaf chain; a running
-//     top-2 per row (v_med3 + v_min + cndmask) is kept per lane and merged
-//     across lanes once at the end.
-//  3. certify: |s^ - s| <= (K+1) 2^-24 (|q_i| + max_j |g_j|)^2.  If the top-2 gap
-//     exceeds 2x that bound (x2 safety), the winner is the exact f64 argmin; else
-//     the row is queued for an exact f64 rescan (4. rescan, one wave per row).
-//  The screen is the MFMA-bound kernel (4.3 GFLOP per 8192^2 x 32 direction).
+// MI355X design: screen every (row, column) pair of a
+// cloud pair with an MFMA distance tile, keep a top-2 per row and per column,
+// certify a winner when its top-2 gap exceeds a rigorous bound on the screen's
+// error, and recompute every uncertified row / column exactly in f64.
+//  * D <= 64 (the product's shapes): f16 x3 split operands on
+//    v_mfma_f32_32x32x16_f16 (feat_maxabs, feat_pack5r / feat_pack5,
+//    featnn_dual7, featnn_colmerge5, featnn_rescan3);
+//  * 64 < D <= 128: the augmented f32 operands on v_mfma_f32_32x32x2_f32
+//    (feat_pack_aug, featnn_dual3, featnn_colmerge3, featnn_rescan2).
+// Both directions come out of one screen launch.
 #include "pcr_internal.h"
 #include "scan.h"
 #include <stdlib.h>
@@ -32,160 +29,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int count_of(const int32_t *n, int p, int Nmax) {
     return n ? min(max(n[p], 0), Nmax) : Nmax;
-}
-
-// X (P, Nmax, D) -> Xp (P, ntiles, S2, 64); cn/nrm (P, ntiles*32); gmax (P) float bits
-__global__ __launch_bounds__(64) void feat_pack(const float *X, const int32_t *n, int Nmax, int D,
-                                                int S2, int ntiles, float *Xp, float *cn,
-                                                float *nrm, unsigned *gmax) {
-    const int p = blockIdx.y, t = blockIdx.x, l = threadIdx.x;
-    const int cnt = count_of(n, p, Nmax);
-    const int row = t * 32 + (l & 31), h = l >> 5;
-    const bool valid = row < cnt;
-    const float *x = X + ((size_t)p * Nmax + (valid ? row : 0)) * D;
-    float *dst = Xp + (((size_t)p * ntiles + t) * S2) * 64 + l;
-    for (int s = 0; s < S2; ++s) {
-        const int k = 2 * s + h;
-        dst[(size_t)s * 64] = (valid && k < D) ? x[k] : 0.0f;
-    }
-    if (h == 0) {
-        float c = __builtin_inff(), r = 0.0f;
-        if (valid) {
-            double acc = 0.0;
-            for (int k = 0; k < D; ++k) acc = acc + (double)x[k] * (double)x[k];
-            c = (float)acc;
-            r = (float)__builtin_sqrt(acc);
-            atomicMax(gmax + p, __float_as_uint(r));
-        }
-        cn[(size_t)p * ntiles * 32 + row] = c;
-        nrm[(size_t)p * ntiles * 32 + row] = r;
-    }
-}
-
-struct ScreenArgs {
-    const float *Qp, *Cp;   // packed queries / candidates
-    const float *ccn;       // candidate |g|^2 (+inf on padding)
-    const float *qnrm;      // query |q|
-    const unsigned *cgmax;  // max candidate |g| (float bits) per pair
-    const int32_t *nq, *nc; // valid counts (may be null)
-    int Nqmax, Ncmax, ntq, ntc, S2;
-    int32_t *nn;            // (P, Nqmax)
-    int *list;              // ambiguous rows: p*Nqmax + row
-    int *list_count;
-};
-
-template <int KCH>
-__global__ __launch_bounds__(256) void featnn_screen(ScreenArgs a) {
-    constexpr int S2 = 8 * KCH;
-    const int p = blockIdx.y;
-    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int qt = blockIdx.x * 4 + wid;
-    const int nq = count_of(a.nq, p, a.Nqmax);
-    if (qt * 32 >= nq) return;  // wave-uniform
-    const int nc = count_of(a.nc, p, a.Ncmax);
-    const int ntc = (nc + 31) >> 5;
-
-    float A[S2];
-    const float *qp = a.Qp + (((size_t)p * a.ntq + qt) * S2) * 64 + l;
-#pragma unroll
-    for (int s = 0; s < S2; ++s) A[s] = -2.0f * qp[(size_t)s * 64];
-
-    float b1[16], b2[16];
-    int i1[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); i1[r] = 0; }
-
-    const float *cbase = a.Cp + ((size_t)p * a.ntc * S2) * 64 + l;
-    const float *cnb = a.ccn + (size_t)p * a.ntc * 32 + (l & 31);
-    for (int ct = 0; ct < ntc; ++ct) {
-        const float *cp = cbase + (size_t)ct * S2 * 64;
-        float B[S2];
-#pragma unroll
-        for (int s = 0; s < S2; ++s) B[s] = cp[(size_t)s * 64];
-        const float c0 = cnb[ct * 32];
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = c0;
-#pragma unroll
-        for (int s = 0; s < S2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], B[s], acc, 0, 0, 0);
-        const int j = ct * 32 + (l & 31);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float v = acc[r];
-            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], v);
-            const bool c = v < b1[r];
-            b1[r] = c ? v : b1[r];
-            i1[r] = c ? j : i1[r];
-        }
-    }
-    // merge the 32 lanes of each half (same rows, disjoint candidate classes)
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float ob1 = __shfl_xor(b1[r], o, 64);
-            const float ob2 = __shfl_xor(b2[r], o, 64);
-            const int oi1 = __shfl_xor(i1[r], o, 64);
-            const bool take = (ob1 < b1[r]) || (ob1 == b1[r] && oi1 < i1[r]);
-            const float nb2 = fminf(fmaxf(b1[r], ob1), fminf(b2[r], ob2));
-            b1[r] = take ? ob1 : b1[r];
-            i1[r] = take ? oi1 : i1[r];
-            b2[r] = nb2;
-        }
-    }
-    const int h = l >> 5, lr = l & 31;
-    if (lr >= 16) return;
-    float mb1 = 0.f, mb2 = 0.f;
-    int mi1 = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
-    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-    if (row >= nq) return;
-    a.nn[(size_t)p * a.Nqmax + row] = mi1;
-    const double G = (double)__uint_as_float(a.cgmax[p]);
-    const double qn = (double)a.qnrm[(size_t)p * a.ntq * 32 + row];
-    const double K = 2.0 * S2;
-    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (qn + G) * (qn + G);
-    if (!((double)mb2 - (double)mb1 > bound)) {
-        const int e = atomicAdd(a.list_count, 1);
-        a.list[e] = p * a.Nqmax + row;
-    }
-}
-
-// exact f64 rescan of ambiguous rows: one wave per row, grid-stride over the list
-__global__ __launch_bounds__(256) void featnn_rescan(const float *Q, const float *C, int Nqmax,
-                                                     int Ncmax, int D, const int32_t *ncnt,
-                                                     const int *list, const int *list_count,
-                                                     int32_t *nn) {
-    const int l = threadIdx.x & 63;
-    const int nwaves = gridDim.x * 4;
-    const int count = *list_count;
-    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < count; e += nwaves) {
-        const int code = list[e];
-        const int p = code / Nqmax, row = code - p * Nqmax;
-        const int nc = count_of(ncnt, p, Ncmax);
-        const float *q = Q + ((size_t)p * Nqmax + row) * D;
-        const float *cb = C + (size_t)p * Ncmax * D;
-        double best = __builtin_inf();
-        int bj = 0x7fffffff;
-        for (int j = l; j < nc; j += 64) {
-            const float *c = cb + (size_t)j * D;
-            double acc = 0.0;
-            for (int k = 0; k < D; ++k) {
-                const double df = (double)q[k] - (double)c[k];
-                acc = acc + df * df;
-            }
-            if (acc < best) { best = acc; bj = j; }
-        }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const double ob = __shfl_xor(best, o, 64);
-            const int oj = __shfl_xor(bj, o, 64);
-            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
-        }
-        if (l == 0) nn[(size_t)p * Nqmax + row] = (bj == 0x7fffffff) ? 0 : bj;
-    }
 }
 
 // mutual filter + ordered compaction (one block per pair)
@@ -220,30 +63,6 @@ __global__ __launch_bounds__(1024) void corres_build(const int32_t *nn12, const 
     if (threadIdx.x == 0) n_corres[p] = use_mutual ? total : n;
 }
 
-
-// ---------------------------------------------------------------------------
-// v2: ONE pass for both directions.  t_ij = -2 f_i.g_j (exact fmaf chain from
-// C = 0); row value t + |g_j|^2, column value t + |f_i|^2 (one more rounding:
-// the (K+2) factor of the bound covers it).  Workgroup = 8 waves x 32 rows =
-// 256 rows; every wave sweeps all candidate tiles in groups of G tiles (G
-// independent accumulator chains).  Row top-2 stays in registers (as v1);
-// column top-2 over the wave's 32 rows is merged across the 8 waves through
-// LDS once per group and written as one partial per 256-row block; a final
-// kernel merges the partials and certifies each column.
-// ---------------------------------------------------------------------------
-struct DualArgs {
-    const float *Fp, *Gp;         // packed rows (src) / columns (tgt)
-    const float *fcn, *gcn;       // |f|^2, |g|^2 (+inf padding), (P, tiles*32)
-    const float *fnr, *gnr;       // |f|, |g|
-    const unsigned *fmax, *gmax;  // per-pair max norms (float bits)
-    const int32_t *n_src, *n_tgt;
-    int Nmax, Mmax, ntn, ntm, nrb;
-    int32_t *nn12;
-    int *list12, *count12;
-    float *cp1, *cp2;             // (P, nrb, ntm*32) column partials
-    int *cpi;
-};
-
 // merge two top-2 states; lowest index wins equal minima.  Branch-free: the
 // screen's values are finite or +inf (never NaN), so plain selects are exact.
 __device__ __forceinline__ void top2_merge(float &b1, int &i1, float &b2, float o1, int oi, float o2) {
@@ -255,155 +74,6 @@ __device__ __forceinline__ void top2_merge(float &b1, int &i1, float &b2, float 
     i1 = take ? oi : i1;
     b2 = n2;
 }
-
-template <int KCH, int G>
-__global__ __launch_bounds__(512) void featnn_dual(DualArgs a) {
-    constexpr int S2 = 8 * KCH;
-    __shared__ float l_c1[2][G][8][32], l_c2[2][G][8][32];
-    __shared__ int l_ci[2][G][8][32];
-    const int p = blockIdx.y, rb = blockIdx.x;
-    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
-    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
-    const int qt = rb * 8 + wid;
-    const bool active = qt * 32 < n;  // wave-uniform; inactive waves still hit barriers
-    const int ntc = (m + 31) >> 5;
-
-    float A[S2];
-    const float *qp = a.Fp + (((size_t)p * a.ntn + (active ? qt : 0)) * S2) * 64 + l;
-#pragma unroll
-    for (int s = 0; s < S2; ++s) A[s] = active ? -2.0f * qp[(size_t)s * 64] : 0.0f;
-    float rn[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        rn[r] = active ? a.fcn[(size_t)p * a.ntn * 32 + row] : __builtin_inff();
-    }
-    float b1[16], b2[16];
-    int i1[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); i1[r] = 0; }
-
-    const float *gbase = a.Gp + ((size_t)p * a.ntm * S2) * 64 + l;
-    const float *gcn = a.gcn + (size_t)p * a.ntm * 32;
-    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
-    int buf = 0;
-    for (int ct0 = 0; ct0 < ntc; ct0 += G, buf ^= 1) {
-        float B[G][S2];
-        f32x16 acc[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int ct = min(ct0 + g, ntc - 1);
-            const float *cp = gbase + (size_t)ct * S2 * 64;
-#pragma unroll
-            for (int s = 0; s < S2; ++s) B[g][s] = cp[(size_t)s * 64];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
-        }
-#pragma unroll
-        for (int s = 0; s < S2; ++s)
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-                acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], B[g][s], acc[g], 0, 0, 0);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int ct = ct0 + g;
-            const bool tile_ok = ct < ntc;  // uniform
-            const int j = ct * 32 + (l & 31);
-            const float gn = tile_ok ? gcn[j] : __builtin_inff();
-            float c1 = __builtin_inff(), c2 = __builtin_inff();
-            int ci = 0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float t = acc[g][r];
-                const float v = t + gn;  // row direction
-                b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], v);
-                const bool c = v < b1[r];
-                b1[r] = c ? v : b1[r];
-                i1[r] = c ? j : i1[r];
-                const float w = t + rn[r];  // column direction (rows increase with r)
-                c2 = __builtin_amdgcn_fmed3f(c1, c2, w);
-                const bool cc = w < c1;
-                c1 = cc ? w : c1;
-                ci = cc ? (qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) : ci;
-            }
-            const float o1 = __shfl_xor(c1, 32, 64), o2 = __shfl_xor(c2, 32, 64);
-            const int oi = __shfl_xor(ci, 32, 64);
-            top2_merge(c1, ci, c2, o1, oi, o2);
-            if (h == 0) {
-                l_c1[buf][g][wid][l] = c1;
-                l_c2[buf][g][wid][l] = c2;
-                l_ci[buf][g][wid][l] = ci;
-            }
-        }
-        __syncthreads();
-        const int t = threadIdx.x;
-        if (t < G * 32) {
-            const int g = t >> 5, col = t & 31, ct = ct0 + g;
-            if (ct < ntc) {
-                float m1 = l_c1[buf][g][0][col], m2 = l_c2[buf][g][0][col];
-                int mi = l_ci[buf][g][0][col];
-#pragma unroll
-                for (int w = 1; w < 8; ++w)
-                    top2_merge(m1, mi, m2, l_c1[buf][g][w][col], l_ci[buf][g][w][col],
-                               l_c2[buf][g][w][col]);
-                const size_t o = cpoff + (size_t)ct * 32 + col;
-                a.cp1[o] = m1;
-                a.cp2[o] = m2;
-                a.cpi[o] = mi;
-            }
-        }
-    }
-    if (!active) return;
-    // rows: merge the 32 lanes of each half, certify, write
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float ob1 = __shfl_xor(b1[r], o, 64);
-            const float ob2 = __shfl_xor(b2[r], o, 64);
-            const int oi1 = __shfl_xor(i1[r], o, 64);
-            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
-        }
-    }
-    const int lr = l & 31;
-    if (lr >= 16) return;
-    float mb1 = 0.f, mb2 = 0.f;
-    int mi1 = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
-    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-    if (row >= n) return;
-    a.nn12[(size_t)p * a.Nmax + row] = mi1;
-    const double Gm = (double)__uint_as_float(a.gmax[p]);
-    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
-    const double K = 2.0 * S2;
-    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (qn + Gm) * (qn + Gm);
-    if (!((double)mb2 - (double)mb1 > bound)) a.list12[atomicAdd(a.count12, 1)] = p * a.Nmax + row;
-}
-
-// merge the per-256-row-block column partials in block order; certify columns
-__global__ void featnn_colmerge(DualArgs a, int32_t *nn21, int *list21, int *count21, int S2) {
-    const int p = blockIdx.y;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int m = count_of(a.n_tgt, p, a.Mmax);
-    if (j >= m) return;
-    const int n = count_of(a.n_src, p, a.Nmax);
-    const int nrb_used = (((n + 31) >> 5) + 7) >> 3;
-    float b1 = __builtin_inff(), b2 = __builtin_inff();
-    int i1 = 0;
-    for (int rb = 0; rb < nrb_used; ++rb) {
-        const size_t o = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32 + j;
-        top2_merge(b1, i1, b2, a.cp1[o], a.cpi[o], a.cp2[o]);
-    }
-    nn21[(size_t)p * a.Mmax + j] = i1;
-    const double F = (double)__uint_as_float(a.fmax[p]);
-    const double gn = (double)a.gnr[(size_t)p * a.ntm * 32 + j];
-    const double K = 2.0 * S2;
-    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (gn + F) * (gn + F);
-    if (!((double)b2 - (double)b1 > bound)) list21[atomicAdd(count21, 1)] = p * a.Mmax + j;
-}
-
 
 // ---------------------------------------------------------------------------
 // v3: augmented operands.  Row operand A_i = [-2 f_i, 1, |f_i|^2], column
@@ -555,173 +225,6 @@ __global__ __launch_bounds__(512) void featnn_dual3(DualArgs3 a) {
                 Pc1[e] = cc1;
                 Pc2[e] = cc2;
                 Pci[e] = cci;
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const int t = threadIdx.x;
-        if (t < G * 32) {
-            const int g = t >> 5, col = t & 31, ct = grp * G + g;
-            if (ct < ntc) {
-                const int e0 = (buf * G + g) * 256 + col;
-                float m1 = Pc1[e0], m2 = Pc2[e0];
-                int mi = Pci[e0];
-#pragma unroll
-                for (int w = 1; w < 8; ++w)
-                    top2_merge(m1, mi, m2, Pc1[e0 + 32 * w], Pci[e0 + 32 * w], Pc2[e0 + 32 * w]);
-                const size_t o = cpoff + (size_t)ct * 32 + col;
-                a.cp1[o] = m1;
-                a.cp2[o] = m2;
-                a.cpi[o] = mi;
-            }
-        }
-    }
-    if (!active) return;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float ob1 = __shfl_xor(b1[r], o, 64);
-            const float ob2 = __shfl_xor(b2[r], o, 64);
-            const int oi1 = __shfl_xor(i1[r], o, 64);
-            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
-        }
-    }
-    const int lr = l & 31;
-    if (lr >= 16) return;
-    float mb1 = 0.f, mb2 = 0.f;
-    int mi1 = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
-    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-    if (row >= n) return;
-    a.nn12[(size_t)p * a.Nmax + row] = mi1;
-    const double Gm = (double)__uint_as_float(a.gmax[p]);
-    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
-    const double K = 2.0 * S2a;
-    const double bound = 4.0 * (K + 2.0) * 5.9604644775390625e-08 * (qn + Gm) * (qn + Gm);
-    if (!((double)mb2 - (double)mb1 > bound)) a.list12[atomicAdd(a.count12, 1)] = p * a.Nmax + row;
-}
-
-
-// ---------------------------------------------------------------------------
-// v4 = v3 + tile-level software pipelining inside each wave: the MFMA chain of
-// tile t+1 is issued, then the VALU top-2 epilogue of tile t runs in its
-// shadow (sched_group_barrier interleaves 1 LDS read : 1 MFMA : N VALU), so
-// the matrix pipe and the VALU overlap within one wave instead of relying on
-// the partner wave (the per-group barrier keeps partners in phase).  G = 8
-// tiles per LDS group; padded tiles exist in the packed buffer with +inf
-// norms, so the loop body has no tail branches.
-// ---------------------------------------------------------------------------
-template <int KCH, int G>
-__global__ __launch_bounds__(512) void featnn_dual4(DualArgs3 a) {
-    constexpr int S2a = 8 * KCH + 1;
-    constexpr int kB = G * S2a * 64;
-    constexpr int kP = G * 8 * 32;
-    __shared__ __attribute__((aligned(16))) float smem[2 * kB + 2 * 3 * kP];
-    float *Bs = smem;
-    float *Pc1 = smem + 2 * kB;
-    float *Pc2 = Pc1 + 2 * kP;
-    int *Pci = reinterpret_cast<int *>(Pc2 + 2 * kP);
-    const int p = blockIdx.y, rb = blockIdx.x;
-    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
-    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
-    const int qt = rb * 8 + wid;
-    const bool active = qt * 32 < n;
-    const int ntc = (m + 31) >> 5;
-    const int ngroups = (ntc + G - 1) / G;
-    const int ntp = a.ntm;  // packed tiles incl. padding (>= ngroups*G)
-
-    float A[S2a];
-    const float *qp = a.Ap + (((size_t)p * a.ntn + (active ? qt : 0)) * S2a) * 64 + l;
-#pragma unroll
-    for (int s = 0; s < S2a; ++s) A[s] = qp[(size_t)s * 64];
-    if (!active) {
-#pragma unroll
-        for (int s = 0; s < S2a - 1; ++s) A[s] = 0.0f;
-        A[S2a - 1] = h == 0 ? 1.0f : __builtin_inff();
-    }
-    float b1[16], b2[16];
-    int i1[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); i1[r] = 0; }
-    const int rowbase = qt * 32 + 4 * h;
-
-    const float *bsrc = a.Bp + ((size_t)p * ntp * S2a) * 64 + l;
-    auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * S2a; c += 8) {
-            const int g = c / S2a, srow = c - g * S2a;
-            const int ct = grp * G + g;
-            const float *src = bsrc + ((size_t)ct * S2a + srow) * 64;
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)src,
-                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + (g * S2a + srow) * 64), 4,
-                0, 0);
-        }
-    };
-    auto chain = [&](const float *Bt) {
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-        for (int s = 0; s < S2a; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], Bt[s * 64], acc, 0, 0, 0);
-        return acc;
-    };
-    auto epilogue = [&](const f32x16 &acc, int ct, int bufg) {
-        const int j = ct * 32 + (l & 31);
-        float c1[4], c2[4];
-        int ci[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { c1[q] = __builtin_inff(); c2[q] = __builtin_inff(); ci[q] = 0; }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float v = acc[r];
-            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], v);
-            const bool c = v < b1[r];
-            b1[r] = c ? v : b1[r];
-            i1[r] = c ? j : i1[r];
-            const int q = r & 3;
-            c2[q] = __builtin_amdgcn_fmed3f(c1[q], c2[q], v);
-            const bool cc = v < c1[q];
-            c1[q] = cc ? v : c1[q];
-            ci[q] = cc ? (rowbase + (r & 3) + 8 * (r >> 2)) : ci[q];
-        }
-        top2_merge(c1[0], ci[0], c2[0], c1[1], ci[1], c2[1]);
-        top2_merge(c1[2], ci[2], c2[2], c1[3], ci[3], c2[3]);
-        top2_merge(c1[0], ci[0], c2[0], c1[2], ci[2], c2[2]);
-        const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
-        const int oi = __shfl_xor(ci[0], 32, 64);
-        top2_merge(c1[0], ci[0], c2[0], o1, oi, o2);
-        // both half-waves hold the same merged state: both write (benign)
-        const int e = bufg * 256 + wid * 32 + (l & 31);
-        Pc1[e] = c1[0];
-        Pc2[e] = c2[0];
-        Pci[e] = ci[0];
-    };
-    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int grp = 0; grp < ngroups; ++grp) {
-        const int buf = grp & 1;
-        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
-        const float *Bb = Bs + buf * kB + l;
-        f32x16 cur = chain(Bb);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            f32x16 nxt;
-            if (g + 1 < G) nxt = chain(Bb + (g + 1) * S2a * 64);
-            epilogue(cur, grp * G + g, buf * G + g);
-            if (g + 1 < G) {
-#pragma unroll
-                for (int k = 0; k < S2a; ++k) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 10, 0); // VALU
-                }
-                cur = nxt;
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1079,372 +582,6 @@ __device__ __forceinline__ float vmed3(float a, float b, float c) {
     return d;
 }
 
-// ABL (debug ablations, results invalid): 1 no epilogue, 2 no MFMA, 3 no
-// barrier/DMA (B read from buffer 0)
-template <int NCH, int G, int ABL = 0>
-__global__ __launch_bounds__(512) void featnn_dual5(DualArgs5 a) {
-    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
-    constexpr int kP = G * 8 * 32;
-    __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 2 * 2 * kP * 4];
-    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem);
-    float *Pc1 = reinterpret_cast<float *>(smem + 2 * kB * 16);  // [2][G][8 waves][32 cols]
-    float *Pc2 = Pc1 + 2 * kP;
-    // XCD-aware: hardware XCD = linear block id % 8; keep a pair on one XCD
-    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
-    if (p >= a.P) return;  // whole block
-    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
-    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
-    const int qt = rb * 8 + wid;  // < ntn (row tiles padded to nrb*8)
-    const int ntc = (m + 31) >> 5;
-    const int ngroups = (ntc + G - 1) / G;
-    // index packing (the codes ride in the low mantissa bits; the
-    // certification charges the perturbation): row values carry the column
-    // tile ct in their low ctbits; column values carry (wave, half, register)
-    // = the row within the 256-row block in their low 8 bits.
-    const unsigned ctmask = (1u << a.ctbits) - 1u;
-    unsigned keep_r = ~ctmask;
-    asm("" : "+v"(keep_r));  // VGPR: a VOP3 reads one SGPR on gfx9 (ct is the other operand)
-    unsigned ccode[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        ccode[r] = (unsigned)((wid << 5) | (h << 4) | r);
-        asm("" : "+v"(ccode[r]));  // opaque: one v_and_or per column value
-    }
-
-    f16x8 A[NCH];
-    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NCH * 64 + l;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
-    float b1[16], b2[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
-
-    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NCH * 64 + l;
-    auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NCH; c += 8) {
-            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)src,
-                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
-        }
-    };
-    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int grp = 0; grp < ngroups; ++grp) {
-        const int buf = ABL == 3 ? 0 : grp & 1;
-        if (ABL != 3 && grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
-        const f16x8 *Bb = Bs + buf * kB + l;
-        f32x16 acc[G];
-        if (ABL == 2) {
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[g][r] = __uint_as_float(ccode[r] ^ (unsigned)(grp * G + g));
-        } else {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-                acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bb[(g * NCH + c) * 64], acc[g],
-                                                                0, 0, 0);
-        }
-        if (ABL == 1) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) b1[g] = vmin(b1[g], acc[g][g]);
-        } else
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            unsigned ct = (unsigned)(grp * G + g);
-            asm("" : "+s"(ct));  // keep ct one scalar: one v_and_or per row value
-            float c1[4], c2[4];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const unsigned ub = __float_as_uint(acc[g][r]);
-                const float vr = __uint_as_float((ub & keep_r) | ct);
-                const float vc = __uint_as_float((ub & 0xFFFFFF00u) | ccode[r]);
-                b2[r] = vmed3(b1[r], b2[r], vr);
-                b1[r] = vmin(b1[r], vr);
-                const int q = r & 3;
-                if (r < 4) {  // chain q starts at r = q
-                    c1[q] = vc;
-                    c2[q] = __builtin_inff();
-                } else {
-                    c2[q] = vmed3(c1[q], c2[q], vc);
-                    c1[q] = vmin(c1[q], vc);
-                }
-            }
-            // packed top-2 merges: second of two sorted pairs = med3(a1, b1, min(a2, b2))
-#pragma unroll
-            for (int q = 0; q < 4; q += 2) {
-                const float m2 = vmin(c2[q], c2[q + 1]);
-                c2[q] = vmed3(c1[q], c1[q + 1], m2);
-                c1[q] = vmin(c1[q], c1[q + 1]);
-            }
-            float m2 = vmin(c2[0], c2[2]);
-            c2[0] = vmed3(c1[0], c1[2], m2);
-            c1[0] = vmin(c1[0], c1[2]);
-            const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
-            m2 = vmin(c2[0], o2);
-            c2[0] = vmed3(c1[0], o1, m2);
-            c1[0] = vmin(c1[0], o1);
-            // both halves hold the merged state; both write (same value)
-            const int e = (buf * G + g) * 256 + wid * 32 + (l & 31);
-            Pc1[e] = c1[0];
-            Pc2[e] = c2[0];
-        }
-        if (ABL == 3) continue;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const int t = threadIdx.x;
-        if (t < G * 32) {
-            const int g = t >> 5, col = t & 31, ct = grp * G + g;
-            if (ct < ntc) {
-                const int e0 = (buf * G + g) * 256 + col;
-                float m1 = Pc1[e0], mm2 = Pc2[e0];
-#pragma unroll
-                for (int w = 1; w < 8; ++w) {
-                    const float o1 = Pc1[e0 + 32 * w], o2 = Pc2[e0 + 32 * w];
-                    const float t2 = vmin(mm2, o2);
-                    mm2 = vmed3(m1, o1, t2);
-                    m1 = vmin(m1, o1);
-                }
-                // no row index stored: featnn_colmerge5 decodes it from m1's
-                // code bits (a third fewer column-partial bytes written and read)
-                const size_t o = cpoff + (size_t)ct * 32 + col;
-                a.cp1[o] = m1;
-                a.cp2[o] = mm2;
-            }
-        }
-    }
-    if (qt * 32 >= n) return;
-    int i1[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + (l & 31);
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float ob1 = __shfl_xor(b1[r], o, 64);
-            const float ob2 = __shfl_xor(b2[r], o, 64);
-            const int oi1 = __shfl_xor(i1[r], o, 64);
-            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
-        }
-    }
-    const int lr = l & 31;
-    if (lr >= 16) return;
-    float mb1 = 0.f, mb2 = 0.f;
-    int mi1 = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
-    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-    if (row >= n) return;
-    if (m == 0) { a.nn12[(size_t)p * a.Nmax + row] = 0; return; }
-    a.nn12[(size_t)p * a.Nmax + row] = mi1;
-    const double Gm = (double)__uint_as_float(a.gmax[p]);
-    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
-    const double pert = __builtin_ldexp(1.0, a.ctbits - 23) *
-                        (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2));
-    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NCH, a.D) + pert))
-        a.list12[(size_t)p * a.Nmax + atomicAdd(a.count12 + p, 1)] = row;
-}
-
-// ---------------------------------------------------------------------------
-// v6 = v5 with the two waves of each SIMD in complementary phases.  A
-// 512-thread workgroup places waves w and w+4 on the same SIMD; with one
-// barrier per LDS group both would issue their MFMAs together and then their
-// VALU epilogues together.  Waves 4-7 therefore lag one group: in barrier
-// interval k they run the epilogue of group k-1 (accumulators kept in
-// registers) and then the MFMAs of group k, while waves 0-3 run MFMAs of k
-// then its epilogue -- every SIMD pairs a matrix phase with a VALU phase.
-// Column partials rotate over 3 LDS buffers; group k's 8-wave merge runs in
-// interval k+2, after both halves have written it.  Waves 4-7 take
-// s_setprio 1 (the second-dispatched half otherwise loses VALU arbitration).
-// ---------------------------------------------------------------------------
-template <int NCH, int G>
-__global__ __launch_bounds__(512) void featnn_dual6(DualArgs5 a) {
-    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
-    constexpr int kP = G * 8 * 32;
-    __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 3 * 2 * kP * 4];
-    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem);
-    float *Pc1 = reinterpret_cast<float *>(smem + 2 * kB * 16);  // [3][G][8 waves][32 cols]
-    float *Pc2 = Pc1 + 3 * kP;
-    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
-    if (p >= a.P) return;  // whole block
-    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
-    const bool lag = wid >= 4;
-    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
-    const int qt = rb * 8 + wid;
-    const int ntc = (m + 31) >> 5;
-    const int ngroups = (ntc + G - 1) / G;
-    const unsigned ctmask = (1u << a.ctbits) - 1u;
-    unsigned keep_r = ~ctmask;
-    asm("" : "+v"(keep_r));
-    unsigned ccode[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        ccode[r] = (unsigned)((wid << 5) | (h << 4) | r);
-        asm("" : "+v"(ccode[r]));
-    }
-    f16x8 A[NCH];
-    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NCH * 64 + l;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
-    float b1[16], b2[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
-
-    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NCH * 64 + l;
-    auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NCH; c += 8) {
-            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)src,
-                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
-        }
-    };
-    auto chain = [&](int buf, f32x16 (&acc)[G]) {
-        const f16x8 *Bb = Bs + buf * kB + l;
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[g][r] = 0.0f;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-                acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bb[(g * NCH + c) * 64], acc[g],
-                                                                0, 0, 0);
-    };
-    auto epilogue = [&](const f32x16 (&acc)[G], int grp) {
-        const int pb = grp % 3;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            unsigned ct = (unsigned)(grp * G + g);
-            asm("" : "+s"(ct));
-            float c1[4], c2[4];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const unsigned ub = __float_as_uint(acc[g][r]);
-                const float vr = __uint_as_float((ub & keep_r) | ct);
-                const float vc = __uint_as_float((ub & 0xFFFFFF00u) | ccode[r]);
-                b2[r] = vmed3(b1[r], b2[r], vr);
-                b1[r] = vmin(b1[r], vr);
-                const int q = r & 3;
-                if (r < 4) {
-                    c1[q] = vc;
-                    c2[q] = __builtin_inff();
-                } else {
-                    c2[q] = vmed3(c1[q], c2[q], vc);
-                    c1[q] = vmin(c1[q], vc);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q += 2) {
-                const float m2 = vmin(c2[q], c2[q + 1]);
-                c2[q] = vmed3(c1[q], c1[q + 1], m2);
-                c1[q] = vmin(c1[q], c1[q + 1]);
-            }
-            float m2 = vmin(c2[0], c2[2]);
-            c2[0] = vmed3(c1[0], c1[2], m2);
-            c1[0] = vmin(c1[0], c1[2]);
-            const float o1 = __shfl_xor(c1[0], 32, 64), o2 = __shfl_xor(c2[0], 32, 64);
-            m2 = vmin(c2[0], o2);
-            c2[0] = vmed3(c1[0], o1, m2);
-            c1[0] = vmin(c1[0], o1);
-            const int e = (pb * G + g) * 256 + wid * 32 + (l & 31);
-            Pc1[e] = c1[0];
-            Pc2[e] = c2[0];
-        }
-    };
-    const size_t cpoff = ((size_t)p * a.nrb + rb) * (size_t)a.ntm * 32;
-    auto merge = [&](int grp) {  // 8-wave column merge of group grp
-        const int t = threadIdx.x;
-        if (t < G * 32) {
-            const int g = t >> 5, col = t & 31, ct = grp * G + g;
-            if (ct < ntc) {
-                const int e0 = ((grp % 3) * G + g) * 256 + col;
-                float m1 = Pc1[e0], mm2 = Pc2[e0];
-#pragma unroll
-                for (int w = 1; w < 8; ++w) {
-                    const float o1 = Pc1[e0 + 32 * w], o2 = Pc2[e0 + 32 * w];
-                    const float t2 = vmin(mm2, o2);
-                    mm2 = vmed3(m1, o1, t2);
-                    m1 = vmin(m1, o1);
-                }
-                // no row index stored: featnn_colmerge5 decodes it from m1's
-                // code bits (a third fewer column-partial bytes written and read)
-                const size_t o = cpoff + (size_t)ct * 32 + col;
-                a.cp1[o] = m1;
-                a.cp2[o] = mm2;
-            }
-        }
-    };
-    if (lag) __builtin_amdgcn_s_setprio(1);
-    f32x16 acc[G];
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int grp = 0; grp < ngroups; ++grp) {
-        const int buf = grp & 1;
-        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
-        if (lag) {
-            if (grp > 0) epilogue(acc, grp - 1);
-            chain(buf, acc);
-        } else {
-            chain(buf, acc);
-            epilogue(acc, grp);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (grp >= 1) merge(grp - 1);
-    }
-    if (ngroups > 0) {
-        if (lag) epilogue(acc, ngroups - 1);
-        __syncthreads();
-        merge(ngroups - 1);
-    }
-    if (qt * 32 >= n) return;
-    int i1[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + (l & 31);
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float ob1 = __shfl_xor(b1[r], o, 64);
-            const float ob2 = __shfl_xor(b2[r], o, 64);
-            const int oi1 = __shfl_xor(i1[r], o, 64);
-            top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
-        }
-    }
-    const int lr = l & 31;
-    if (lr >= 16) return;
-    float mb1 = 0.f, mb2 = 0.f;
-    int mi1 = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
-    const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-    if (row >= n) return;
-    if (m == 0) { a.nn12[(size_t)p * a.Nmax + row] = 0; return; }
-    a.nn12[(size_t)p * a.Nmax + row] = mi1;
-    const double Gm = (double)__uint_as_float(a.gmax[p]);
-    const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
-    const double pert = __builtin_ldexp(1.0, a.ctbits - 23) *
-                        (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2));
-    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NCH, a.D) + pert))
-        a.list12[(size_t)p * a.Nmax + atomicAdd(a.count12 + p, 1)] = row;
-}
-
 // ---------------------------------------------------------------------------
 // v7 = v5 with an in-wave software pipeline.  Ablations of v5 showed its
 // phases add: MFMA chain (after its B-fragment LDS reads have landed) and
@@ -1665,6 +802,13 @@ struct RescanArgs5 {
     int Nmax, Mmax, D;
     const int *list12, *list21, *cnt12, *cnt21;
     int32_t *nn12, *nn21;
+    // candidate slices (gridDim.z = S): the first `cap` listed rows of a pair and
+    // direction are scanned by S blocks over disjoint candidate ranges, each
+    // writing its lexicographic (d, j) minimum to slot (p, dir, e, s), merged by
+    // featnn_rescan_merge; rows past `cap` are scanned whole by slice 0
+    int cap;
+    double *sd;
+    int *sj;
 };
 
 template <int DV, bool V4>
@@ -1676,20 +820,29 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
     // broadcast.  Dims in [D, DV) are zero on both sides (exact zero terms).
     constexpr int kChunk = 128, kSt = DV + 4;
     __shared__ __attribute__((aligned(16))) float csb[2][kChunk * kSt];  // double buffer (V4 path)
-    const int dir = blockIdx.y, p = blockIdx.x;
+    const int dir = blockIdx.y, p = blockIdx.x, S = gridDim.z, sid = blockIdx.z;
     const int tid = threadIdx.x, r = tid >> 3, sl = tid & 7;
     const float *Q = dir ? a.G : a.F;
     const float *C = dir ? a.F : a.G;
     const int Nq = dir ? a.Mmax : a.Nmax, Nc = dir ? a.Nmax : a.Mmax;
-    const int nc = count_of(dir ? a.n_src : a.n_tgt, p, Nc);
+    const int ncand = count_of(dir ? a.n_src : a.n_tgt, p, Nc);
     const int *list = (dir ? a.list21 : a.list12) + (size_t)p * Nq;
     const int cnt = (dir ? a.cnt21 : a.cnt12)[p];
-    if (tid == 0 && cnt > 0) atomicAdd(&g_featnn_rescan_rows[dir], (unsigned long long)cnt);
+    if (tid == 0 && sid == 0 && cnt > 0) atomicAdd(&g_featnn_rescan_rows[dir], (unsigned long long)cnt);
     int32_t *nn = (dir ? a.nn21 : a.nn12) + (size_t)p * Nq;
     const int D = a.D;
     const float *cb = C + (size_t)p * Nc * D;
-    for (int b0 = 0; b0 < cnt; b0 += 32) {
-        const bool act = b0 + r < cnt;
+    // this slice's candidates: whole 128-candidate chunks [clo, chi)
+    const int nchunk = (ncand + kChunk - 1) / kChunk;
+    const int clo = S > 1 ? min(ncand, (int)((long long)nchunk * sid / S) * kChunk) : 0;
+    const int chi = S > 1 ? min(ncand, (int)((long long)nchunk * (sid + 1) / S) * kChunk) : ncand;
+    const int ecap = S > 1 ? min(cnt, a.cap) : 0;  // rows handled by the slices
+    // slices take rows [0, ecap); slice 0 also the rows past the cap, whole
+    for (int b0 = 0; b0 < (sid > 0 ? ecap : cnt); b0 += 32) {
+        const bool sliced = b0 < ecap;
+        const int c_lo = sliced ? clo : 0, c_hi = sliced ? chi : ncand;
+        const int bend = sliced ? ecap : cnt;
+        const bool act = b0 + r < bend;
         const int row = act ? list[b0 + r] : 0;
         const float *q = Q + ((size_t)p * Nq + row) * D;
         double qd[DV];
@@ -1707,12 +860,12 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
         // loads are in flight while the current chunk is scanned
         constexpr int kPer = kChunk * (DV / 4) / 256;  // float4 per thread per chunk
         float4 stage[kPer];
-        auto gload = [&](int c0) {
+        auto gload = [&](int c0, int cend) {
 #pragma unroll
             for (int u = 0; u < kPer; ++u) {
                 const int e = tid + 256 * u, i = e / (DV / 4), k = (e - i * (DV / 4)) * 4;
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (c0 + i < nc && k < D)
+                if (c0 + i < cend && k < D)
                     v = *reinterpret_cast<const float4 *>(cb + (size_t)(c0 + i) * D + k);
                 stage[u] = v;
             }
@@ -1764,27 +917,29 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
         };
         if (V4) {
             __syncthreads();  // previous batch done with both buffers
-            gload(0);
-            lstore(csb[0]);
+            if (c_lo < c_hi) {
+                gload(c_lo, c_hi);
+                lstore(csb[0]);
+            }
             __syncthreads();
             int buf = 0;
-            for (int c0 = 0; c0 < nc; c0 += kChunk, buf ^= 1) {
-                const bool more = c0 + kChunk < nc;
-                if (more) gload(c0 + kChunk);
-                scan(csb[buf], c0, min(kChunk, nc - c0));
+            for (int c0 = c_lo; c0 < c_hi; c0 += kChunk, buf ^= 1) {
+                const bool more = c0 + kChunk < c_hi;
+                if (more) gload(c0 + kChunk, c_hi);
+                scan(csb[buf], c0, min(kChunk, c_hi - c0));
                 if (more) lstore(csb[buf ^ 1]);  // read last in the previous iteration
                 __syncthreads();
             }
         } else {
-            for (int c0 = 0; c0 < nc; c0 += kChunk) {
-                const int ncand = min(kChunk, nc - c0);
+            for (int c0 = c_lo; c0 < c_hi; c0 += kChunk) {
+                const int nin = min(kChunk, c_hi - c0);
                 __syncthreads();  // previous chunk fully consumed
                 for (int e = tid; e < kChunk * DV; e += 256) {
                     const int i = e / DV, k = e - i * DV;
-                    csb[0][i * kSt + k] = (i < ncand && k < D) ? cb[(size_t)(c0 + i) * D + k] : 0.0f;
+                    csb[0][i * kSt + k] = (i < nin && k < D) ? cb[(size_t)(c0 + i) * D + k] : 0.0f;
                 }
                 __syncthreads();
-                scan(csb[0], c0, ncand);
+                scan(csb[0], c0, nin);
             }
         }
 #pragma unroll
@@ -1793,7 +948,35 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
             const int oj = __shfl_xor(bj, o, 64);
             if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
         }
-        if (sl == 0 && act) nn[row] = (bj == 0x7fffffff) ? 0 : bj;
+        if (sl == 0 && act) {
+            if (sliced) {
+                const size_t slot = (((size_t)p * 2 + dir) * a.cap + b0 + r) * S + sid;
+                a.sd[slot] = best;
+                a.sj[slot] = bj;
+            } else {
+                nn[row] = (bj == 0x7fffffff) ? 0 : bj;
+            }
+        }
+    }
+}
+
+// lexicographic (d, j) minimum of the S slice results of each sliced row
+__global__ __launch_bounds__(256) void featnn_rescan_merge(RescanArgs5 a, int S) {
+    const int dir = blockIdx.y, p = blockIdx.x;
+    const int Nq = dir ? a.Mmax : a.Nmax;
+    const int cnt = min((dir ? a.cnt21 : a.cnt12)[p], a.cap);
+    const int *list = (dir ? a.list21 : a.list12) + (size_t)p * Nq;
+    int32_t *nn = (dir ? a.nn21 : a.nn12) + (size_t)p * Nq;
+    for (int e = threadIdx.x; e < cnt; e += 256) {
+        const size_t slot = (((size_t)p * 2 + dir) * a.cap + e) * S;
+        double best = a.sd[slot];
+        int bj = a.sj[slot];
+        for (int s = 1; s < S; ++s) {
+            const double d = a.sd[slot + s];
+            const int j = a.sj[slot + s];
+            if (d < best || (d == best && j < bj)) { best = d; bj = j; }
+        }
+        nn[list[e]] = (bj == 0x7fffffff) ? 0 : bj;
     }
 }
 
@@ -1903,14 +1086,6 @@ static int launch_rescans(const float *F, const float *G, int Nmax, int Mmax, in
     return PCR_OK;
 }
 
-// 1: two-pass v1, 2: one-pass v2, 3: v3, 4: pipelined v4, 5: f16x3 split v5,
-// 6: v5 with phase-split wave pairs, 7 (default): v5 software-pipelined in-wave
-// (read per call: a getenv is noise next to a launch, and tests switch modes)
-static int featnn_mode() {
-    const char *e = getenv("PCR_FEATNN_MODE");
-    return (e && e[0] >= '1' && e[0] <= '7') ? e[0] - '0' : 7;
-}
-
 static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
                             const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12,
                             int32_t *nn21, hipStream_t s) {
@@ -1949,16 +1124,7 @@ static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int
     d.cpi = (int *)(d.cp2 + cpn);
     const dim3 g(d.nrb, P);
     prof_begin(s, kProfFeatScreen);
-    if (featnn_mode() == 4) {
-        switch (KCH) {
-#define PCR_D4CASE(K, GG) \
-    case K: hipLaunchKernelGGL((featnn_dual4<K, GG>), g, dim3(512), 0, s, d); break;
-            PCR_D4CASE(1, 4) PCR_D4CASE(2, 4) PCR_D4CASE(3, 4) PCR_D4CASE(4, 4)
-            PCR_D4CASE(5, 2) PCR_D4CASE(6, 2) PCR_D4CASE(7, 2) PCR_D4CASE(8, 2)
-#undef PCR_D4CASE
-            default: set_error("feature dim too large"); return PCR_ERR_ARG;
-        }
-    } else {
+    {
         switch (KCH) {
 #define PCR_D3CASE(K, GG) \
     case K: hipLaunchKernelGGL((featnn_dual3<K, GG>), g, dim3(512), 0, s, d); break;
@@ -1976,13 +1142,11 @@ static int feature_match_v3(const float *F, const float *G, int P, int Nmax, int
     return launch_rescans(F, G, Nmax, Mmax, D, n_src, n_tgt, list, list21, list_count, nn12, nn21, s);
 }
 
-
 static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
                             const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12,
                             int32_t *nn21, hipStream_t s) {
     const int NCH = cdiv(3 * D + 6, 16);
     constexpr int G5 = 4;
-    const int mode = featnn_mode();
     const Split5 sp = split5_params(D);
     const int nrb = cdiv(cdiv(Nmax, 32), 8);
     const int ntn = nrb * 8;                       // row tiles, padded to whole blocks
@@ -2034,38 +1198,25 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     d.ntm = ntm; d.nrb = nrb; d.D = D; d.ctbits = ctbits; d.nn12 = nn12; d.list12 = list12;
     d.count12 = cnt12;
     const size_t cpn = (size_t)P * nrb * ntm * 32;
-    char *cw = (char *)workspace(11, cpn * 12 + 64);
+    char *cw = (char *)workspace(11, cpn * 8 + 64);
     PCR_REQUIRE(cw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     d.cp1 = (float *)cw;
     d.cp2 = d.cp1 + cpn;
-    d.cpi = (int *)(d.cp2 + cpn);
+    d.cpi = nullptr;
     const long long nblk = 8LL * nrb * cdiv(P, 8);  // XCD-aware 1-D grid
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_match: grid too large");
     prof_begin(s, kProfFeatScreen);
-    const bool v6 = mode == 6, v7 = mode == 7;
-    const char *abl = getenv("PCR_FEATNN_ABL");
-    if (abl && NCH == 7 && abl[0] >= '1' && abl[0] <= '3') {  // debug ablations: screen only
-        const dim3 gr((unsigned)nblk), bl(512);
-        if (abl[0] == '1') hipLaunchKernelGGL((featnn_dual5<7, G5, 1>), gr, bl, 0, s, d);
-        if (abl[0] == '2') hipLaunchKernelGGL((featnn_dual5<7, G5, 2>), gr, bl, 0, s, d);
-        if (abl[0] == '3') hipLaunchKernelGGL((featnn_dual5<7, G5, 3>), gr, bl, 0, s, d);
-        PCR_LAUNCH_CHECK();
-        prof_end(s, kProfFeatScreen);
-        return PCR_OK;
-    }
     switch (NCH) {
-#define PCR_D5CASE(K)                                                                             \
-    case K:                                                                                       \
-        if (v7) hipLaunchKernelGGL((featnn_dual7<K, (K <= 7 ? 8 : 4)>), dim3((unsigned)nblk),      \
-                                   dim3(512), 0, s, d);                                           \
-        else if (v6) hipLaunchKernelGGL((featnn_dual6<K, G5>), dim3((unsigned)nblk), dim3(512), 0, s, d); \
-        else hipLaunchKernelGGL((featnn_dual5<K, G5>), dim3((unsigned)nblk), dim3(512), 0, s, d);    \
+#define PCR_D7CASE(K)                                                                        \
+    case K:                                                                                  \
+        hipLaunchKernelGGL((featnn_dual7<K, (K <= 7 ? 8 : 4)>), dim3((unsigned)nblk), dim3(512), \
+                           0, s, d);                                                         \
         break;
-        PCR_D5CASE(1) PCR_D5CASE(2) PCR_D5CASE(3) PCR_D5CASE(4) PCR_D5CASE(5) PCR_D5CASE(6)
-        PCR_D5CASE(7) PCR_D5CASE(8) PCR_D5CASE(9) PCR_D5CASE(10) PCR_D5CASE(11) PCR_D5CASE(12)
-        PCR_D5CASE(13)
-#undef PCR_D5CASE
-        default: set_error("feature dim too large for v5"); return PCR_ERR_ARG;
+        PCR_D7CASE(1) PCR_D7CASE(2) PCR_D7CASE(3) PCR_D7CASE(4) PCR_D7CASE(5) PCR_D7CASE(6)
+        PCR_D7CASE(7) PCR_D7CASE(8) PCR_D7CASE(9) PCR_D7CASE(10) PCR_D7CASE(11) PCR_D7CASE(12)
+        PCR_D7CASE(13)
+#undef PCR_D7CASE
+        default: set_error("feature dim too large for the f16 split screen"); return PCR_ERR_ARG;
     }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfFeatScreen);
@@ -2077,7 +1228,18 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     ra.D = D; ra.list12 = list12; ra.list21 = list21; ra.cnt12 = cnt12; ra.cnt21 = cnt21;
     ra.nn12 = nn12; ra.nn21 = nn21;
     const bool v4 = (D % 4) == 0 && ((uintptr_t)F & 15) == 0 && ((uintptr_t)G & 15) == 0;
-    const dim3 rg(P, 2);
+    // candidate slices per (pair, direction): ~2048 blocks whatever the batch
+    const int S = std::max(1, std::min(16, 1024 / std::max(P, 1)));
+    ra.cap = 256;
+    ra.sd = nullptr;
+    ra.sj = nullptr;
+    if (S > 1) {
+        char *rw = (char *)workspace(6, (sizeof(double) + sizeof(int)) * (size_t)P * 2 * ra.cap * S + 64);
+        PCR_REQUIRE(rw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
+        ra.sd = (double *)rw;
+        ra.sj = (int *)(ra.sd + (size_t)P * 2 * ra.cap * S);
+    }
+    const dim3 rg(P, 2, S);
     prof_begin(s, kProfFeatRescan);
     const int dv = cdiv(D, 16) * 16;
 #define PCR_R3(DVV)                                                                    \
@@ -2088,108 +1250,20 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     PCR_R3(16) PCR_R3(32) PCR_R3(48) PCR_R3(64)
 #undef PCR_R3
     PCR_LAUNCH_CHECK();
-    prof_end(s, kProfFeatRescan);
-    return PCR_OK;
-}
-
-// direction-agnostic exact 1-NN of Q rows among C rows, both packed already
-static int screen_and_rescan(const float *Q, const float *C, const float *Qp, const float *Cp,
-                             const float *ccn, const float *qnrm, const unsigned *cgmax,
-                             const int32_t *nq, const int32_t *nc, int P, int Nqmax, int Ncmax,
-                             int D, int KCH, int32_t *nn, int *list, int *list_count,
-                             hipStream_t s) {
-    ScreenArgs a;
-    a.Qp = Qp; a.Cp = Cp; a.ccn = ccn; a.qnrm = qnrm; a.cgmax = cgmax; a.nq = nq; a.nc = nc;
-    a.Nqmax = Nqmax; a.Ncmax = Ncmax; a.ntq = cdiv(Nqmax, 32); a.ntc = cdiv(Ncmax, 32);
-    a.S2 = 8 * KCH; a.nn = nn; a.list = list; a.list_count = list_count;
-    PCR_HIP_CHECK(hipMemsetAsync(list_count, 0, sizeof(int), s));
-    const dim3 g(cdiv(a.ntq, 4), P);
-    prof_begin(s, kProfFeatScreen);
-    switch (KCH) {
-#define PCR_CASE(K) \
-    case K: hipLaunchKernelGGL(featnn_screen<K>, g, dim3(256), 0, s, a); break;
-        PCR_CASE(1) PCR_CASE(2) PCR_CASE(3) PCR_CASE(4) PCR_CASE(5) PCR_CASE(6) PCR_CASE(7) PCR_CASE(8)
-#undef PCR_CASE
-        default: set_error("feature dim too large"); return PCR_ERR_ARG;
+    if (S > 1) {
+        hipLaunchKernelGGL(featnn_rescan_merge, dim3(P, 2), dim3(256), 0, s, ra, S);
+        PCR_LAUNCH_CHECK();
     }
-    PCR_LAUNCH_CHECK();
-    prof_end(s, kProfFeatScreen);
-    hipLaunchKernelGGL(featnn_rescan, dim3(1024), dim3(256), 0, s, Q, C, Nqmax, Ncmax, D, nc, list,
-                       list_count, nn);
-    PCR_LAUNCH_CHECK();
+    prof_end(s, kProfFeatRescan);
     return PCR_OK;
 }
 
 int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
                        const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12, int32_t *nn21,
                        hipStream_t s) {
-    const int KCH = cdiv(D, 16);
-    PCR_REQUIRE(D >= 1 && KCH <= 8, PCR_ERR_ARG, "feature_match: D=%d unsupported (1..128)", D);
-    if (featnn_mode() >= 5 && D <= 64)
-        return feature_match_v5(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
-    if (featnn_mode() >= 3)
-        return feature_match_v3(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
-    const int S2 = 8 * KCH;
-    const int ntn = cdiv(Nmax, 32), ntm = cdiv(Mmax, 32);
-    const size_t fp_n = (size_t)P * ntn * S2 * 64, fp_m = (size_t)P * ntm * S2 * 64;
-    const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
-    const size_t bytes = 4 * (fp_n + fp_m + 2 * nn_n + 2 * nn_m + 2 * (size_t)P + 2 + (size_t)P * (Nmax + Mmax));
-    char *ws = (char *)workspace(2, bytes + 256);
-    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
-    float *Fp = (float *)ws;
-    float *Gp = Fp + fp_n;
-    float *fcn = Gp + fp_m;
-    float *fnr = fcn + nn_n;
-    float *gcn = fnr + nn_n;
-    float *gnr = gcn + nn_m;
-    unsigned *gmax = (unsigned *)(gnr + nn_m);  // [0..P): max|g| ; [P..2P): max|f|
-    int *list_count = (int *)(gmax + 2 * P);
-    int *list = list_count + 2;
-    PCR_HIP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned) * 2 * P, s));
-    hipLaunchKernelGGL(feat_pack, dim3(ntn, P), dim3(64), 0, s, F, n_src, Nmax, D, S2, ntn, Fp, fcn,
-                       fnr, gmax + P);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(feat_pack, dim3(ntm, P), dim3(64), 0, s, G, n_tgt, Mmax, D, S2, ntm, Gp, gcn,
-                       gnr, gmax);
-    PCR_LAUNCH_CHECK();
-    if (featnn_mode() == 1) {
-        int rc = screen_and_rescan(F, G, Fp, Gp, gcn, fnr, gmax, n_src, n_tgt, P, Nmax, Mmax, D,
-                                   KCH, nn12, list, list_count, s);
-        if (rc != PCR_OK) return rc;
-        return screen_and_rescan(G, F, Gp, Fp, fcn, gnr, gmax + P, n_tgt, n_src, P, Mmax, Nmax, D,
-                                 KCH, nn21, list, list_count + 1, s);
-    }
-    // one pass, both directions
-    DualArgs d;
-    d.Fp = Fp; d.Gp = Gp; d.fcn = fcn; d.gcn = gcn; d.fnr = fnr; d.gnr = gnr;
-    d.fmax = gmax + P; d.gmax = gmax; d.n_src = n_src; d.n_tgt = n_tgt;
-    d.Nmax = Nmax; d.Mmax = Mmax; d.ntn = ntn; d.ntm = ntm; d.nrb = cdiv(ntn, 8);
-    d.nn12 = nn12;
-    int *list21 = list + (size_t)P * Nmax;
-    d.list12 = list; d.count12 = list_count;
-    const size_t cpn = (size_t)P * d.nrb * ntm * 32;
-    char *cw = (char *)workspace(11, cpn * 12 + 64);
-    PCR_REQUIRE(cw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
-    d.cp1 = (float *)cw;
-    d.cp2 = d.cp1 + cpn;
-    d.cpi = (int *)(d.cp2 + cpn);
-    PCR_HIP_CHECK(hipMemsetAsync(list_count, 0, 2 * sizeof(int), s));
-    const dim3 g(d.nrb, P);
-    prof_begin(s, kProfFeatScreen);
-    switch (KCH) {
-#define PCR_DCASE(K, GG) \
-    case K: hipLaunchKernelGGL((featnn_dual<K, GG>), g, dim3(512), 0, s, d); break;
-        PCR_DCASE(1, 4) PCR_DCASE(2, 3) PCR_DCASE(3, 2) PCR_DCASE(4, 2)
-        PCR_DCASE(5, 1) PCR_DCASE(6, 1) PCR_DCASE(7, 1) PCR_DCASE(8, 1)
-#undef PCR_DCASE
-        default: set_error("feature dim too large"); return PCR_ERR_ARG;
-    }
-    PCR_LAUNCH_CHECK();
-    prof_end(s, kProfFeatScreen);
-    hipLaunchKernelGGL(featnn_colmerge, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, list21,
-                       list_count + 1, S2);
-    PCR_LAUNCH_CHECK();
-    return launch_rescans(F, G, Nmax, Mmax, D, n_src, n_tgt, list, list21, list_count, nn12, nn21, s);
+    PCR_REQUIRE(D >= 1 && D <= 128, PCR_ERR_ARG, "feature_match: D=%d unsupported (1..128)", D);
+    if (D <= 64) return feature_match_v5(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
+    return feature_match_v3(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
 }
 
 int corres_impl(const int32_t *nn12, const int32_t *nn21, const int32_t *n_src,

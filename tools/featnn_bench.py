@@ -1,7 +1,7 @@
 """Feature-NN (a5) microbenchmark: P pairs of N x D descriptors built like
 synth.make_pair's (shared code pool + Gaussian noise), generated on the GPU.
 Prints one JSON line with per-kernel times (library event profiler) and the
-number of rows sent to the exact rescan.  PCR_FEATNN_MODE selects the kernel."""
+number of rows sent to the exact rescan."""
 import argparse
 import json
 import os
@@ -49,7 +49,7 @@ def main():
              ("pack", _lib.PROF_FEAT_PACK))}
     rows = _lib.featnn_rescan_rows(reset=True)
     flops = 2.0 * a.pairs * a.n * a.n * a.d
-    print(json.dumps({"mode": os.environ.get("PCR_FEATNN_MODE", "default"), "pairs": a.pairs,
+    print(json.dumps({"pairs": a.pairs,
                       "n": a.n, "d": a.d, "ms_total": ev0.elapsed_time(ev1) / a.iters,
                       "ms": prof, "screen_alg_tflops": flops / prof["screen"] / 1e9,
                       "rescan_rows": [r / a.iters for r in rows]}))

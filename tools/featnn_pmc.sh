@@ -1,15 +1,15 @@
 #!/usr/bin/env bash
 # PMC passes over the feature-NN microbenchmark (separate --pmc runs, kernel
-# trace only).  Usage on the GPU box: bash tools/featnn_pmc.sh MODE [PAIRS]
+# trace only).  Usage on the GPU box: bash tools/featnn_pmc.sh [PAIRS]
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-M=${1:-7}; P=${2:-64}
-OUT=gpurun_out/pmc_m$M
+P=${1:-64}
+OUT=gpurun_out/pmc_featnn
 mkdir -p "$OUT"
 run() {  # name counters...
   local name=$1; shift
-  PCR_FEATNN_MODE=$M timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run \
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run \
     --output-format csv -- python3 tools/featnn_bench.py --pairs "$P" --iters 2 > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
