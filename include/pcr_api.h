@@ -295,6 +295,45 @@ int pcr_radius_neighbors(const float *queries, int32_t nq, const float *supports
                          pcr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * a5 (ii) -- the level voting of c2p-net/ngenet/models/vote.py:12-37 (after the
+ * h / m / l feature-space 1-NN of get_coor_points, :6-9, on pcr_feature_match).
+ *   tgt_xyz (m,3) f32, nn_h / nn_m / nn_l (n) i32 (source -> target at each
+ *   level), feature rows (n,D) / (m,D) f32, all device.  For every source i:
+ *   d12, d13, d23 = f32 Euclidean distances between its three targets (numpy's
+ *   order, correctly rounded sqrt); sel_h = d12 < thr or d13 < thr, sel_m = d23
+ *   < thr with thr = (float)(2 voxel_size); where !sel_h and sel_m the h rows
+ *   are replaced in place: src_feat_h[i] <- src_feat_m[i] and
+ *   tgt_feat_h[nn_m[i]] <- tgt_feat_m[nn_m[i]].  replaced (n) u8 optional.
+ *   Asynchronous on `stream`.
+ * ------------------------------------------------------------------------- */
+int pcr_vote_apply(const float *tgt_xyz, int32_t m, const int32_t *nn_h, const int32_t *nn_m,
+                   const int32_t *nn_l, int32_t n, double voxel_size, float *src_feat_h,
+                   const float *src_feat_m, float *tgt_feat_h, const float *tgt_feat_m, int32_t D,
+                   uint8_t *replaced, pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * f2 -- Open3D voxel down-sampling (dip/demo.py:73-74 pcd.voxel_down_sample,
+ * Open3D 0.13 PointCloud::VoxelDownSample; oracle/voxel_oracle.cpp restates it).
+ *   points (n,3) f64 device, optional normals / colors (n,3) f64 device (NULL:
+ *   none); cloud_len (nb) HOST (lengths summing to <= n).  Per cloud: voxel
+ *   min bound = min - voxel_size/2, voxel = int(floor((p - bound)/voxel_size)),
+ *   per voxel the f64 sums in input order (normals with a NaN component
+ *   skipped) divided by double(count), emitted in the iteration order of
+ *   Open3D's unordered_map<Vector3i, ..., hash_eigen> (replayed on the host).
+ *   Writes out_points / out_normals / out_colors (capacity n*3 each, device),
+ *   out_cloud_len (HOST, nb) and *out_total (HOST).  Synchronous.  Errors as
+ *   the reference: voxel_size <= 0, "voxel_size is too small"; non-finite
+ *   coordinates -> PCR_ERR_ARG.
+ * pcr_voxel3i_map_order: host-only helper behind it -- iteration order of that
+ *   map after inserting the n distinct (x, y, z) int keys in order.
+ * ------------------------------------------------------------------------- */
+int pcr_voxel_down_sample(const double *points, int32_t n, const int32_t *cloud_len, int32_t nb,
+                          double voxel_size, const double *normals, const double *colors,
+                          double *out_points, double *out_normals, double *out_colors,
+                          int32_t *out_cloud_len, int32_t *out_total, pcr_stream_t stream);
+int pcr_voxel3i_map_order(const int32_t *xyz, int32_t n, int32_t *order);
+
+/* ---------------------------------------------------------------------------
  * f1 -- normal estimation and FPFH, the preprocessing of
  * DataPreparation/RANSAC.py:12-22 (Open3D 0.13 PointCloud::estimate_normals
  * with KDTreeSearchParamHybrid(4 voxel, 30) and

@@ -93,6 +93,9 @@ def _setup_sigs():
     L.oracle_corres.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
     L.oracle_philox.argtypes = [c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     L.oracle_horn_rotation.argtypes = [c.c_void_p, c.c_void_p]
+    L.oracle_voxel_down_sample.restype = c.c_int
+    L.oracle_voxel_down_sample.argtypes = [c.c_void_p, c.c_int, c.c_double, c.c_void_p, c.c_void_p,
+                                           c.c_void_p, c.c_void_p, c.c_void_p]
     L.oracle_xs_sum.restype = c.c_double
     L.oracle_xs_sum.argtypes = [c.c_void_p, c.c_int]
     L.oracle_lrf_count.restype = c.c_int
@@ -127,6 +130,24 @@ def philox(seed, pair, itr, block=0):
     return out
 
 
+def voxel_down_sample(points, voxel_size, normals=None, colors=None):
+    """Open3D PointCloud::VoxelDownSample restated (oracle/voxel_oracle.cpp):
+    (points, normals or None, colors or None) in the map's iteration order."""
+    p = _f64(points).reshape(-1, 3)
+    n = p.shape[0]
+    nr = None if normals is None else _f64(normals).reshape(-1, 3)
+    cl = None if colors is None else _f64(colors).reshape(-1, 3)
+    op = np.zeros((max(n, 1), 3))
+    on = np.zeros((max(n, 1), 3)) if nr is not None else None
+    oc = np.zeros((max(n, 1), 3)) if cl is not None else None
+    k = L().oracle_voxel_down_sample(_p(p), n, float(voxel_size), _p(nr) if nr is not None else None,
+                                     _p(cl) if cl is not None else None, _p(op),
+                                     _p(on) if on is not None else None, _p(oc) if oc is not None else None)
+    if k < 0:
+        raise ValueError("voxel_down_sample: voxel_size <= 0 or too small")
+    return op[:k].copy(), (on[:k].copy() if on is not None else None), (oc[:k].copy() if oc is not None else None)
+
+
 def xs_sum(v):
     """Exact fixed-point sum of f64 terms rounded once (the ICP Umeyama sums)."""
     v = _f64(v).reshape(-1)
@@ -155,6 +176,31 @@ def featnn(F, G):
     nn = np.zeros(F.shape[0], np.int32)
     L().oracle_featnn(_p(F), _p(G), F.shape[0], G.shape[0], F.shape[1], _p(nn))
     return nn
+
+
+def vote(source, target, source_feats, target_feats, voxel_size):
+    """c2p-net/ngenet/models/vote.py:12-37 restated: the three nearest-target
+    searches by the exact 1-NN (featnn; get_coor_points :6-9), then the f32
+    distance tests and the in-place h-row replacement.  Returns
+    [source, target, fs_h, ft_h] like the reference (fs_h / ft_h are copies
+    here) and the replaced mask."""
+    tgt = np.asarray(target, np.float32)
+    fs = [np.array(f, np.float32) for f in source_feats]
+    ft = [np.array(f, np.float32) for f in target_feats]
+    i1, i2, i3 = (featnn(a, b) for a, b in zip(fs, ft))
+    y1, y2, y3 = tgt[i1], tgt[i2], tgt[i3]
+
+    def dist(a, b):
+        d = a - b
+        return np.sqrt((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
+
+    thr = np.float32(voxel_size * 2)
+    sel_h = (dist(y1, y2) < thr) | (dist(y1, y3) < thr)
+    sel_m = dist(y2, y3) < thr
+    rep = ~sel_h & sel_m
+    fs[0][rep] = fs[1][rep]
+    ft[0][i2[rep]] = ft[1][i2[rep]]
+    return [source, target, fs[0], ft[0]], rep
 
 
 def corres(nn12, nn21, mutual=True, ransac_n=3):

@@ -68,6 +68,9 @@ SIGNATURES = {
     "pcr_ndp_warp": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
     "pcr_grid_subsample": [_p, _i32, _p, _i32, _p, _i32, _f32, _i32, _p, _p, _p, _p, _p],
     "pcr_voxel_map_order": [_p, _i32, _p],
+    "pcr_voxel_down_sample": [_p, _i32, _p, _i32, _f64, _p, _p, _p, _p, _p, _p, _p, _p],
+    "pcr_voxel3i_map_order": [_p, _i32, _p],
+    "pcr_vote_apply": [_p, _i32, _p, _p, _p, _i32, _f64, _p, _p, _p, _p, _i32, _p, _p],
     "pcr_radius_count": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _p, _p, _p],
     "pcr_radius_neighbors": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _i32, _p, _p, _p],
     "pcr_transform_batch": [_p, _i32, _i32, _p, _p, _p],

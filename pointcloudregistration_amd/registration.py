@@ -272,10 +272,44 @@ def radius_nn(tgt, queries, r, n_tgt=None, n_q=None):
 
 
 class PointCloud:
-    """Minimal stand-in for o3d.geometry.PointCloud: ``.points`` (N, 3)."""
+    """Minimal stand-in for o3d.geometry.PointCloud: ``.points`` (N, 3), optional
+    ``.normals`` / ``.colors``, and the methods the reference's hot-path callers
+    use (voxel_down_sample, transform, paint_uniform_color)."""
 
     def __init__(self, points=None):
         self.points = np.zeros((0, 3)) if points is None else points
+        self.normals = None
+        self.colors = None
+
+    def has_normals(self):
+        return self.normals is not None and len(self.normals) > 0
+
+    def has_colors(self):
+        return self.colors is not None and len(self.colors) > 0
+
+    def paint_uniform_color(self, color):
+        self.colors = np.tile(np.asarray(color, np.float64).reshape(1, 3), (len(self.points), 1))
+        return self
+
+    def voxel_down_sample(self, voxel_size):
+        """o3d PointCloud.voxel_down_sample on the GPU (geometry.voxel_down_sample)."""
+        from .geometry import voxel_down_sample
+        return voxel_down_sample(self, voxel_size)
+
+    def transform(self, T):
+        """In place, like Open3D's Transform: p <- ((T00 x + T01 y) + T02 z) + T03
+        per row in f64 (the order every kernel of this library uses), normals
+        rotated."""
+        T = np.asarray(T, np.float64)
+        p = np.asarray(self.points, np.float64).reshape(-1, 3)
+        x, y, z = p[:, 0], p[:, 1], p[:, 2]
+        self.points = np.stack([((T[r, 0] * x + T[r, 1] * y) + T[r, 2] * z) + T[r, 3]
+                                for r in range(3)], axis=1)
+        if self.has_normals():
+            q = np.asarray(self.normals, np.float64).reshape(-1, 3)
+            a, b, c = q[:, 0], q[:, 1], q[:, 2]
+            self.normals = np.stack([(T[r, 0] * a + T[r, 1] * b) + T[r, 2] * c for r in range(3)], axis=1)
+        return self
 
 
 class Feature:

@@ -6,6 +6,7 @@ reference's outputs); the reference itself never travels.
   rigid_fit        c2p-net/deformationpyramid/model/geometry.py:8-34
   Error_R/Error_t  ROPNet/src/metrics/metrics.py:6-33
   get_coor_points  c2p-net/ngenet/models/vote.py:6-9
+  vote             c2p-net/ngenet/models/vote.py:12-37
   lrf.get          dip/lrf.py:19-78
   NDP warp         c2p-net/deformationpyramid/model/nets.py:10-177 (small config)
 
@@ -104,6 +105,40 @@ def vote_cases():
         tgt = rng.random((m, 3)).astype(np.float32)
         _, inds = get_coor_points(fs, ft, tgt, False)
         out[f"vote/{name}/fs"], out[f"vote/{name}/ft"], out[f"vote/{name}/inds"] = fs, ft, inds
+    out.update(vote_full_case())
+    return out
+
+
+def vote_full_case():
+    """vote() itself on a case built so that every branch occurs: targets with
+    near twins (distinct indices closer than 2 voxel), sources whose m / l
+    levels agree on a target while h points elsewhere (replaced), h agreeing
+    too (kept), and sources with three unrelated levels."""
+    from ngenet.models.vote import vote
+    rng = np.random.default_rng(19)
+    n, m, d, voxel = 300, 350, 16, 0.025
+    tgt = rng.random((m, 3)).astype(np.float32)
+    tgt[300:] = tgt[:50] + rng.uniform(-0.02, 0.02, (50, 3)).astype(np.float32)
+    ft = [rng.standard_normal((m, d)).astype(np.float32) for _ in range(3)]
+    t_of = rng.integers(0, m, n)
+    t_twin = np.where(t_of < 50, t_of + 300, t_of)
+    kind = rng.integers(0, 4, n)  # 0 all agree, 1 h off, 2 all off, 3 l on the twin
+    fs = [rng.standard_normal((n, d)).astype(np.float32) for _ in range(3)]
+    for lvl in range(3):
+        for i in range(n):
+            k = kind[i]
+            j = t_of[i]
+            if k == 2 or (k == 1 and lvl == 0):
+                continue
+            if k == 3 and lvl == 2:
+                j = t_twin[i]
+            fs[lvl][i] = ft[lvl][j] + np.float32(0.05) * rng.standard_normal(d).astype(np.float32)
+    src = rng.random((n, 3)).astype(np.float32)
+    out = {"vote/full/src": src, "vote/full/tgt": tgt, "vote/full/voxel": np.array(voxel)}
+    for lvl, nm in enumerate("hml"):
+        out[f"vote/full/fs_{nm}"], out[f"vote/full/ft_{nm}"] = fs[lvl].copy(), ft[lvl].copy()
+    res = vote(src.copy(), tgt.copy(), [f.copy() for f in fs], [f.copy() for f in ft], voxel, False)
+    out["vote/full/fs_h_out"], out["vote/full/ft_h_out"] = res[2], res[3]
     return out
 
 

@@ -1,0 +1,158 @@
+"""GPU parity of C2P-Net's level voting (a5 ii, c2p-net/ngenet/models/vote.py:6-37)
+and of the composed C5 flow (testScript.py:161-196: vote -> feature RANSAC ->
+estimate -> NDP on the unique inlier sources).
+
+Bar: bit-exact against the reference's own vote() outputs (tests/golden/
+vote_golden.npz, made by make_golden_py.py importing the reference) and against
+the oracle restatement on larger cases; the composed flow's RANSAC transform,
+inlier sources and NDP input bit-exact against the oracle chain."""
+import numpy as np
+import pytest
+import torch
+
+from pointcloudregistration_amd import c2p, synth
+from pointcloudregistration_amd.ndp_opt import NDPConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "vote_golden.npz"))
+
+
+def test_get_coor_points_vs_reference_golden():
+    g = _golden()
+    for name in ("h32", "d8"):
+        fs, ft = g[f"vote/{name}/fs"], g[f"vote/{name}/ft"]
+        tgt = np.random.default_rng(1).random((ft.shape[0], 3)).astype(np.float32)
+        y, inds = c2p.get_coor_points(fs, ft, tgt)
+        assert np.array_equal(inds, g[f"vote/{name}/inds"])
+        assert np.array_equal(y, tgt[inds])
+
+
+def test_vote_vs_reference_golden_in_place():
+    """numpy inputs: the h rows are replaced in place and returned, like the
+    reference's fancy assignment."""
+    g = _golden()
+    fs = [g[f"vote/full/fs_{c}"].copy() for c in "hml"]
+    ft = [g[f"vote/full/ft_{c}"].copy() for c in "hml"]
+    src, tgt = g["vote/full/src"], g["vote/full/tgt"]
+    out, rep = c2p.vote(src, tgt, fs, ft, float(g["vote/full/voxel"]), return_mask=True)
+    assert out[0] is src and out[1] is tgt and out[2] is fs[0] and out[3] is ft[0]
+    assert np.array_equal(fs[0], g["vote/full/fs_h_out"])
+    assert np.array_equal(ft[0], g["vote/full/ft_h_out"])
+    assert int(rep.sum()) > 20  # the case exercises the replacement branch
+
+
+def _levels(rng, n, m, d, share=0.7):
+    """three feature levels with partial agreement (some m/l pairs point at the
+    same target, h at another)"""
+    tgt = rng.random((m, 3)).astype(np.float32)
+    ft = [rng.standard_normal((m, d)).astype(np.float32) for _ in range(3)]
+    fs = [rng.standard_normal((n, d)).astype(np.float32) for _ in range(3)]
+    t_of = rng.integers(0, m, n)
+    agree = rng.random((3, n)) < share
+    for lvl in range(3):
+        i = np.nonzero(agree[lvl])[0]
+        fs[lvl][i] = ft[lvl][t_of[i]] + np.float32(0.1) * rng.standard_normal((len(i), d)).astype(np.float32)
+    return tgt, fs, ft
+
+
+@pytest.mark.parametrize("n,m,d", [(5000, 6000, 32), (1234, 999, 16), (64, 3000, 33)])
+def test_vote_tensors_vs_oracle(oracle, n, m, d):
+    rng = np.random.default_rng(n + d)
+    tgt, fs, ft = _levels(rng, n, m, d)
+    voxel = 0.03
+    exp, rep_exp = oracle.vote(None, tgt, fs, ft, voxel)
+    dev = torch.device("cuda")
+    S = [torch.from_numpy(f).to(dev) for f in fs]
+    T = [torch.from_numpy(f).to(dev) for f in ft]
+    out, rep = c2p.vote(None, torch.from_numpy(tgt).to(dev), S, T, voxel, return_mask=True)
+    assert out[2] is S[0] and out[3] is T[0]  # device tensors updated in place
+    assert np.array_equal(rep.cpu().numpy(), rep_exp)
+    assert np.array_equal(S[0].cpu().numpy(), exp[2])
+    assert np.array_equal(T[0].cpu().numpy(), exp[3])
+
+
+def test_vote_mixed_level_dims(oracle):
+    """the l level may have its own width (separate screens, no batching)"""
+    rng = np.random.default_rng(3)
+    tgt, fs, ft = _levels(rng, 800, 900, 24)
+    fs[2], ft[2] = fs[2][:, :8].copy(), ft[2][:, :8].copy()
+    exp, rep_exp = oracle.vote(None, tgt, fs, ft, 0.05)
+    out, rep = c2p.vote(None, tgt, [f.copy() for f in fs], [f.copy() for f in ft], 0.05,
+                        return_mask=True)
+    assert np.array_equal(rep.cpu().numpy(), rep_exp)
+    assert np.array_equal(out[2], exp[2]) and np.array_equal(out[3], exp[3])
+
+
+def test_vote_rejects_bad_shapes():
+    rng = np.random.default_rng(0)
+    tgt, fs, ft = _levels(rng, 50, 60, 8)
+    with pytest.raises(ValueError):
+        c2p.vote(None, tgt, fs[:2], ft, 0.05)
+    with pytest.raises(ValueError):
+        c2p.vote(None, tgt[:10], fs, ft, 0.05)
+    fs[1] = fs[1][:, :4].copy()
+    with pytest.raises(ValueError):
+        c2p.vote(None, tgt, fs, ft, 0.05)
+
+
+def _c5_case(seed, n=3000):
+    B = synth.make_batch(1, n=n, m=n, d=32, base_seed=seed)
+    rng = np.random.default_rng(seed)
+    fs = [B.src_feat[0]] + [(B.src_feat[0] + rng.normal(0, 0.6, B.src_feat[0].shape)).astype(np.float32)
+                            for _ in range(2)]
+    ft = [B.tgt_feat[0]] + [(B.tgt_feat[0] + rng.normal(0, 0.6, B.tgt_feat[0].shape)).astype(np.float32)
+                            for _ in range(2)]
+    return B, fs, ft
+
+
+def _oracle_chain(oracle, src, tgt, fs, ft, voxel, seed, pair_id):
+    out, _ = oracle.vote(src, tgt, fs, ft, voxel)
+    fs_h, ft_h = out[2], out[3]
+    co = oracle.corres(oracle.featnn(fs_h, ft_h), oracle.featnn(ft_h, fs_h), True, 3)
+    r = oracle.ransac(src, tgt, co, voxel, dist_check=voxel, seed=seed, pair_id=pair_id)
+    T = r["T"]
+    p = src.astype(np.float64)
+    est = np.stack([((T[k, 0] * p[:, 0] + T[k, 1] * p[:, 1]) + T[k, 2] * p[:, 2]) + T[k, 3]
+                    for k in range(3)], axis=1).astype(np.float32)
+    return r, est
+
+
+def test_c5_composed_flow_vs_oracle_chain(oracle):
+    B, fs, ft = _c5_case(41)
+    voxel = 0.04
+    cfg = NDPConfig(iters=15, m=3, width=32)
+    torch.manual_seed(0)
+    res = c2p.register_c2p(B.src[0], B.tgt[0], fs, ft, voxel, ndp_config=cfg, seed=9, pair_id=4)
+    r, est = _oracle_chain(oracle, B.src[0], B.tgt[0], fs, ft, voxel, 9, 4)
+    assert res["T"].cpu().numpy().tobytes() == r["T"].tobytes()
+    assert np.array_equal(res["corrs"].cpu().numpy(), np.unique(r["correspondence_set"][:, 0]))
+    assert res["estimate"].cpu().numpy().tobytes() == est.tobytes()
+    rre, rte = synth.rre_rte(r["T"][:3, :3], r["T"][:3, 3], B.R[0], B.t[0])
+    assert rre < 5.0 and rte < 0.1
+    w = res["warped"]
+    assert w.shape == (B.src.shape[1], 3) and bool(torch.isfinite(w).all())
+    # the NDP stage ran on that subset and lowered its own (truncated Chamfer) loss
+    losses = res["info"][0]["losses"]
+    assert len(losses) > 1 and losses[-1] < losses[0]
+
+
+def test_c5_numpy_dropin_flow(oracle):
+    """the reference's own call sequence on numpy: vote (in place) ->
+    execute_global_registration -> np.unique of the correspondence sources"""
+    B, fs, ft = _c5_case(43, n=2000)
+    voxel = 0.04
+    src, tgt = B.src[0].copy(), B.tgt[0].copy()
+    fsc, ftc = [f.copy() for f in fs], [f.copy() for f in ft]
+    src_o, tgt_o, fs_h, ft_h = c2p.vote(src, tgt, fsc, ftc, voxel)
+    T, estimate, result = c2p.execute_global_registration(
+        c2p.PointCloud(src_o), c2p.PointCloud(tgt_o), c2p.Feature(fs_h.T), c2p.Feature(ft_h.T),
+        voxel, seed=5)
+    corrs = np.unique(np.asarray(result.correspondence_set).T[0])
+    r, est = _oracle_chain(oracle, B.src[0], B.tgt[0], fs, ft, voxel, 5, 0)
+    assert T.tobytes() == r["T"].tobytes()
+    assert np.array_equal(corrs, np.unique(r["correspondence_set"][:, 0]))
+    assert np.asarray(estimate.points).astype(np.float32).tobytes() == est.tobytes()

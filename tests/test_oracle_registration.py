@@ -40,6 +40,18 @@ def test_rre_rte_matches_reference_metrics(gp):
     np.testing.assert_allclose(rte, gp["metrics/err_t"], rtol=1e-12, atol=1e-12)
 
 
+def test_oracle_vote_matches_reference_vote(oracle):
+    """the full vote() (vote.py:12-37) restated: h rows replaced exactly where
+    the reference replaced them"""
+    g = np.load(os.path.join(GOLD, "vote_golden.npz"))
+    out, rep = oracle.vote(g["vote/full/src"], g["vote/full/tgt"],
+                           [g[f"vote/full/fs_{c}"] for c in "hml"],
+                           [g[f"vote/full/ft_{c}"] for c in "hml"], float(g["vote/full/voxel"]))
+    assert np.array_equal(out[2], g["vote/full/fs_h_out"])
+    assert np.array_equal(out[3], g["vote/full/ft_h_out"])
+    assert rep.sum() > 20
+
+
 def test_oracle_featnn_matches_reference_vote(oracle):
     g = np.load(os.path.join(GOLD, "vote_golden.npz"))
     for name in ("h32", "d8"):
@@ -126,3 +138,15 @@ def test_xs_sum_exact_and_order_independent(oracle):
     # ties round to even (f64 spacing at 2^46 is 2^-6; the format holds |sum| < 2^47)
     assert oracle.xs_sum(np.array([2.0 ** 46, 2.0 ** -7])) == 2.0 ** 46
     assert oracle.xs_sum(np.array([2.0 ** 46, 3 * 2.0 ** -7])) == 2.0 ** 46 + 2.0 ** -5
+
+
+def test_oracle_voxel_down_sample_known_answer(oracle):
+    """Two voxels, hand-computed means; voxel_size <= 0 is an error (Open3D's
+    '[VoxelDownSample] voxel_size <= 0.')."""
+    pts = np.array([[0.0, 0.0, 0.0], [0.2, 0.0, 0.0], [1.0, 1.0, 1.0], [0.1, 0.1, 0.1]])
+    out, _, _ = oracle.voxel_down_sample(pts, 0.5)
+    got = out[np.argsort(out[:, 0])]
+    assert got.shape == (2, 3)
+    assert np.allclose(got, [[0.1, 1.0 / 30.0, 1.0 / 30.0], [1.0, 1.0, 1.0]], rtol=0, atol=1e-15)
+    with pytest.raises(ValueError):
+        oracle.voxel_down_sample(pts, 0.0)
