@@ -14,7 +14,7 @@ itself when --gpus N > 1 is given without a launcher -- barrier + synchronize
 around the timed loop, max over ranks; value = all pairs of the job / that time.
 Beside it: the PCIe-inclusive rate (host-resident inputs, `host_resident`), weak
 scaling at N > 1 (P pairs on every rank), the pair-parallel CPU baseline and the
-C2 / a4 / a10 / f1 / f4 side measurements at N = 1.
+C2 / a4 / a10 / f1 / f2 / f4 / C5 side measurements at N = 1.
 """
 from __future__ import annotations
 
@@ -190,10 +190,19 @@ def measure_lrf(with_cpu):
     _lib.call("pcr_lrf_count", _lib.ptr(P_), 2, 20000, None, _lib.ptr(Q_), 2048, None, ker,
               _lib.ptr(counts), st)
     cnt = counts.cpu().numpy()
+    # the draws in demo.py's order (frag1 i, frag2 i, ...): libpcr's restatement
+    # of legacy RandomState.choice (the product path) and numpy's own loop
+    np.random.seed(3)
     t0 = time.perf_counter()
-    inds = np.stack([np.stack([np.random.choice(max(int(c), ps), ps, replace=False)
-                               for c in cnt[p]]) for p in range(2)]).astype(np.int32)
+    inds = L.legacy_choice_batch(np.maximum(cnt.T.reshape(-1), ps), ps)
     host_ms = (time.perf_counter() - t0) * 1e3
+    inds = np.ascontiguousarray(inds.reshape(2048, 2, ps).transpose(1, 0, 2))
+    np.random.seed(3)
+    t0 = time.perf_counter()
+    ref = np.stack([np.random.choice(max(int(cnt[p, i]), ps), ps, replace=False)
+                    for i in range(2048) for p in range(2)])
+    numpy_ms = (time.perf_counter() - t0) * 1e3
+    draws_equal = bool(np.array_equal(ref.reshape(2048, 2, ps).transpose(1, 0, 2), inds))
     I_ = torch.as_tensor(inds, device="cuda").contiguous()
     patches = torch.empty(2, 2048, ps, 3, dtype=torch.float64, device="cuda")
     T = torch.empty(2, 2048, 16, dtype=torch.float64, device="cuda")
@@ -209,6 +218,7 @@ def measure_lrf(with_cpu):
     flops = 4096 * 2 * 20000 * 8.0
     res = {"workload": "C3 DIP: 2 clouds x 20000 pts, 2 x 2048 queries, kernel 3*sqrt(3), patch 256",
            "gpu_ms": ms, "queries_per_s": 4096 / (ms * 1e-3), "host_choice_ms": host_ms,
+           "host_choice_numpy_loop_ms": numpy_ms, "host_choice_equal_to_numpy": draws_equal,
            "median_neighbours": float(np.median(cnt)),
            "roofline": {"bound": "valu-f64", "achieved_tflops": flops / (ms * 1e-3) / 1e12,
                         "peak_tflops": 78.6, "note": "brute-force f64 sweeps; cloud is L2-resident"}}
@@ -425,6 +435,97 @@ def measure_ndp_opt(with_cpu):
                                "cores": torch.get_num_threads(), "kind": "port",
                                "sample": f"{reps} iterations of one level on the CPU (torch, cdist "
                                          "Chamfer), x 360"}
+    return res
+
+
+def measure_c5(with_cpu):
+    """C5 end to end (c2p-net/testScript.py:161-196) on one 20k-point pair:
+    vote over three 32-d feature levels -> mutual feature RANSAC at d = 0.025 ->
+    estimate -> NDP 9 levels x 40 iterations (width 128, early stop disabled so
+    every run does the same work) on the unique inlier sources; wall clock per
+    stage, inputs resident on the device."""
+    from pointcloudregistration_amd import c2p, ndp_opt, registration as reg, synth
+    B = synth.make_batch(1, n=20000, m=20000, d=32, base_seed=515)
+    rng = np.random.default_rng(5)
+
+    def lv(f):
+        return [f] + [(f + rng.normal(0, 0.6, f.shape)).astype(np.float32) for _ in range(2)]
+    fs, ft = lv(B.src_feat[0]), lv(B.tgt_feat[0])
+    dev = torch.device("cuda")
+    S, G = torch.from_numpy(B.src[0]).to(dev), torch.from_numpy(B.tgt[0]).to(dev)
+    FS = [torch.from_numpy(f).to(dev) for f in fs]
+    FT = [torch.from_numpy(f).to(dev) for f in ft]
+    cfg = ndp_opt.NDPConfig(max_break_count=10**6)
+    voxel = 0.025
+
+    def run():
+        a, b = [f.clone() for f in FS], [f.clone() for f in FT]
+        torch.cuda.synchronize()
+        t = [time.perf_counter()]
+        _, _, fs_h, ft_h = c2p.vote(S, G, a, b, voxel)
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        prm = reg.RansacParams(max_correspondence_distance=voxel, distance_check=voxel, seed=1)
+        br = reg.register_feature_ransac_batch(S, G, fs_h, ft_h, prm, want_mask=False)
+        est = reg.transform_batch(S.unsqueeze(0), br.transformation)[0]
+        corrs = torch.nonzero(br.corr_tgt[0] >= 0).flatten().cpu().numpy()
+        t.append(time.perf_counter())
+        torch.manual_seed(0)
+        P = ndp_opt.DeformationPyramid(3, 128, dev, -8, 9, True)
+        w, _, _, info = ndp_opt.optimize_deformation_pyramid(est, G, corrs, cfg, NDP=P)
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        return np.diff(t) * 1e3, br, len(corrs)
+    run()
+    ms, br, k = run()
+    T = br.transformation[0].cpu().numpy()
+    rre, rte = synth.rre_rte(T[:3, :3], T[:3, 3], B.R[0], B.t[0])
+    res = {"workload": "C5 flow: one 20000-pt pair, vote (3 x 32-d levels) -> feature RANSAC "
+                       "d=0.025 -> NDP 9 x 40 on the inlier sources, wall clock",
+           "ms": float(ms.sum()), "vote_ms": float(ms[0]), "ransac_ms": float(ms[1]),
+           "ndp_ms": float(ms[2]), "inlier_sources": int(k), "rre_deg": float(rre),
+           "rte": float(rte)}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        rows = 500
+        t0 = time.perf_counter()
+        O.vote(None, B.tgt[0], [f[:rows] for f in fs], ft, voxel)
+        vote_s = (time.perf_counter() - t0) * (20000 / rows)
+        res["cpu_baseline"] = {"vote_ms_extrapolated": vote_s * 1e3, "cores": 1, "kind": "port",
+                               "sample": f"oracle vote on {rows} of 20000 source rows "
+                                         "(3 exact f64 1-NN screens + the tests), x 40"}
+    return res
+
+
+def measure_voxel(with_cpu):
+    """f2: Open3D voxel_down_sample of 16 clouds of 200k points (3DMatch-like
+    extent, 2.5 cm voxels: o3d.py / DataPreparation callers) in one batched call,
+    vs the oracle's C++ restatement (one thread) on one cloud."""
+    from pointcloudregistration_amd import geometry, synth
+    rng = np.random.default_rng(21)
+    clouds = [(synth.surface_points(rng, 200000) * 2.0).astype(np.float64) for _ in range(16)]
+    dev = torch.device("cuda")
+    C = [torch.from_numpy(c).to(dev) for c in clouds]
+    geometry.voxel_down_sample_batch(C, 0.025)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        outs = geometry.voxel_down_sample_batch(C, 0.025)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    res = {"workload": "f2 voxel_down_sample: 16 clouds x 200000 pts, voxel 0.025, one batched call",
+           "ms": ms, "points_per_s": 16 * 200000 / (ms * 1e-3),
+           "out_points": int(sum(o[0].shape[0] for o in outs))}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        t0 = time.perf_counter()
+        O.voxel_down_sample(clouds[0], 0.025)
+        s = time.perf_counter() - t0
+        res["cpu_baseline"] = {"points_per_s": 200000 / s, "cores": 1, "kind": "port",
+                               "sample": "oracle (C++ unordered_map restatement) on 1 of the 16 clouds"}
     return res
 
 
@@ -864,7 +965,9 @@ def main():
                             "a4_lrf": measure_lrf(wc),
                             "a10_ndp_warp": measure_ndp(wc),
                             "f1_fpfh": measure_fpfh(wc),
-                            "f4_ndp_opt": measure_ndp_opt(wc)}
+                            "f4_ndp_opt": measure_ndp_opt(wc),
+                            "f2_voxel": measure_voxel(wc),
+                            "c5_flow": measure_c5(wc)}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

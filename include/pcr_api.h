@@ -222,6 +222,13 @@ int pcr_lrf_compute(const double *pts, int32_t P, int32_t Nmax, const int32_t *n
                     const double *queries, int32_t Qmax, const int32_t *n_q, double kernel,
                     int32_t patch_size, const int32_t *inds, int32_t max_count,
                     double *patches, double *T, int32_t *counts, pcr_stream_t stream);
+/* Host only (no device work): the patch-index draws of dip/lrf.py:76,
+ * np.random.choice(pop[c], k, replace=False) for c = 0..calls-1 in order, on the
+ * caller's legacy RandomState MT19937 state (key[624], *pos as returned by
+ * RandomState.get_state(); both updated as numpy would leave them).
+ * out (calls, k) i32.  Fails with PCR_ERR_ARG when pop[c] < k, like numpy. */
+int pcr_legacy_choice_batch(uint32_t *key, int32_t *pos, const int32_t *pop, int32_t calls,
+                            int32_t k, int32_t *out);
 
 /* ---------------------------------------------------------------------------
  * a10 -- NDP deformation-pyramid warp, all levels in one launch.  Replaces

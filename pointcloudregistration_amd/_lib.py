@@ -70,6 +70,7 @@ SIGNATURES = {
     "pcr_voxel_map_order": [_p, _i32, _p],
     "pcr_voxel_down_sample": [_p, _i32, _p, _i32, _f64, _p, _p, _p, _p, _p, _p, _p, _p],
     "pcr_voxel3i_map_order": [_p, _i32, _p],
+    "pcr_legacy_choice_batch": [_p, _p, _p, _i32, _i32, _p],
     "pcr_vote_apply": [_p, _i32, _p, _p, _p, _i32, _f64, _p, _p, _p, _p, _i32, _p, _p],
     "pcr_radius_count": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _p, _p, _p],
     "pcr_radius_neighbors": [_p, _i32, _p, _i32, _p, _p, _i32, _f32, _i32, _p, _p, _p],

@@ -6,7 +6,9 @@ come from libpcr (pcr_lrf_count / pcr_lrf_compute).  The reference's
 `np.random.choice(ptall.shape[0], patch_size, replace=False)` (dip/lrf.py:76)
 is drawn here on the host, from the same global numpy RNG and at the same
 point in the call sequence, so a caller that seeds numpy gets the reference's
-patches.  `get_batch` and `demo_patches` compute many queries in two launches
+patches; a whole query set's draws run in one call of libpcr's restatement of
+legacy RandomState.choice (pcr_legacy_choice_batch, csrc/legacy_choice.cpp)
+instead of one Python call per query.  `get_batch` and `demo_patches` compute many queries in two launches
 while drawing the indices in the reference's per-call order.
 """
 from __future__ import annotations
@@ -22,9 +24,31 @@ def _points(pcd):
     return np.asarray(pts, dtype=np.float64).reshape(-1, 3)
 
 
+def legacy_choice_batch(pops, k, random_state=None):
+    """[np.random.choice(n, k, replace=False) for n in pops] as one (len(pops), k)
+    int32 array, drawn by libpcr's host restatement (pcr_legacy_choice_batch) on
+    the stream of `random_state` (default: numpy's global RandomState), which is
+    left exactly where the Python loop would leave it."""
+    rs = random_state if random_state is not None else np.random.mtrand._rand
+    name, key, pos, has_gauss, gauss = rs.get_state(legacy=True)
+    if name != "MT19937":
+        raise ValueError(f"legacy_choice_batch needs an MT19937 RandomState, got {name}")
+    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+    pos_c = np.array([pos], np.int32)
+    pops = np.ascontiguousarray(pops, dtype=np.int32).reshape(-1)
+    out = np.zeros((len(pops), int(k)), np.int32)
+    if len(pops):
+        _lib.call("pcr_legacy_choice_batch", key.ctypes.data, pos_c.ctypes.data, pops.ctypes.data,
+                  len(pops), int(k), out.ctypes.data)
+        rs.set_state((name, key, int(pos_c[0]), has_gauss, gauss))
+    return out
+
+
 def _draw(counts, patch_size, choice):
-    return np.stack([np.asarray(choice(max(int(c), patch_size), patch_size), dtype=np.int32)
-                     for c in counts])
+    pops = np.maximum(np.asarray(counts, np.int64), patch_size)
+    if choice is None:
+        return legacy_choice_batch(pops, patch_size)
+    return np.stack([np.asarray(choice(int(c), patch_size), dtype=np.int32) for c in pops])
 
 
 def _check_sparse(cnt, qn, kernel, allow_sparse):
@@ -69,7 +93,6 @@ def lrf_batch(points, queries, kernel, patch_size, n_pts=None, n_q=None, inds=No
     qn = np.full(P, Qm) if n_q is None else np.minimum(np.asarray(n_q), Qm)
     _check_sparse(cnt, qn, kernel, allow_sparse)
     if inds is None:
-        choice = choice or (lambda n, k: np.random.choice(n, k, replace=False))
         inds = np.zeros((P, Qm, patch_size), np.int32)
         for p in range(P):
             if qn[p] > 0:
@@ -135,11 +158,9 @@ def demo_patches(pcd1, pcd2, pts1, pts2, lrf_kernel, patch_size, choice=None):
                   float(lrf_kernel), _lib.ptr(counts), _lib.stream_handle(dev))
     cnt = counts.cpu().numpy()
     _check_sparse(cnt, np.array([len(q1), len(q1)]), lrf_kernel, False)
-    choice = choice or (lambda n, k: np.random.choice(n, k, replace=False))
-    inds = np.zeros((2, len(q1), patch_size), np.int32)
-    for i in range(len(q1)):
-        for p in range(2):
-            inds[p, i] = choice(max(int(cnt[p, i]), patch_size), patch_size)
+    # the demo's call order: frag1 i, frag2 i, frag1 i+1, ...
+    inds = _draw(cnt.T.reshape(-1), patch_size, choice).reshape(len(q1), 2, patch_size)
+    inds = np.ascontiguousarray(inds.transpose(1, 0, 2))
     patches, _, _, _ = lrf_batch(P_, Q_, lrf_kernel, patch_size, n_pts=ns, inds=inds,
                                  allow_sparse=True)
     out = patches.transpose(2, 3)  # (2, Q, 3, ps) as demo.py's patchesX[i] = pts.T

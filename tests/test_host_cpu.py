@@ -1,4 +1,5 @@
 """CPU: host-side logic of the registration façade (no compute calls)."""
+import pytest
 import numpy as np
 import torch
 
@@ -28,3 +29,35 @@ def test_ransac_params_from_open3d_objects():
     c = prm.to_c()
     assert (c.edge_length_ratio, c.distance_check, c.max_iteration, c.ransac_n) == (0.9, 0.04, 100000, 3)
     assert c.mutual_filter == 1 and c.seed == 7
+
+
+# --- a4 host draws: legacy RandomState.choice restated (csrc/legacy_choice.cpp) ---
+
+@pytest.mark.parametrize("seed", [0, 42, 1000, 2**31 - 5])
+def test_legacy_choice_batch_equals_numpy_loop(seed):
+    """pcr_legacy_choice_batch == [np.random.choice(n, k, replace=False) ...] on the
+    global stream, and leaves the stream where the loop leaves it (dip/lrf.py:76)."""
+    from pointcloudregistration_amd.lrf import legacy_choice_batch
+    rng = np.random.default_rng(seed)
+    pops = np.concatenate([[256, 257, 511, 512, 513, 1024, 1025], rng.integers(256, 3000, 200)])
+    np.random.seed(seed)
+    np.random.random(int(rng.integers(0, 700)))  # arbitrary position in the 624-word block
+    st = np.random.get_state()
+    exp = np.stack([np.random.choice(int(n), 256, replace=False) for n in pops])
+    after = np.random.random(5)
+    np.random.set_state(st)
+    got = legacy_choice_batch(pops, 256)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(np.random.random(5), after)
+
+
+def test_legacy_choice_batch_own_state_and_errors():
+    from pointcloudregistration_amd import _lib
+    from pointcloudregistration_amd.lrf import legacy_choice_batch
+    rs1, rs2 = np.random.RandomState(7), np.random.RandomState(7)
+    got = legacy_choice_batch([300, 10, 5000], 10, random_state=rs1)
+    exp = np.stack([rs2.choice(n, 10, replace=False) for n in (300, 10, 5000)])
+    assert np.array_equal(got, exp) and rs1.randint(1 << 30) == rs2.randint(1 << 30)
+    with pytest.raises(_lib.PcrError, match="larger sample"):
+        legacy_choice_batch([300, 9], 10, random_state=rs1)
+    assert legacy_choice_batch([], 4).shape == (0, 4)
