@@ -94,6 +94,8 @@ def _setup_sigs():
     L.oracle_philox.argtypes = [c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     L.oracle_horn_rotation.argtypes = [c.c_void_p, c.c_void_p]
     L.oracle_voxel_down_sample.restype = c.c_int
+    L.oracle_voxel3i_map_order.restype = None
+    L.oracle_voxel3i_map_order.argtypes = [c.c_void_p, c.c_int, c.c_void_p]
     L.oracle_voxel_down_sample.argtypes = [c.c_void_p, c.c_int, c.c_double, c.c_void_p, c.c_void_p,
                                            c.c_void_p, c.c_void_p, c.c_void_p]
     L.oracle_xs_sum.restype = c.c_double
@@ -146,6 +148,15 @@ def voxel_down_sample(points, voxel_size, normals=None, colors=None):
     if k < 0:
         raise ValueError("voxel_down_sample: voxel_size <= 0 or too small")
     return op[:k].copy(), (on[:k].copy() if on is not None else None), (oc[:k].copy() if oc is not None else None)
+
+
+def voxel3i_map_order(xyz):
+    """iteration order of std::unordered_map<Vector3i, ., hash_eigen> for the keys
+    (K, 3) int32 inserted in row order (the real container)"""
+    xyz = _i32(xyz).reshape(-1, 3)
+    out = np.zeros(xyz.shape[0], np.int32)
+    L().oracle_voxel3i_map_order(_p(xyz), xyz.shape[0], _p(out))
+    return out
 
 
 def xs_sum(v):

@@ -95,3 +95,14 @@ extern "C" int oracle_voxel_down_sample(const double *pts, int n, double voxel_s
     }
     return k;
 }
+
+/* the iteration order of the same map type for keys inserted in the given order
+   (order[k] = insertion index of the k-th visited key): the check for the
+   product's array simulation of it (csrc/voxel.hip voxel3i_map_order) */
+extern "C" void oracle_voxel3i_map_order(const int *xyz, int n, int *order)
+{
+    std::unordered_map<Key, int, HashEigen> m;
+    for (int r = 0; r < n; r++) m.emplace(Key{{xyz[3 * r], xyz[3 * r + 1], xyz[3 * r + 2]}}, r);
+    int k = 0;
+    for (const auto &kv : m) order[k++] = kv.second;
+}

@@ -27,6 +27,7 @@
 #include <climits>
 #include <cmath>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 namespace pcr {
@@ -192,12 +193,70 @@ struct HashEigenV3i {
 
 // host replay of the reference's unordered_map<Vector3i, AccumulatedPoint,
 // hash_eigen> iteration order for the voxels of ONE cloud given in
-// first-occurrence order; order[k] = index (into keys) of the k-th emitted voxel
+// first-occurrence order; order[k] = index (into keys) of the k-th emitted voxel.
+//
+// libstdc++'s unique-key _Hashtable keeps all nodes in one singly linked list
+// and, per bucket, a pointer to the node BEFORE the bucket's first node; its
+// iteration order is that list.  It is simulated here with index arrays (no node
+// allocation): the same hash codes (hash_eigen), the same bucket counts (the
+// library's own _Prime_rehash_policy, asked exactly when the container asks it:
+// before every insertion of a new key), the same insertion rule (a new node goes
+// first in its bucket; into an empty bucket it goes first in the whole list and
+// the bucket of the former first node is re-pointed at it) and the same rehash
+// relinking (old list order, each node to the front of its new bucket, or of the
+// list when that bucket is empty).  oracle_voxel3i_map_order builds the real
+// container for the parity test.
 void voxel3i_map_order(const int32_t *xyz, int n, int32_t *order) {
-    std::unordered_map<V3i, int, HashEigenV3i> m;
-    for (int r = 0; r < n; ++r) m.emplace(V3i{xyz[3 * r], xyz[3 * r + 1], xyz[3 * r + 2]}, r);
+    if (n <= 0) return;
+    constexpr int kNil = -2, kBefore = -1;  // bucket slot: empty / the list head
+    std::vector<size_t> code((size_t)n);
+    for (int r = 0; r < n; ++r) code[r] = HashEigenV3i()(V3i{xyz[3 * r], xyz[3 * r + 1], xyz[3 * r + 2]});
+    std::vector<int> nxt((size_t)n, kNil), bkt(1, kNil), nb;
+    int head = kNil;
+    size_t nbkt = 1;
+    std::__detail::_Prime_rehash_policy pol;  // max_load_factor 1
+    auto link_after = [&](int before, int node) {  // node after `before` (head if kBefore)
+        int &slot = before == kBefore ? head : nxt[before];
+        nxt[node] = slot;
+        slot = node;
+    };
+    for (int r = 0; r < n; ++r) {
+        const std::pair<bool, size_t> rh = pol._M_need_rehash(nbkt, (size_t)r, 1);
+        if (rh.first) {
+            const size_t nn = rh.second;
+            nb.assign(nn, kNil);
+            int p = head;
+            head = kNil;
+            size_t bbegin = 0;
+            while (p != kNil) {
+                const int next = nxt[p];
+                const size_t b = code[p] % nn;
+                if (nb[b] == kNil) {
+                    nxt[p] = head;
+                    head = p;
+                    nb[b] = kBefore;
+                    if (nxt[p] != kNil) nb[bbegin] = p;
+                    bbegin = b;
+                } else {
+                    link_after(nb[b], p);
+                }
+                p = next;
+            }
+            bkt.swap(nb);
+            nbkt = nn;
+        }
+        const size_t b = code[r] % nbkt;
+        if (bkt[b] != kNil) {
+            link_after(bkt[b], r);
+        } else {
+            nxt[r] = head;
+            head = r;
+            if (nxt[r] != kNil) bkt[code[nxt[r]] % nbkt] = r;
+            bkt[b] = kBefore;
+        }
+    }
     int k = 0;
-    for (const auto &kv : m) order[k++] = kv.second;
+    for (int p = head; p != kNil; p = nxt[p]) order[k++] = p;
 }
 
 }  // namespace pcr
@@ -327,18 +386,18 @@ extern "C" int pcr_voxel_down_sample(const double *points, int32_t n, const int3
     std::vector<u64> hk(V);
     PCR_HIP_CHECK(hipMemcpyAsync(hk.data(), okey, sizeof(u64) * V, hipMemcpyDeviceToHost, st));
     PCR_HIP_CHECK(hipStreamSynchronize(st));
-    // per cloud: the map's iteration order (voxels in first-occurrence order)
-    std::vector<int> hout;
-    hout.reserve(V);
-    std::vector<int32_t> xyz, ord;
+    // per cloud: the map's iteration order (voxels in first-occurrence order);
+    // clouds are independent, so their replays run on host threads
     const u64 mxk = (1ull << bx) - 1ull, myk = (1ull << by) - 1ull, mzk = (1ull << bz) - 1ull;
-    for (int r0 = 0; r0 < V;) {
-        const u64 cb = bbat ? (hk[r0] >> a.sb) : 0ull;
-        int r1 = r0;
-        while (r1 < V && (bbat ? (hk[r1] >> a.sb) : 0ull) == cb) ++r1;
-        const int cnt = r1 - r0;
-        xyz.resize(3 * (size_t)cnt);
-        ord.resize(cnt);
+    std::vector<int> r0s;
+    for (int r = 0; r < V; ++r)
+        if (r == 0 || (bbat && (hk[r] >> a.sb) != (hk[r - 1] >> a.sb))) r0s.push_back(r);
+    r0s.push_back(V);
+    const int ncl = (int)r0s.size() - 1;
+    std::vector<int> hout((size_t)V);
+    auto replay = [&](int c) {
+        const int r0 = r0s[c], cnt = r0s[c + 1] - r0;
+        std::vector<int32_t> xyz(3 * (size_t)cnt), ord((size_t)cnt);
         for (int k = 0; k < cnt; ++k) {
             const u64 key = hk[r0 + k];
             xyz[3 * k] = (int32_t)((key >> a.sx) & mxk);
@@ -346,9 +405,20 @@ extern "C" int pcr_voxel_down_sample(const double *points, int32_t n, const int3
             xyz[3 * k + 2] = (int32_t)((key >> a.sz) & mzk);
         }
         voxel3i_map_order(xyz.data(), cnt, ord.data());
-        for (int k = 0; k < cnt; ++k) hout.push_back(r0 + ord[k]);
-        out_cloud_len[cb] = cnt;
-        r0 = r1;
+        for (int k = 0; k < cnt; ++k) hout[r0 + k] = r0 + ord[k];
+    };
+    const int nth = std::min(ncl, 16);
+    if (nth <= 1 || V < 65536) {
+        for (int c = 0; c < ncl; ++c) replay(c);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back([&, t]() { for (int c = t; c < ncl; c += nth) replay(c); });
+        for (auto &h : th) h.join();
+    }
+    for (int c = 0; c < ncl; ++c) {
+        const u64 cb = bbat ? (hk[r0s[c]] >> a.sb) : 0ull;
+        out_cloud_len[cb] = r0s[c + 1] - r0s[c];
     }
     const int total = (int)hout.size();
     PCR_HIP_CHECK(hipMemcpyAsync(outr, hout.data(), sizeof(int) * total, hipMemcpyHostToDevice, st));

@@ -61,3 +61,27 @@ def test_legacy_choice_batch_own_state_and_errors():
     with pytest.raises(_lib.PcrError, match="larger sample"):
         legacy_choice_batch([300, 9], 10, random_state=rs1)
     assert legacy_choice_batch([], 4).shape == (0, 4)
+
+
+# --- f2 host step: libstdc++ unordered_map iteration order simulated with arrays ---
+
+@pytest.mark.parametrize("n,kind", [(1, "rand"), (2, "rand"), (13, "rand"), (14, "rand"),
+                                    (97, "grid"), (1000, "rand"), (54321, "grid"),
+                                    (200000, "rand"), (300000, "grid")])
+def test_voxel_map_order_equals_real_container(oracle, n, kind):
+    """pcr_voxel3i_map_order (csrc/voxel.hip) == the iteration order of a real
+    std::unordered_map<Vector3i, ., hash_eigen> after inserting the same keys
+    (oracle_voxel3i_map_order), across every rehash of the container."""
+    from pointcloudregistration_amd import _lib
+    rng = np.random.default_rng(n)
+    if kind == "rand":
+        xyz = rng.integers(-(1 << 20), 1 << 20, (n, 3)).astype(np.int32)
+    else:  # voxel-like: distinct cells of a surface grid, first-occurrence order
+        side = int(np.ceil(n ** (1 / 2))) + 1
+        g = np.stack(np.meshgrid(np.arange(side), np.arange(side), [0, 1], indexing="ij"), -1)
+        xyz = g.reshape(-1, 3)[rng.permutation(2 * side * side)[:n]].astype(np.int32)
+    xyz = np.unique(xyz, axis=0)[rng.permutation(len(np.unique(xyz, axis=0)))]
+    xyz = np.ascontiguousarray(xyz, np.int32)
+    got = np.zeros(len(xyz), np.int32)
+    _lib.call("pcr_voxel3i_map_order", xyz.ctypes.data, len(xyz), got.ctypes.data)
+    assert np.array_equal(got, oracle.voxel3i_map_order(xyz))
