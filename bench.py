@@ -498,6 +498,65 @@ def measure_c5(with_cpu):
     return res
 
 
+def measure_c3(with_cpu):
+    """C3 end to end (dip/demo.py:64-178) on one pair of 40k-point mm-scale clouds:
+    voxel_down_sample(1.0) -> 2 x 2048 samples -> LRF patches (3*sqrt(3), 256) ->
+    descriptor network (weight-random PointNet-shaped stand-in, D = 64, torch) ->
+    5th-percentile filter -> feature RANSAC at 1.5; wall clock of the whole call."""
+    from pointcloudregistration_amd import dip, synth
+    rng = np.random.default_rng(31)
+    U = synth.surface_points(rng, 60000) * 40.0
+    R = synth.rotation_xyz(*np.deg2rad(rng.uniform(-30, 30, 3)))
+    t = rng.uniform(-10, 10, 3)
+    src = U[rng.permutation(60000)[:40000]] + rng.normal(0, 0.05, (40000, 3))
+    tgt = (U[rng.permutation(60000)[:40000]] + rng.normal(0, 0.05, (40000, 3))) @ R.T + t
+    net = dip.RandomPointNet(64, seed=1).cuda()
+    np.random.seed(5)
+    dip.demo_register(src, tgt, net, seed=3)
+    torch.cuda.synchronize()
+    np.random.seed(5)
+    t0 = time.perf_counter()
+    out = dip.demo_register(src, tgt, net, seed=3)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    T = out["result"].transformation
+    rre, rte = synth.rre_rte(T[:3, :3], T[:3, 3], R, t)
+    res = {"workload": "C3 DIP demo: 2 x 40000-pt clouds (mm), voxel 1.0 -> 2 x 2048 LRF "
+                       "patches -> D=64 descriptors (random-weight stand-in) -> 5th pct filter "
+                       "-> feature RANSAC d=1.5, wall clock",
+           "ms": ms, "downsampled_points": [len(out["pcd1"].points), len(out["pcd2"].points)],
+           "inlier_correspondences": int(len(out["result"].correspondence_set)),
+           "rre_deg": float(rre), "rte_mm": float(rte)}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        ker, ps = 3.0 * np.sqrt(3.0), 256
+        t0 = time.perf_counter()
+        d1, _, _ = O.voxel_down_sample(src, 1.0)
+        d2, _, _ = O.voxel_down_sample(tgt, 1.0)
+        t_vox = time.perf_counter() - t0
+        q = d1[out["inds1"][:128]]
+        t0 = time.perf_counter()
+        for i in range(128):
+            c = O.lrf_count(d1, q[i], ker)
+            O.lrf(d1, q[i], ker, ps, np.random.choice(max(c, ps), ps, replace=False))
+        t_lrf = (time.perf_counter() - t0) * 4096 / 128
+        g1, g2 = out["good1"], out["good2"]
+        a = d1[out["inds1"]][g1].astype(np.float32)
+        b = d2[out["inds2"]][g2].astype(np.float32)
+        fa, fb = out["desc1"][g1].astype(np.float32), out["desc2"][g2].astype(np.float32)
+        t0 = time.perf_counter()
+        co = O.corres(O.featnn(fa, fb), O.featnn(fb, fa), True, 3)
+        O.ransac(a, b, co, 1.5, dist_check=1.5, seed=3)
+        t_reg = time.perf_counter() - t0
+        res["cpu_baseline"] = {"ms": (t_vox + t_lrf + t_reg) * 1e3, "voxel_ms": t_vox * 1e3,
+                               "lrf_ms_extrapolated": t_lrf * 1e3, "match_ransac_ms": t_reg * 1e3,
+                               "cores": 1, "kind": "port",
+                               "sample": "oracle voxel x2, LRF on 128 of 4096 queries (x 32), "
+                                         "featnn x2 + RANSAC; the descriptor network is not timed"}
+    return res
+
+
 def measure_voxel(with_cpu):
     """f2: Open3D voxel_down_sample of 16 clouds of 200k points (3DMatch-like
     extent, 2.5 cm voxels: o3d.py / DataPreparation callers) in one batched call,
@@ -967,6 +1026,7 @@ def main():
                             "f1_fpfh": measure_fpfh(wc),
                             "f4_ndp_opt": measure_ndp_opt(wc),
                             "f2_voxel": measure_voxel(wc),
+                            "c3_flow": measure_c3(wc),
                             "c5_flow": measure_c5(wc)}
     if rank == 0:
         print(json.dumps(out))

@@ -85,3 +85,14 @@ def test_voxel_map_order_equals_real_container(oracle, n, kind):
     got = np.zeros(len(xyz), np.int32)
     _lib.call("pcr_voxel3i_map_order", xyz.ctypes.data, len(xyz), got.ctypes.data)
     assert np.array_equal(got, oracle.voxel3i_map_order(xyz))
+
+
+def test_dip_percentile_keep_matches_demo_rule():
+    """dip/demo.py:149-153: |mx| (f64) strictly above its 5th percentile"""
+    from pointcloudregistration_amd import dip
+    rng = np.random.default_rng(0)
+    mx = rng.random((2048, 256)).astype(np.float32)
+    mag = np.linalg.norm(mx.astype(np.float64), axis=1)
+    keep = dip.percentile_keep(mx, 5)
+    assert np.array_equal(keep, mag > np.percentile(mag, 5))
+    assert 1940 <= keep.sum() <= 1946
