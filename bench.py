@@ -971,7 +971,7 @@ def main():
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS},
         "roofline_chamfer": _chamfer_roofline(prof["nnd_grid_query"], P, N),
-        "roofline_ransac": _sweep_roofline("a7 RANSAC verification", "ransac_pair_kernel",
+        "roofline_ransac": _sweep_roofline("a7 RANSAC verification", "ransac_val_kernel",
                                            prof["ransac_validate"], validated, N, cb_r),
         "roofline_icp": _sweep_roofline("a8 ICP", "icp_kernel", prof["icp"], icp_sweeps, N, cb_i),
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
