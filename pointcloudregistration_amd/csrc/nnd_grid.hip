@@ -183,11 +183,22 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
     const int w = xcd_slot(blockIdx.x, gridDim.x);
     const int grp = w / nchunk, chunk = w - grp * nchunk;
     const int dir = grp / a.B, b = grp - dir * a.B;
-    const int sub = threadIdx.x % LPQ, qi = chunk * QPB + threadIdx.x / LPQ;
+    const int sub = threadIdx.x % LPQ, qslot = chunk * QPB + threadIdx.x / LPQ;
     const int qs = dir, gs = 1 - dir;  // queries from set dir, candidates from the other set
-    if (qi >= a.n[qs]) return;  // a query's lanes leave together
-    const float *q = a.xyz[qs] + ((size_t)b * a.n[qs] + qi) * 3;
-    const float qx = q[0], qy = q[1], qz = q[2];
+    if (qslot >= a.n[qs]) return;  // a query's lanes leave together
+    // queries in the slot order of their own cloud's grid (cell-sorted): the
+    // lanes of a wave walk neighbouring cells (less divergence, shared lines);
+    // the reference-loop clouds (flag) have no grid and go in index order
+    int qi = qslot;
+    float qx, qy, qz;
+    if (a.flag[b]) {
+        const float *q = a.xyz[qs] + ((size_t)b * a.n[qs] + qi) * 3;
+        qx = q[0]; qy = q[1]; qz = q[2];
+    } else {
+        const float4 qp = a.pts[((size_t)qs * a.B + b) * a.nmax + qslot];
+        qx = qp.x; qy = qp.y; qz = qp.z;
+        qi = __float_as_int(qp.w);
+    }
     const int m = a.n[gs];
     const float *C = a.xyz[gs] + (size_t)b * m * 3;
     float best = __builtin_inff();

@@ -198,3 +198,32 @@ def test_nnd_grid_lanes_per_query_vs_oracle(oracle, monkeypatch, kind, lpq):
     for k, g, e in zip(("d1", "d2", "i1", "i2", "g1", "g2"), got, (e1, e2, j1, j2, eg1, eg2)):
         assert_bitexact(g, e, f"{kind}/lpq{lpq}/{k}")
 
+
+
+def test_nnd_grid_mixed_batch_vs_oracle(oracle, monkeypatch):
+    """A 70-cloud batch holding every hard kind at once -- outliers (full-scan
+    fallback), planar, identical, quantised ties, a NaN and an Inf cloud (the
+    reference loop) -- next to ordinary clouds, with the queries walked in their
+    own grid's slot order: bit for bit against the oracle, backward included."""
+    monkeypatch.setenv("PCR_NND_ALGO", "grid")
+    rng = np.random.default_rng(64)
+    B, n, m = 70, 1100, 1200
+    x1 = rng.random((B, n, 3), dtype=np.float32)
+    x2 = rng.random((B, m, 3), dtype=np.float32)
+    x1[0, ::50] += np.float32(100.0)                        # outliers
+    x1[1, :, 2] = 0.5
+    x2[1, :, 2] = 0.5                                       # planar
+    x1[2] = 0.25
+    x2[2] = 0.25                                            # identical
+    x1[3] = (rng.integers(0, 8, (n, 3)) / 8).astype(np.float32)
+    x2[3] = (rng.integers(0, 8, (m, 3)) / 8).astype(np.float32)   # quantised ties
+    x2[4, 0, 2] = np.nan
+    x1[5, 7, 0] = np.inf                                    # the reference loop
+    gd1 = rng.standard_normal((B, n)).astype(np.float32)
+    gd2 = rng.standard_normal((B, m)).astype(np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        got = _run_fwd_bwd(x1, x2, gd1, gd2)
+        e1, e2, j1, j2 = oracle.nnd_forward(x1, x2)
+        eg1, eg2 = oracle.nnd_backward(x1, x2, gd1, gd2, j1, j2)
+    for k, g, e in zip(("d1", "d2", "i1", "i2", "g1", "g2"), got, (e1, e2, j1, j2, eg1, eg2)):
+        assert_bitexact(g, e, f"mixed/{k}")
