@@ -51,9 +51,9 @@ __device__ __forceinline__ int coop_load(const int *p) {
 }
 
 // host: workgroups per pair for a launch of P pairs whose kernel fits `per_cu`
-// workgroups per CU (0 = cannot tell): fill the chip, at most 8, 1 when the pairs
-// alone fill it
-int coop_groups(int P, int per_cu);
+// workgroups per CU (0 = cannot tell): fill the chip, at most gmax, 1 when the
+// pairs alone fill it
+int coop_groups(int P, int per_cu, int gmax = 8);
 
 // host: launch `fn` with P*G workgroups (cooperative when G > 1)
 hipError_t coop_launch(const void *fn, int P, int G, int threads, void **args, size_t lds,

@@ -426,7 +426,10 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         (void)hipGetLastError();
         per_cu = 0;
     }
-    a.G = coop_groups(P, per_cu);
+    // at most 4: an ICP iteration meets at four pair barriers, and past 4
+    // workgroups their cost outgrows the split sweep (32-pair shard: G = 4
+    // 0.80 ms, G = 8 0.97 ms; RANSAC, two barriers per sweep, is best at 8)
+    a.G = coop_groups(P, per_cu, 4);
     // working copy and correspondences, by position
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
     char *ws = (char *)workspace(8, (sizeof(double) * 3 + sizeof(float4)) * (size_t)P * nm + 64);

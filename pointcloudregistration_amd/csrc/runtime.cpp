@@ -61,7 +61,7 @@ void *workspace(int slot, size_t bytes) {
 }
 
 // ---- several workgroups per pair (coop.h) ---------------------------------
-int coop_groups(int P, int per_cu) {
+int coop_groups(int P, int per_cu, int gmax) {
     if (const char *e = getenv("PCR_COOP_G")) {  // tests: force a split
         const int g = atoi(e);
         if (g >= 1 && g <= 16) return g;
@@ -75,7 +75,7 @@ int coop_groups(int P, int per_cu) {
     const long cap = (long)per_cu * cus;
     if ((long)P * 2 > cap) return 1;
     const long g = cap / P;
-    return (int)(g > 8 ? 8 : g);
+    return (int)(g > gmax ? gmax : g);
 }
 
 hipError_t coop_launch(const void *fn, int P, int G, int threads, void **args, size_t lds,
