@@ -34,7 +34,8 @@ BLUE = [0 / 255, 76 / 255, 153 / 255]
 
 def percentile_keep(mx, perc=5):
     """demo.py:149-153: rows whose |mx| (f64 norm) exceeds the perc-th percentile"""
-    mag = np.linalg.norm(np.asarray(mx, np.float64), axis=1)
+    mx = np.asarray(mx, np.float64)
+    mag = np.linalg.norm(mx.reshape(mx.shape[0], -1), axis=1)  # (B, 256) or (B, 256, 1)
     return mag > np.percentile(mag, perc)
 
 
@@ -92,25 +93,50 @@ def demo_register(source, target, net, voxel_size=1.0, lrf_kernel=3.0 * np.sqrt(
             "good1": good1, "good2": good2}
 
 
-class RandomPointNet(torch.nn.Module):
-    """A weight-random stand-in with PointNetFeature's interface (dip/network.py:
-    (B,3,ps) -> (f (B,dim) l2-normalised, mx (B,256), amx)) for tests and the bench:
-    a shared per-point MLP 3 -> 128 -> 256, max-pool, linear 256 -> dim.  The
-    trained network is out of scope (it stays PyTorch)."""
+def _block(layer, n):
+    return torch.nn.Sequential(layer, torch.nn.Dropout(p=0.5), torch.nn.BatchNorm1d(n), torch.nn.ReLU())
 
-    def __init__(self, dim=64, seed=0):
+
+class _STN3d(torch.nn.Module):
+    def __init__(self):
         super().__init__()
-        g = torch.Generator().manual_seed(seed)
-        self.w1 = torch.nn.Parameter(torch.randn(128, 3, generator=g) * 0.5)
-        self.w2 = torch.nn.Parameter(torch.randn(256, 128, generator=g) / 128 ** 0.5)
-        self.w3 = torch.nn.Parameter(torch.randn(dim, 256, generator=g) / 256 ** 0.5)
+        self.conv1 = _block(torch.nn.Conv1d(3, 128, 1), 128)
+        self.conv2 = _block(torch.nn.Conv1d(128, 256, 1), 256)
+        self.fc1 = _block(torch.nn.Linear(256, 128), 128)
+        self.fc2 = torch.nn.Sequential(torch.nn.Linear(128, 9))
 
     def forward(self, x):
-        h = torch.relu(torch.einsum("oc,bcn->bon", self.w1.to(x), x))
-        h = torch.relu(torch.einsum("oc,bcn->bon", self.w2.to(x), h))
-        mx, amx = h.max(dim=2)
-        f = torch.nn.functional.normalize(mx @ self.w3.to(x).t(), dim=1)
+        x = self.conv2(self.conv1(x)).max(dim=2)[0]
+        x = self.fc2(self.fc1(x)) + torch.eye(3, device=x.device, dtype=x.dtype).reshape(1, 9)
+        return x.view(-1, 3, 3)
+
+
+class PointNetFeature(torch.nn.Module):
+    """The architecture of DIP's descriptor network (dip/network.py:50-122:
+    T-net, Conv1d 3->128->256 with BatchNorm, max-pool, Linear 256->128->dim,
+    l2-normalised), with the same parameter names so the reference's state dict
+    loads into it.  It stays PyTorch (not on the hot path); with a seeded random
+    init it is SURVEY 8(d)'s C3 descriptor for tests and the bench.  forward(x)
+    -> (f (B, dim), mx (B, 256, 1), amx) as the demo calls it (:137)."""
+
+    def __init__(self, dim=64, l2norm=True, tnet=True):
+        super().__init__()
+        self.l2norm, self.tnet = l2norm, tnet
+        self.stn3d = _STN3d()
+        self.conv1 = _block(torch.nn.Conv1d(3, 128, 1), 128)
+        self.conv2 = _block(torch.nn.Conv1d(128, 256, 1), 256)
+        self.fc1 = _block(torch.nn.Linear(256, 128), 128)
+        self.fc2 = torch.nn.Sequential(torch.nn.Linear(128, dim))
+
+    def forward(self, x):
+        if self.tnet:
+            x = torch.bmm(self.stn3d(x), x)
+        x = self.conv2(self.conv1(x))
+        mx, amx = torch.max(x, 2, keepdim=True)
+        f = self.fc2(self.fc1(mx.view(-1, 256)))
+        if self.l2norm:
+            f = torch.nn.functional.normalize(f, p=2, dim=1)
         return f, mx, amx
 
 
-__all__ = ["demo_register", "execute_global_registration", "percentile_keep", "RandomPointNet"]
+__all__ = ["demo_register", "execute_global_registration", "percentile_keep", "PointNetFeature"]
