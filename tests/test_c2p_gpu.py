@@ -156,3 +156,35 @@ def test_c5_numpy_dropin_flow(oracle):
     assert T.tobytes() == r["T"].tobytes()
     assert np.array_equal(corrs, np.unique(r["correspondence_set"][:, 0]))
     assert np.asarray(estimate.points).astype(np.float32).tobytes() == est.tobytes()
+
+
+def test_vote_edge_sizes(oracle):
+    """one target row (every source votes for it: all distances 0 -> no
+    replacement) and an empty source"""
+    rng = np.random.default_rng(2)
+    d = 8
+    tgt = rng.random((1, 3)).astype(np.float32)
+    fs = [rng.standard_normal((50, d)).astype(np.float32) for _ in range(3)]
+    ft = [rng.standard_normal((1, d)).astype(np.float32) for _ in range(3)]
+    exp, rep_exp = oracle.vote(None, tgt, fs, ft, 0.05)
+    out, rep = c2p.vote(None, tgt, [f.copy() for f in fs], [f.copy() for f in ft], 0.05,
+                        return_mask=True)
+    assert not rep_exp.any() and not rep.cpu().numpy().any()
+    assert np.array_equal(out[2], exp[2]) and np.array_equal(out[3], exp[3])
+    empty = [np.zeros((0, d), np.float32) for _ in range(3)]
+    ft2 = [rng.standard_normal((20, d)).astype(np.float32) for _ in range(3)]
+    out, rep = c2p.vote(None, rng.random((20, 3)).astype(np.float32), empty,
+                        [f.copy() for f in ft2], 0.05, return_mask=True)
+    assert out[2].shape == (0, d) and rep.numel() == 0
+    assert np.array_equal(out[3], ft2[0])
+
+
+def test_get_coor_points_device_tensors(oracle):
+    rng = np.random.default_rng(4)
+    fs = rng.standard_normal((300, 32)).astype(np.float32)
+    ft = rng.standard_normal((400, 32)).astype(np.float32)
+    tgt = torch.from_numpy(rng.random((400, 3)).astype(np.float32)).cuda()
+    y, inds = c2p.get_coor_points(torch.from_numpy(fs).cuda(), torch.from_numpy(ft).cuda(), tgt)
+    exp = oracle.featnn(fs, ft)
+    assert np.array_equal(inds.cpu().numpy(), exp)
+    assert torch.equal(y, tgt[torch.from_numpy(exp).cuda().long()])
