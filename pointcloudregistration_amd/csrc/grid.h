@@ -71,33 +71,100 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
             if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; if constexpr (kSlot) bs = s; }
         }
     };
-    for (int x = x0; x <= x1; ++x) {
-        const double gx = cell_gap(px, x, g.cell);
-        if (gx > lim) continue;
-        for (int y = y0; y <= y1; ++y) {
-            const double gxy = gx + cell_gap(py, y, g.cell);
-            if (gxy > lim) continue;
-            for (int z = z0; z <= z1; ++z) {
-                if (gxy + cell_gap(pz, z, g.cell) > lim) continue;
+    if (x1 - x0 <= 1 && y1 - y0 <= 1 && z1 - z0 <= 1 && g.S <= 32768) {
+        // The usual case (cells 2.01 r wide, <= 32768 points): at most 2 x 2 x 2
+        // cells, slot numbers below 2^16.  Their
+        // slot ranges form one flat candidate sequence walked two at a time, so
+        // a wave runs as long as its longest lane's TOTAL, not the sum over cells
+        // of each cell's longest lane (the nested cell / slot loops did that).
+        // q[k] = (lo | hi << 16) of the k-th non-empty range, queued from q[0].
+        unsigned q[8];
+        int nq = 0, total = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int x = x0 + (c >> 2), y = y0 + ((c >> 1) & 1), z = z0 + (c & 1);
+            const bool in = x <= x1 && y <= y1 && z <= z1 &&
+                            cell_gap(px, x, g.cell) + cell_gap(py, y, g.cell) + cell_gap(pz, z, g.cell) <= lim;
+            q[c] = 0u;
+            if (in) {
                 const unsigned h = cell_hash(x, y, z, g.S);
-                int s = (int)g.start[h];
-                const int s1 = (int)g.start[h + 1];
-                for (; s + 1 < s1; s += 2) {
-                    // both loads first, then the two updates in slot order
-                    const float ax = g.x[s], ay = g.y[s], az = g.z[s];
-                    const float bx = g.x[s + 1], by = g.y[s + 1], bz = g.z[s + 1];
-                    const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
-                    const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
-                    if (da < thr) {
-                        const int j = (int)g.idx[s];
-                        if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = s; }
-                    }
-                    if (db < thr) {
-                        const int j = (int)g.idx[s + 1];
-                        if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = s + 1; }
-                    }
+                const int lo = (int)g.start[h], hi = (int)g.start[h + 1];
+                if (hi > lo) {
+                    // compact: the k-th non-empty range goes to q[k]
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (k == nq) q[k] = (unsigned)lo | ((unsigned)hi << 16);
+                    ++nq;
+                    total += hi - lo;
                 }
-                if (s < s1) take(s);
+            }
+        }
+        int s = (int)(q[0] & 0xffffu), e = (int)(q[0] >> 16);
+        auto advance = [&]() {  // next range: shift the queue down by one
+#pragma unroll
+            for (int k = 0; k < 7; ++k) q[k] = q[k + 1];
+            q[7] = 0u;
+            s = (int)(q[0] & 0xffffu);
+            e = (int)(q[0] >> 16);
+        };
+        while (total > 0) {
+            // two candidates: (s, s + 1) in this range, or s and the next range's first
+            const int sa = s;
+            int sb;
+            if (s + 1 < e) {
+                sb = s + 1;
+                s += 2;
+            } else {
+                advance();
+                sb = s;
+                ++s;
+            }
+            const bool hb = total >= 2;
+            if (s >= e && total > 2) advance();
+            const float ax = g.x[sa], ay = g.y[sa], az = g.z[sa];
+            const int sbb = hb ? sb : sa;
+            const float bx = g.x[sbb], by = g.y[sbb], bz = g.z[sbb];
+            const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
+            const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
+            if (da < thr) {
+                const int j = (int)g.idx[sa];
+                if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = sa; }
+            }
+            if (hb && db < thr) {
+                const int j = (int)g.idx[sbb];
+                if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = sbb; }
+            }
+            total -= hb ? 2 : 1;
+        }
+    } else {
+        for (int x = x0; x <= x1; ++x) {
+            const double gx = cell_gap(px, x, g.cell);
+            if (gx > lim) continue;
+            for (int y = y0; y <= y1; ++y) {
+                const double gxy = gx + cell_gap(py, y, g.cell);
+                if (gxy > lim) continue;
+                for (int z = z0; z <= z1; ++z) {
+                    if (gxy + cell_gap(pz, z, g.cell) > lim) continue;
+                    const unsigned h = cell_hash(x, y, z, g.S);
+                    int s = (int)g.start[h];
+                    const int s1 = (int)g.start[h + 1];
+                    for (; s + 1 < s1; s += 2) {
+                        // both loads first, then the two updates in slot order
+                        const float ax = g.x[s], ay = g.y[s], az = g.z[s];
+                        const float bx = g.x[s + 1], by = g.y[s + 1], bz = g.z[s + 1];
+                        const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
+                        const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
+                        if (da < thr) {
+                            const int j = (int)g.idx[s];
+                            if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = s; }
+                        }
+                        if (db < thr) {
+                            const int j = (int)g.idx[s + 1];
+                            if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = s + 1; }
+                        }
+                    }
+                    if (s < s1) take(s);
+                }
             }
         }
     }

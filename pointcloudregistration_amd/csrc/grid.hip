@@ -112,14 +112,26 @@ __global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, c
                                                              double inv_cell, int32_t *order) {
     extern __shared__ int bk[];  // kOrdBuckets + 1: counts -> starts -> cursors
     __shared__ int smin[3][16], smax[3][16];
+    constexpr int kReg = 8;      // points per thread whose cell coordinates stay in registers
     const int p = blockIdx.x, t = threadIdx.x;
     const int m = count_of(n, p, Nmax);
     const float *P = pts + (size_t)p * Nmax * 3;
     int32_t *o = order + (size_t)p * Nmax;
+    auto cellq = [&](int i, int c) { return (int)__builtin_floor((double)P[3 * i + c] * inv_cell); };
+    int qr[kReg][3];
     int mn[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff}, mx[3] = {-0x7fffffff, -0x7fffffff, -0x7fffffff};
-    for (int i = t; i < m; i += 1024)
+#pragma unroll
+    for (int u = 0; u < kReg; ++u) {
+        const int i = t + 1024 * u;
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const int q = (int)__builtin_floor((double)P[3 * i + c] * inv_cell);
+            qr[u][c] = i < m ? cellq(i, c) : 0;
+            if (i < m) { mn[c] = min(mn[c], qr[u][c]); mx[c] = max(mx[c], qr[u][c]); }
+        }
+    }
+    for (int i = t + 1024 * kReg; i < m; i += 1024)
+        for (int c = 0; c < 3; ++c) {
+            const int q = cellq(i, c);
             mn[c] = min(mn[c], q);
             mx[c] = max(mx[c], q);
         }
@@ -141,18 +153,33 @@ __global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, c
     }
     int shift = 0;
     while ((ext >> shift) >= (1 << kOrdBits)) ++shift;
-    auto key = [&](int i) -> unsigned {
+    auto key_of = [&](const int (&q)[3]) -> unsigned {
         unsigned k = 0;
         for (int c = 0; c < 3; ++c) {
-            const int q = ((int)__builtin_floor((double)P[3 * i + c] * inv_cell) - base[c]) >> shift;
-            k |= spread10((unsigned)min(max(q, 0), (1 << kOrdBits) - 1)) << c;
+            const int v = (q[c] - base[c]) >> shift;
+            k |= spread10((unsigned)min(max(v, 0), (1 << kOrdBits) - 1)) << c;
         }
         return k;
     };
-    for (int i = t; i < m; i += 1024) atomicAdd(&bk[key(i)], 1);
+    auto key = [&](int i) -> unsigned {
+        const int q[3] = {cellq(i, 0), cellq(i, 1), cellq(i, 2)};
+        return key_of(q);
+    };
+    unsigned kr[kReg];
+#pragma unroll
+    for (int u = 0; u < kReg; ++u) {
+        kr[u] = key_of(qr[u]);
+        if (t + 1024 * u < m) atomicAdd(&bk[kr[u]], 1);
+    }
+    for (int i = t + 1024 * kReg; i < m; i += 1024) atomicAdd(&bk[key(i)], 1);
     __syncthreads();
     block_exclusive_scan_1024(bk, bk, kOrdBuckets, false);
-    for (int i = t; i < m; i += 1024) o[atomicAdd(&bk[key(i)], 1)] = i;
+#pragma unroll
+    for (int u = 0; u < kReg; ++u) {
+        const int i = t + 1024 * u;
+        if (i < m) o[atomicAdd(&bk[kr[u]], 1)] = i;
+    }
+    for (int i = t + 1024 * kReg; i < m; i += 1024) o[atomicAdd(&bk[key(i)], 1)] = i;
     for (int i = m + t; i < Nmax; i += 1024) o[i] = i;
 }
 
