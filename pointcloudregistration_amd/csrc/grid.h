@@ -195,6 +195,14 @@ inline size_t grid_lds_bytes(int mstride, int S, size_t budget) {
     return a <= budget ? a : 0;
 }
 
+// view of a grid copy that grid_to_lds placed at `lds` (no data movement)
+__device__ inline GridT<uint16_t> grid_lds_view(const GridBatch &gb, char *lds) {
+    float *lx = (float *)lds;
+    uint16_t *li = (uint16_t *)(lx + 3 * (size_t)gb.mstride);
+    return GridT<uint16_t>{lx, lx + gb.mstride, lx + 2 * (size_t)gb.mstride, li, li + gb.mstride,
+                           gb.S, gb.cell, 1.0 / gb.cell};
+}
+
 // cooperative copy of pair p's grid into LDS (all threads of the block call);
 // layout: x[m] y[m] z[m] idx16[m] start16[S+1]
 __device__ inline GridT<uint16_t> grid_to_lds(const GridBatch &gb, int p, int m, char *lds) {

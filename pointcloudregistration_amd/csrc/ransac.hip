@@ -13,26 +13,30 @@
 //    edge-length and distance checkers; the pass bits (one ballot word per 64
 //    iterations) and the passing transforms go to HBM.  The Jacobi state needs
 //    ~440 VGPRs: a kernel of its own runs it at one wave per SIMD without
-//    spilling (inside the 1024-thread verification kernel it spilled ~320 VGPRs
-//    to scratch);
-//  * ransac_val_kernel (1024 threads, the pair's target hash grid copied to
-//    LDS): walks the pass bits in iteration order and validates each passing
-//    hypothesis below the live bound est_k -- every source point transformed
-//    and queried (64-query chunks in spatial order taken from a counter),
-//    inlier count + exact fixed-point error sum + inlier ratio over the
-//    correspondences -- then applies Open3D's update rule and
-//    est_k = min(est_k, ceil(log(1-conf)/log(1-w^n))).  The result is exactly
-//    the sequential one whatever the round boundaries.  With fewer pairs than
-//    CUs a pair's sweeps are split over G workgroups (cooperative launch, coop.h)
-//    that add integer partials and take the same decision;
-//  * the pair's correspondence set / inlier mask come from the best
-//    hypothesis' own sweep (double-buffered target indices), written by the
-//    round in which the pair finishes.
+//    spilling;
+//  * ransac_task_kernel: the round's tasks = the passing hypotheses below the
+//    pair's live bound, in iteration order;
+//  * ransac_sweep_kernel (persistent 1024-thread workgroups, one per CU, the
+//    task's target hash grid copied to LDS): validates the tasks of ALL pairs
+//    speculatively and in parallel -- rank-major (every pair's first passing
+//    hypothesis, then every pair's second, ...) from a global counter, so a
+//    pair with many hypotheses no longer holds one CU for the whole launch
+//    while the others idle.  A sweep transforms and queries every source point
+//    (64-query chunks in spatial order), counts inliers, sums the exact
+//    fixed-point error and the inlier ratio over the correspondences.  Results
+//    are independent of each other; two exact shortcuts use the pair's already
+//    finished tasks (cut bound, skip beyond est_k: see the kernel);
+//  * ransac_replay_kernel (one workgroup per pair): Open3D's update rule and
+//    est_k = min(est_k, ceil(log(1-conf)/log(1-w^n))) applied to the results in
+//    iteration order, stopping at the first hypothesis at or beyond est_k --
+//    exactly the sequential loop's decisions, `validated` count included.
+//    The best hypothesis' targets come from its sweep's slot (or one more sweep
+//    when it had none); outputs are written in the round the pair finishes.
 #include "pcr_internal.h"
-#include "coop.h"
 #include "geom.h"
 #include "grid.h"
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 namespace pcr {
@@ -51,14 +55,26 @@ struct RState {
     double best_fit, best_rmse;
     int est_k, best_itr, validated, last_upd;
     int best_cnt;   // inlier count of the best hypothesis (0: none yet)
-    int cur_buf, best_buf;  // cand buffer of the running sweep / of the best hypothesis
+    int fix;        // 1: bestbuf does not hold the best hypothesis' targets (no slot)
     int active;     // 1 while hypotheses remain below min(max_iter, est_k)
+    int pad;
 };
 
-// integer partials of one split sweep (G > 1), per pair and parity
-struct SweepAcc {
-    unsigned long long acc;
-    int cnt, cin, misses, chunk;
+// one speculative validation: hypothesis `tasks[p][r]` swept over all source points
+struct TaskRes {
+    unsigned long long acc;  // fixed-point sum of the inliers' d2
+    int cnt, cin;            // inliers, inlier correspondences
+    int status;              // kPending / kDone / kCut / kSkipped
+    int pad;
+};
+constexpr int kPending = 0, kDone = 1, kCut = 2, kSkipped = 3;
+
+// round-global counters (zeroed before every round)
+struct RHeader {
+    int task_ctr;      // next task of the persistent sweep kernel
+    int maxtask;       // max tasks of one pair in this round
+    int active_count;  // pairs still active after the round
+    int bad;           // replay met a task it needed that was never swept (bug guard)
 };
 
 struct RArgs {
@@ -66,7 +82,7 @@ struct RArgs {
     const int32_t *n_src, *n_tgt;
     const int32_t *corres, *n_corres;
     const uint32_t *pair_ids;
-    int Nmax, Mmax, Kmax;
+    int P, Nmax, Mmax, Kmax;
     double d, thr, dd, edge, dcheck, conf;
     int rn, max_iter;
     uint64_t seed;
@@ -76,16 +92,18 @@ struct RArgs {
     uint32_t *mask;
     int words;
     const int32_t *order;   // (P, Nmax) spatial order of the source points, or null
-    int32_t *cand;          // (P, 2, Nmax): target per source point, best / current sweep
     RState *state;          // (P)
     double *hypT;           // (P, hcap, 12) passing transforms of the round
     unsigned long long *hypbits;  // (P, hcap / 64) pass bits of the round
     int hcap;               // hypotheses per round slot (multiple of 256)
     int b0, b1;             // iterations of this round
-    int G;                  // workgroups per pair (val kernel)
-    SweepAcc *sacc;         // (P, 2) when G > 1
-    unsigned *bar;          // (P, 2) when G > 1
-    int *active_count;      // pairs still active after the round
+    int *ntask;             // (P) tasks of the round per pair
+    int *tasks;             // (P, hcap) their iterations, ascending
+    TaskRes *res;           // (P, hcap)
+    int32_t *slots;         // (P, nslots, Nmax) targets found by task r < nslots
+    int nslots;
+    int32_t *bestbuf;       // (P, Nmax) targets of the best hypothesis so far
+    RHeader *hdr;
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -196,214 +214,336 @@ struct Shared {  // LDS header (the grid copy follows)
     double Te[12];
     unsigned long long racc[kWaves];
     int rcnt[kWaves], rcin[kWaves];
-    int chunk;     // next 64-query chunk of the current sweep (G = 1)
-    int misses;    // source points without a correspondence so far in this sweep (G = 1)
-    int nsweep;    // sweeps done in this launch (parity of the split accumulators)
-    int done;
+    int chunk;     // next 64-query chunk of the running sweep
+    int misses;    // source points without a correspondence so far in this sweep
+    int task, lb, skip, gp;  // current task, its cut bound, skip flag, pair whose grid is loaded
+    int best_r, done;
 };
 
-// one WG per pair (G = 1) or G WGs per pair (cooperative launch): blockIdx = p*G + g
-template <bool kLds, int RN>
-__global__ __launch_bounds__(kThreads) void ransac_val_kernel(RArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char dsm[];
-    Shared &sh = *reinterpret_cast<Shared *>(dsm);
-    const int G = a.G;
-    const int p = blockIdx.x / G, g = blockIdx.x - p * G;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int n = cnt_of(a.n_src, p, a.Nmax), m = cnt_of(a.n_tgt, p, a.Mmax);
-    const int K = a.n_corres ? min(max(a.n_corres[p], 0), a.Kmax) : a.Kmax;
-    const bool ok = pair_ok(a, p, RN);
-    if (tid == 0) {
-        if (a.b0 == 0) {
-            RState &s = sh.st;
-            for (int k = 0; k < 12; ++k) s.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
-            s.best_fit = 0.0; s.best_rmse = 0.0;
-            s.est_k = a.max_iter; s.best_itr = -1; s.validated = 0; s.last_upd = -1;
-            s.best_cnt = 0; s.cur_buf = 0; s.best_buf = 0; s.active = ok ? 1 : 0;
-        } else {
-            sh.st = a.state[p];
-        }
-        sh.chunk = 0; sh.misses = 0; sh.nsweep = 0; sh.done = 0;
+// One step of the sequential loop (Open3D's rule) for validated hypothesis
+// `itr` with sweep result r; T (may be null) is copied when it becomes the best.
+__device__ inline bool apply_result(RState &s, int itr, const TaskRes &r, const double *T, int n,
+                                    int K, double scale, double conf, int RN) {
+    const bool cut = r.status == kCut;  // its inliers were below the best's: cannot win
+    double fit = 0.0, rmse = 0.0;
+    if (!cut && r.cnt > 0) {
+        fit = (double)r.cnt / (double)n;
+        rmse = __builtin_sqrt(((double)r.acc / scale) / (double)r.cnt);
     }
-    __syncthreads();
-    const bool was_active = sh.st.active != 0 || (a.b0 == 0);  // round 0 finishes invalid pairs
-    if (!was_active) return;  // uniform over the pair's G workgroups
+    s.validated += 1;
+    if (!cut && (fit > s.best_fit || (fit == s.best_fit && rmse < s.best_rmse))) {
+        s.best_cnt = r.cnt;
+        s.best_fit = fit;
+        s.best_rmse = rmse;
+        s.best_itr = itr;
+        s.last_upd = itr;
+        if (T)
+            for (int k = 0; k < 12; ++k) s.bestT[k] = T[k];
+        const double kd = est_k_bound((double)r.cin / (double)K, RN, conf);
+        if (kd < (double)s.est_k) s.est_k = (int)__builtin_ceil(kd);
+        return true;
+    }
+    return false;
+}
+
+// One workgroup sweeps every source point of pair p under Te: inliers, exact
+// fixed-point error sum and (unless cut) the inlier correspondences, in
+// 64-query chunks of the spatial order taken from an LDS counter.  The sweep
+// stops once its misses exceed lim_miss.  cbuf (may be null): target per source.
+template <bool kLds, int RN, typename Grid>
+__device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p, int n, int K,
+                              const double *Te, int lim_miss, int32_t *cbuf) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
     const int32_t *co = a.corres + (size_t)p * a.Kmax * 2;
     const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
-    GridT<uint16_t> gl{};
-    GridView gg{};
-    if (ok && sh.st.active) {
-        if constexpr (kLds) gl = grid_to_lds(a.grid, p, m, dsm + ((sizeof(Shared) + 15) & ~size_t(15)));
-        else gg = a.grid.view(p);
-    }
-    __syncthreads();
     const double scale = fx_scale(a.thr);
     const int nch = (n + 63) >> 6;
-    const int hw = a.hcap / 64;
-    const unsigned long long *bits = a.hypbits + (size_t)p * hw;
-    const int span = min(a.b1, a.max_iter) - a.b0;
-    bool stop = !(ok && sh.st.active);
-    for (int w = 0; !stop && w * 64 < span; ++w) {
-        unsigned long long word = bits[w];
-        while (word) {
-            const int e = __builtin_ctzll(word);
-            word &= word - 1ull;
-            const int itr_e = a.b0 + w * 64 + e;
-            if (itr_e >= sh.st.est_k) { stop = true; break; }  // uniform: LDS value after a barrier
-            if (tid < 12) sh.Te[tid] = a.hypT[((size_t)p * a.hcap + (itr_e - a.b0)) * 12 + tid];
-            __syncthreads();
-            double Te[12];
-#pragma unroll
-            for (int k = 0; k < 12; ++k) Te[k] = sh.Te[k];
-            SweepAcc *sa = (G > 1) ? a.sacc + (size_t)p * 2 + (sh.nsweep & 1) : nullptr;
-            unsigned long long acc = 0;
-            int cnt = 0, cin = 0;
-            // a hypothesis with more than n - best_cnt misses cannot reach the
-            // best fitness (not even tie it): Open3D's rule can never accept
-            // it, so its sweep stops there (exact; no effect on T, fitness,
-            // rmse or est_k)
-            const int lim_miss = sh.st.best_cnt > 0 ? n - sh.st.best_cnt : 0x7fffffff;
-            int32_t *cbuf = a.cand + ((size_t)p * 2 + sh.st.cur_buf) * a.Nmax;
-            for (;;) {
-                int c = 0;
-                if (lane == 0) c = (G > 1) ? coop_fetch_add(&sa->chunk, 1) : atomicAdd(&sh.chunk, 1);
-                c = __shfl(c, 0, 64);
-                if (c >= nch) break;
-                const int k = (c << 6) + lane;
-                int j = 0;
-                if (k < n) {
-                    const int i = ord ? ord[k] : k;
-                    double px, py, pz, d2;
-                    xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
-                    if constexpr (kLds) j = grid_query(gl, a.d, a.thr, px, py, pz, d2);
-                    else j = grid_query(gg, a.d, a.thr, px, py, pz, d2);
-                    if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
-                    cbuf[i] = j;
-                }
-                const int miss = __popcll(__ballot(k < n && j < 0));
-                int tot = 0;
-                if (lane == 0)
-                    tot = ((G > 1) ? coop_fetch_add(&sa->misses, miss) : atomicAdd(&sh.misses, miss)) + miss;
-                tot = __shfl(tot, 0, 64);
-                if (tot > lim_miss) break;
-            }
-            const int seen = (G > 1) ? coop_load(&sa->misses) : __atomic_load_n(&sh.misses, __ATOMIC_RELAXED);
-            // (not unrolled: an unrolled copy of this loop spilled ~260 VGPRs)
-            if (seen <= lim_miss)  // not (yet) hopeless: this WG's share of the inlier ratio
+    unsigned long long acc = 0;
+    int cnt = 0, cin = 0;
+    for (;;) {
+        int c = 0;
+        if (lane == 0) c = atomicAdd(&sh.chunk, 1);
+        c = __shfl(c, 0, 64);
+        if (c >= nch) break;
+        const int k = (c << 6) + lane;
+        int j = 0;
+        if (k < n) {
+            const int i = ord ? ord[k] : k;
+            double px, py, pz, d2;
+            xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
+            j = grid_query(gr, a.d, a.thr, px, py, pz, d2);
+            if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
+            if (cbuf) cbuf[i] = j;
+        }
+        const int miss = __popcll(__ballot(k < n && j < 0));
+        int tot = 0;
+        if (lane == 0) tot = atomicAdd(&sh.misses, miss) + miss;
+        tot = __shfl(tot, 0, 64);
+        if (tot > lim_miss) break;
+    }
+    __syncthreads();  // every wave's misses are in: one cut decision for all
+    const bool cut = sh.misses > lim_miss;
+    // (not unrolled: an unrolled copy of this loop spilled ~260 VGPRs)
+    if (!cut)  // the inlier ratio over the correspondences (est_k of a new best)
 #pragma unroll 1
-                for (int q = g * kThreads + tid; q < K; q += G * kThreads) {
-                    const int si = co[2 * q], ti = co[2 * q + 1];
-                    double px, py, pz;
-                    xform12(Te, (double)S[3 * si], (double)S[3 * si + 1], (double)S[3 * si + 2], px, py, pz);
-                    if (dist2(px, py, pz, (double)Gt[3 * ti], (double)Gt[3 * ti + 1], (double)Gt[3 * ti + 2]) < a.dd)
-                        ++cin;
-                }
+        for (int q = tid; q < K; q += kThreads) {
+            const int si = co[2 * q], ti = co[2 * q + 1];
+            double px, py, pz;
+            xform12(Te, (double)S[3 * si], (double)S[3 * si + 1], (double)S[3 * si + 2], px, py, pz);
+            if (dist2(px, py, pz, (double)Gt[3 * ti], (double)Gt[3 * ti + 1], (double)Gt[3 * ti + 2]) < a.dd)
+                ++cin;
+        }
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                acc += __shfl_xor(acc, o, 64);
-                cnt += __shfl_xor(cnt, o, 64);
-                cin += __shfl_xor(cin, o, 64);
+    for (int o = 32; o >= 1; o >>= 1) {
+        acc += __shfl_xor(acc, o, 64);
+        cnt += __shfl_xor(cnt, o, 64);
+        cin += __shfl_xor(cin, o, 64);
+    }
+    if (lane == 0) { sh.racc[wid] = acc; sh.rcnt[wid] = cnt; sh.rcin[wid] = cin; }
+    __syncthreads();
+    TaskRes r{};
+    for (int w = 0; w < kWaves; ++w) { r.acc += sh.racc[w]; r.cnt += sh.rcnt[w]; r.cin += sh.rcin[w]; }
+    r.status = cut ? kCut : kDone;
+    __syncthreads();  // racc / chunk / misses are reused by the caller's next sweep
+    if (tid == 0) { sh.chunk = 0; sh.misses = 0; }
+    return r;
+}
+
+// Round setup, one wave per pair: the round-0 state, then the round's tasks =
+// the passing hypotheses below min(b1, max_iter, est_k), in iteration order.
+__global__ __launch_bounds__(64) void ransac_task_kernel(RArgs a, int RN) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    RState *sp = a.state + p;
+    if (a.b0 == 0 && lane == 0) {
+        RState s;
+        for (int k = 0; k < 12; ++k) s.bestT[k] = (k % 5 == 0) ? 1.0 : 0.0;
+        s.best_fit = 0.0; s.best_rmse = 0.0;
+        s.est_k = a.max_iter; s.best_itr = -1; s.validated = 0; s.last_upd = -1;
+        s.best_cnt = 0; s.fix = 0; s.pad = 0;
+        s.active = pair_ok(a, p, RN) ? 1 : 0;
+        *sp = s;
+    }
+    __syncthreads();
+    const RState &s = *sp;
+    int nt = 0;
+    if (s.active) {
+        const int lim = min(min(a.b1, a.max_iter), s.est_k) - a.b0;
+        const unsigned long long *bits = a.hypbits + (size_t)p * (a.hcap / 64);
+        int *tk = a.tasks + (size_t)p * a.hcap;
+        TaskRes *rs = a.res + (size_t)p * a.hcap;
+        for (int w0 = 0; w0 * 64 < lim; w0 += 64) {
+            const int w = w0 + lane;
+            unsigned long long word = (w * 64 < lim) ? bits[w] : 0ull;
+            if ((w + 1) * 64 > lim && w * 64 < lim) word &= (lim - w * 64 >= 64) ? ~0ull : ((1ull << (lim - w * 64)) - 1ull);
+            const int c = __popcll(word);
+            int pre = c;  // inclusive prefix over the lanes
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(pre, o, 64);
+                if (lane >= o) pre += v;
             }
-            if (lane == 0) { sh.racc[wid] = acc; sh.rcnt[wid] = cnt; sh.rcin[wid] = cin; }
-            __syncthreads();
-            unsigned long long A = 0;
-            int C = 0, CI = 0, MS = 0;
-            if (tid == 0) {
-                for (int ww = 0; ww < kWaves; ++ww) { A += sh.racc[ww]; C += sh.rcnt[ww]; CI += sh.rcin[ww]; }
-                if (G > 1) {
-                    __hip_atomic_fetch_add(&sa->acc, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    coop_fetch_add(&sa->cnt, C);
-                    coop_fetch_add(&sa->cin, CI);
-                } else {
-                    MS = sh.misses;
-                }
+            int at = nt + pre - c;
+            while (word) {
+                const int e = __builtin_ctzll(word);
+                word &= word - 1ull;
+                tk[at] = a.b0 + w * 64 + e;
+                TaskRes z{};
+                z.status = kPending;
+                rs[at] = z;
+                ++at;
             }
-            if (G > 1) {
-                pair_barrier(a.bar + 2 * (size_t)p, G);
-                if (tid == 0) {
-                    A = __hip_atomic_load(&sa->acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    C = coop_load(&sa->cnt);
-                    CI = coop_load(&sa->cin);
-                    MS = coop_load(&sa->misses);
-                }
-            }
-            if (tid == 0) {
-                RState &s = sh.st;
-                double fit = 0.0, rmse = 0.0;
-                if (C > 0) {
-                    fit = (double)C / (double)n;
-                    rmse = __builtin_sqrt(((double)A / scale) / (double)C);
-                }
-                const bool cut = MS > lim_miss;  // sweep stopped early: cannot win
-                s.validated += 1;
-                sh.chunk = 0;  // next sweep (published by the barrier below)
-                sh.misses = 0;
-                sh.nsweep += 1;
-                if (!cut && (fit > s.best_fit || (fit == s.best_fit && rmse < s.best_rmse))) {
-                    s.best_cnt = C;
-                    s.best_fit = fit;
-                    s.best_rmse = rmse;
-                    s.best_itr = itr_e;
-                    s.last_upd = itr_e;
-                    s.best_buf = s.cur_buf;  // its correspondences stay; the next sweep
-                    s.cur_buf ^= 1;          // writes the other buffer
-                    for (int k = 0; k < 12; ++k) s.bestT[k] = Te[k];
-                    const double kd = est_k_bound((double)CI / (double)K, RN, a.conf);
-                    if (kd < (double)s.est_k) s.est_k = (int)__builtin_ceil(kd);
-                }
-            }
-            if (G > 1) {
-                // the OTHER parity was last read before the previous sweep's second
-                // barrier: WG 0 clears it for the next sweep, and this barrier
-                // publishes both the clear and the decision
-                if (g == 0 && tid == 0) {
-                    SweepAcc *nx = a.sacc + (size_t)p * 2 + (sh.nsweep & 1);
-                    nx->acc = 0ull; nx->cnt = 0; nx->cin = 0; nx->misses = 0; nx->chunk = 0;
-                }
-                pair_barrier(a.bar + 2 * (size_t)p, G);
-            } else {
-                __syncthreads();
-            }
+            nt += __shfl(pre, 63, 64);
         }
     }
-    // round end: the pair is finished once the next iteration would be at or
-    // beyond min(max_iter, est_k)
+    if (lane == 0) {
+        a.ntask[p] = nt;
+        if (nt > 0) atomicMax(&a.hdr->maxtask, nt);
+    }
+}
+
+// Persistent sweep workgroups take tasks t = (rank r = t / P, pair p = t % P)
+// from a global counter: every pair's first hypothesis, then every pair's
+// second, ...  Each sweep is independent of the others; the sequential rule is
+// applied afterwards (ransac_replay_kernel).  Two exact shortcuts from the
+// tasks of the same pair that are already finished:
+//  * cut bound: a hypothesis with more than n - c misses, c = the inliers of
+//    any earlier finished hypothesis, is below the best at its turn (whose
+//    inliers are >= c): it cannot be accepted, so its sweep stops there;
+//  * skip: replaying the finished prefix of the pair's tasks gives an est_k
+//    that can only fall further; a task at or beyond it is never validated.
+template <bool kLds, int RN>
+__global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    Shared &sh = *reinterpret_cast<Shared *>(dsm);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int maxtask = a.hdr->maxtask;
+    const double scale = fx_scale(a.thr);
+    if (tid == 0) { sh.chunk = 0; sh.misses = 0; sh.gp = -1; }
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) sh.task = atomicAdd(&a.hdr->task_ctr, 1);
+        __syncthreads();
+        const int t = sh.task;
+        const int r = t / a.P, p = t - r * a.P;
+        if (r >= maxtask) break;
+        const int nt = a.ntask[p];
+        if (r >= nt) continue;
+        const int n = cnt_of(a.n_src, p, a.Nmax);
+        const int K = a.n_corres ? min(max(a.n_corres[p], 0), a.Kmax) : a.Kmax;
+        const int *tk = a.tasks + (size_t)p * a.hcap;
+        TaskRes *rs = a.res + (size_t)p * a.hcap;
+        const int itr = tk[r];
+        if (wid == 0) {  // cut bound and skip test from the finished prefix
+            RState s = a.state[p];
+            int lb = s.best_cnt;
+            bool replay = true, skip = false;
+            for (int b = 0; b < r && replay && !skip; b += 64) {
+                const int rr = b + lane;
+                int st = kPending, c = 0, ci = 0, it = 0;
+                unsigned long long ac = 0;
+                if (rr < r) {
+                    st = __hip_atomic_load(&rs[rr].status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (st == kDone || st == kCut) { c = rs[rr].cnt; ci = rs[rr].cin; ac = rs[rr].acc; }
+                    it = tk[rr];
+                    if (st == kDone) lb = max(lb, c);
+                }
+                const int m = min(64, r - b);
+                for (int e = 0; e < m; ++e) {
+                    const int ste = __shfl(st, e, 64), ite = __shfl(it, e, 64);
+                    if (ste == kPending) { replay = false; break; }
+                    if (ste == kSkipped || ite >= s.est_k) { skip = true; break; }
+                    TaskRes tr;
+                    tr.status = ste;
+                    tr.cnt = __shfl(c, e, 64);
+                    tr.cin = __shfl(ci, e, 64);
+                    tr.acc = __shfl(ac, e, 64);
+                    apply_result(s, ite, tr, nullptr, n, K, scale, a.conf, RN);
+                }
+            }
+            if (!skip && itr >= s.est_k) skip = true;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) lb = max(lb, __shfl_xor(lb, o, 64));
+            if (lane == 0) { sh.lb = lb; sh.skip = skip ? 1 : 0; }
+        }
+        if (tid < 12) sh.Te[tid] = a.hypT[((size_t)p * a.hcap + (itr - a.b0)) * 12 + tid];
+        __syncthreads();
+        if (sh.skip) {
+            if (tid == 0) __hip_atomic_store(&rs[r].status, kSkipped, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        char *glds = dsm + ((sizeof(Shared) + 15) & ~size_t(15));
+        if (kLds && sh.gp != p) {  // this pair's grid into LDS (kept while the next task is the same pair)
+            (void)grid_to_lds(a.grid, p, cnt_of(a.n_tgt, p, a.Mmax), glds);
+            if (tid == 0) sh.gp = p;
+        }
+        double Te[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Te[k] = sh.Te[k];
+        const int lim_miss = sh.lb > 0 ? n - sh.lb : 0x7fffffff;
+        int32_t *cbuf = r < a.nslots ? a.slots + ((size_t)p * a.nslots + r) * a.Nmax : nullptr;
+        TaskRes out;
+        if constexpr (kLds) out = sweep_pair<kLds, RN>(a, sh, grid_lds_view(a.grid, glds), p, n, K, Te, lim_miss, cbuf);
+        else out = sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, lim_miss, cbuf);
+        if (tid == 0) {
+            rs[r].acc = out.acc;
+            rs[r].cnt = out.cnt;
+            rs[r].cin = out.cin;
+        }
+        // every thread's target stores and thread 0's result before the status
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_store(&rs[r].status, out.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// One workgroup per pair: the sequential loop over the round's sweep results
+// (exactly oracle_ransac's order of decisions), the best hypothesis' targets
+// kept, and -- once the pair is finished -- its outputs.
+template <bool kLds, int RN>
+__global__ __launch_bounds__(kThreads) void ransac_replay_kernel(RArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    Shared &sh = *reinterpret_cast<Shared *>(dsm);
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int n = cnt_of(a.n_src, p, a.Nmax), m = cnt_of(a.n_tgt, p, a.Mmax);
+    const int K = a.n_corres ? min(max(a.n_corres[p], 0), a.Kmax) : a.Kmax;
+    const bool ok = pair_ok(a, p, RN);
     if (tid == 0) {
-        RState &s = sh.st;
+        RState s = a.state[p];
+        const bool was_active = s.active != 0 || a.b0 == 0;  // round 0 finishes invalid pairs
+        int best_r = -1;
+        if (was_active && s.active) {
+            const double scale = fx_scale(a.thr);
+            const int nt = a.ntask[p];
+            const int *tk = a.tasks + (size_t)p * a.hcap;
+            const TaskRes *rs = a.res + (size_t)p * a.hcap;
+            for (int r = 0; r < nt; ++r) {
+                const int itr = tk[r];
+                if (itr >= s.est_k) break;
+                const TaskRes tr = rs[r];
+                if (tr.status != kDone && tr.status != kCut) {  // cannot happen: guarded
+                    atomicAdd(&a.hdr->bad, 1);
+                    break;
+                }
+                const double *T = a.hypT + ((size_t)p * a.hcap + (itr - a.b0)) * 12;
+                if (apply_result(s, itr, tr, T, n, K, scale, a.conf, RN)) best_r = r;
+            }
+            if (best_r >= 0) s.fix = best_r < a.nslots ? 0 : 1;
+        }
         const bool fin = !ok || a.b1 >= min(a.max_iter, s.est_k);
-        s.active = fin ? 0 : 1;
-        sh.done = fin ? 1 : 0;
-        if (g == 0) {
+        if (was_active) {
+            s.active = fin ? 0 : 1;
             a.state[p] = s;
-            if (!fin) atomicAdd(a.active_count, 1);
+            if (!fin) atomicAdd(&a.hdr->active_count, 1);
+        }
+        sh.st = s;
+        sh.best_r = best_r;
+        sh.done = (was_active && fin) ? 1 : 0;
+        sh.chunk = 0;
+        sh.misses = 0;
+    }
+    __syncthreads();
+    const int best_r = sh.best_r;
+    int32_t *bb = a.bestbuf + (size_t)p * a.Nmax;
+    if (best_r >= 0 && best_r < a.nslots) {  // the new best's targets leave the round's slots
+        const int32_t *sl = a.slots + ((size_t)p * a.nslots + best_r) * a.Nmax;
+        for (int i = tid; i < n; i += kThreads) bb[i] = sl[i];
+    }
+    if (!sh.done) return;
+    const RState &s = sh.st;
+    const bool found = ok && s.best_itr >= 0;
+    if (found && s.fix) {  // the best had no slot: sweep it once more for its targets
+        double Te[12];
+        for (int k = 0; k < 12; ++k) Te[k] = s.bestT[k];
+        if constexpr (kLds) {
+            const GridT<uint16_t> gl = grid_to_lds(a.grid, p, m, dsm + ((sizeof(Shared) + 15) & ~size_t(15)));
+            (void)sweep_pair<kLds, RN>(a, sh, gl, p, n, K, Te, 0x7fffffff, bb);
+        } else {
+            (void)sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, 0x7fffffff, bb);
         }
     }
     __syncthreads();
-    if (!sh.done) return;
     // outputs.  Loop exit iteration of the sequential algorithm: first itr >=
     // est_k after the last bound update (or max_iter)
-    const RState &s = sh.st;
     const int iters = ok ? min(a.max_iter, max(s.last_upd + 1, s.est_k)) : 0;
-    const bool found = ok && s.best_itr >= 0;
-    // correspondence set of the best transformation: the targets its validation
-    // sweep found (a sweep that became the best ran to completion)
-    const int32_t *bbuf = a.cand + ((size_t)p * 2 + s.best_buf) * a.Nmax;
     if (a.corr_tgt)
-        for (int i = g * kThreads + tid; i < a.Nmax; i += G * kThreads)
-            a.corr_tgt[(size_t)p * a.Nmax + i] = (found && i < n) ? bbuf[i] : -1;
+        for (int i = tid; i < a.Nmax; i += kThreads)
+            a.corr_tgt[(size_t)p * a.Nmax + i] = (found && i < n) ? bb[i] : -1;
     if (a.mask)
-        for (int w = g * kThreads + tid; w < a.words; w += G * kThreads) {
+        for (int w = tid; w < a.words; w += kThreads) {
             uint32_t bitsw = 0u;
             if (found)
                 for (int b = 0; b < 32; ++b) {
                     const int i = 32 * w + b;
-                    if (i < n && bbuf[i] >= 0) bitsw |= 1u << b;
+                    if (i < n && bb[i] >= 0) bitsw |= 1u << b;
                 }
             a.mask[(size_t)p * a.words + w] = bitsw;
         }
-    if (g == 0 && tid == 0) {
+    if (tid == 0) {
         double *Tp = a.T_out + (size_t)p * 16;
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 4; ++c) Tp[4 * r + c] = s.bestT[4 * r + c];
@@ -423,8 +563,14 @@ template <int RN>
 const void *hyp_fn() { return (const void *)ransac_hyp_kernel<RN>; }
 
 template <int RN>
-const void *val_fn(bool lds) {
-    return lds ? (const void *)ransac_val_kernel<true, RN> : (const void *)ransac_val_kernel<false, RN>;
+void val_fns(bool lds, const void **sweep, const void **replay) {
+    *sweep = lds ? (const void *)ransac_sweep_kernel<true, RN> : (const void *)ransac_sweep_kernel<false, RN>;
+    *replay = lds ? (const void *)ransac_replay_kernel<true, RN> : (const void *)ransac_replay_kernel<false, RN>;
+}
+
+int env_int(const char *name, int dflt) {  // test hooks (PCR_RANSAC_WGS / _SLOTS)
+    const char *e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
 }
 
 }  // namespace
@@ -439,7 +585,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     PCR_REQUIRE(prm->max_iteration >= 0, PCR_ERR_ARG, "ransac: negative max_iteration");
     RArgs a;
     a.src = src; a.tgt = tgt; a.n_src = n_src; a.n_tgt = n_tgt; a.corres = corres;
-    a.n_corres = n_corres; a.pair_ids = pair_ids; a.Nmax = Nmax; a.Mmax = Mmax; a.Kmax = Kmax;
+    a.n_corres = n_corres; a.pair_ids = pair_ids; a.P = P; a.Nmax = Nmax; a.Mmax = Mmax; a.Kmax = Kmax;
     a.d = prm->max_correspondence_distance;
     a.thr = radius_thr(a.d);
     a.dd = a.d * a.d;
@@ -453,17 +599,24 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.words = (Nmax + 31) / 32;
     a.order = nullptr;
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
-    a.cand = (int32_t *)workspace(21, sizeof(int32_t) * 2 * (size_t)P * nm);
-    PCR_REQUIRE(a.cand, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
     a.hcap = kRoundN;  // >= kRound0, multiple of 256
+    // target slots of the first tasks of every pair (the best's are kept from
+    // there; a best without one is swept again at the end): up to 32 per pair
+    // within 256 MB
+    const size_t per = sizeof(int32_t) * (size_t)P * nm;
+    a.nslots = (int)std::min<size_t>(32, ((size_t)256 << 20) / per);
+    a.nslots = std::max(0, std::min(a.nslots, env_int("PCR_RANSAC_SLOTS", a.nslots)));
+    a.bestbuf = (int32_t *)workspace(21, per);
     a.state = (RState *)workspace(22, sizeof(RState) * (size_t)P);
     a.hypT = (double *)workspace(23, sizeof(double) * 12 * (size_t)P * a.hcap);
     a.hypbits = (unsigned long long *)workspace(24, sizeof(unsigned long long) * (size_t)P * (a.hcap / 64));
-    char *misc = (char *)workspace(25, (sizeof(SweepAcc) * 2 + sizeof(unsigned) * 2) * (size_t)P + 256);
-    PCR_REQUIRE(a.state && a.hypT && a.hypbits && misc, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
-    a.active_count = (int *)misc;
-    a.sacc = (SweepAcc *)(misc + 256);
-    a.bar = (unsigned *)(misc + 256 + sizeof(SweepAcc) * 2 * (size_t)P);
+    a.hdr = (RHeader *)workspace(25, sizeof(RHeader) + sizeof(int) * (size_t)P);
+    a.tasks = (int *)workspace(29, sizeof(int) * (size_t)P * a.hcap);
+    a.res = (TaskRes *)workspace(30, sizeof(TaskRes) * (size_t)P * a.hcap);
+    a.slots = (int32_t *)workspace(31, a.nslots > 0 ? per * a.nslots : 16);
+    PCR_REQUIRE(a.bestbuf && a.state && a.hypT && a.hypbits && a.hdr && a.tasks && a.res && a.slots,
+                PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
+    a.ntask = (int *)(a.hdr + 1);
     a.grid = GridBatch{};
     a.grid.S = 1;
     a.grid.cell = 1.0;
@@ -480,49 +633,56 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds_bytes(Mmax, a.grid.S, budget) : 0;
     const bool lds = gbytes > 0;
     const size_t sm = lds ? hdr + gbytes : hdr;
-    const void *hfn = nullptr, *vfn = nullptr;
+    const void *hfn = nullptr, *sfn = nullptr, *rfn = nullptr;
     switch (a.rn) {
 #define PCR_RCASE(N)                  \
     case N:                           \
         hfn = hyp_fn<N>();            \
-        vfn = val_fn<N>(lds);         \
+        val_fns<N>(lds, &sfn, &rfn);  \
         break;
         PCR_RCASE(3) PCR_RCASE(4) PCR_RCASE(5) PCR_RCASE(6) PCR_RCASE(7) PCR_RCASE(8)
 #undef PCR_RCASE
         default: set_error("ransac: bad ransac_n"); return PCR_ERR_ARG;
     }
-    PCR_HIP_CHECK(hipFuncSetAttribute(vfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vfn, kThreads, sm) != hipSuccess) {
+    PCR_HIP_CHECK(hipFuncSetAttribute(sfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+    PCR_HIP_CHECK(hipFuncSetAttribute(rfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sfn, kThreads, sm) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
         (void)hipGetLastError();
-        per_cu = 0;
+        per_cu = 1;
+        cus = 1;
     }
-    a.G = coop_groups(P, per_cu);
+    const int nwg = std::max(1, env_int("PCR_RANSAC_WGS", std::max(1, per_cu) * std::max(1, cus)));
+    const int rnarg = a.rn;
     prof_begin(s, kProfRansacValidate);
     // rounds: [0, kRound0), then kRoundN at a time while a pair is still running
     a.b0 = 0;
     a.b1 = std::min(a.max_iter, kRound0);
     for (;;) {
-        PCR_HIP_CHECK(hipMemsetAsync(a.active_count, 0, sizeof(int), s));
+        PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, sizeof(RHeader), s));
         const int span = a.b1 - a.b0;
+        void *args[] = {&a};
         if (span > 0) {
-            void *args[] = {&a};
             PCR_HIP_CHECK(hipLaunchKernel(hfn, dim3((span + kHypThreads - 1) / kHypThreads, P),
                                           dim3(kHypThreads), args, 0, s));
             PCR_LAUNCH_CHECK();
         }
         {
-            if (a.G > 1)  // split-sweep accumulators (both parities) and barriers
-                PCR_HIP_CHECK(hipMemsetAsync(a.sacc, 0, (sizeof(SweepAcc) * 2 + sizeof(unsigned) * 2) * (size_t)P, s));
-            void *args[] = {&a};
-            PCR_HIP_CHECK(coop_launch(vfn, P, a.G, kThreads, args, sm, s));
+            void *targs[] = {&a, (void *)&rnarg};
+            PCR_HIP_CHECK(hipLaunchKernel((const void *)ransac_task_kernel, dim3(P), dim3(64), targs, 0, s));
             PCR_LAUNCH_CHECK();
         }
-        if (a.b1 >= a.max_iter) break;
-        int active = 0;
-        PCR_HIP_CHECK(hipMemcpyAsync(&active, a.active_count, sizeof(int), hipMemcpyDeviceToHost, s));
+        PCR_HIP_CHECK(hipLaunchKernel(sfn, dim3(nwg), dim3(kThreads), args, sm, s));
+        PCR_LAUNCH_CHECK();
+        PCR_HIP_CHECK(hipLaunchKernel(rfn, dim3(P), dim3(kThreads), args, sm, s));
+        PCR_LAUNCH_CHECK();
+        RHeader h;
+        PCR_HIP_CHECK(hipMemcpyAsync(&h, a.hdr, sizeof(RHeader), hipMemcpyDeviceToHost, s));
         PCR_HIP_CHECK(hipStreamSynchronize(s));
-        if (active == 0) break;
+        PCR_REQUIRE(h.bad == 0, PCR_ERR_HIP, "ransac: %d pairs met an unswept task", h.bad);
+        if (a.b1 >= a.max_iter || h.active_count == 0) break;
         a.b0 = a.b1;
         a.b1 = std::min(a.max_iter, a.b0 + kRoundN);
     }

@@ -1,10 +1,18 @@
-"""Several workgroups per pair (coop.h): RANSAC verification sweeps and ICP
-iterations split over G = 1, 2, 4, 8 workgroups of a cooperative launch must give
-the oracle's results bit for bit -- the split only changes who adds which integer
-partial.  PCR_COOP_G forces the split (the library picks G from the batch size:
-G > 1 only when the pairs alone cannot fill the CUs, e.g. 32 pairs per GPU at 8
-GPUs).  Also: ICP past its position checkpoint (> 8 iterations) and clouds with
-more points than a split's threads."""
+"""Scheduling must not change any bit.
+
+RANSAC: the verification sweeps of all pairs run speculatively on persistent
+workgroups (ransac.hip); the sequential rule is replayed afterwards.  Whatever the
+number of workgroups (PCR_RANSAC_WGS: 1 = every task in order on one workgroup,
+where the skip/cut shortcuts see every earlier result) and of target slots
+(PCR_RANSAC_SLOTS: 0 = the best hypothesis' targets always come from one more
+sweep), the results equal the oracle's sequential loop bit for bit.
+
+ICP: iterations split over G = 1, 2, 4, 8 workgroups of a cooperative launch
+(coop.h) must give the oracle's results bit for bit -- the split only changes who
+adds which integer partial.  PCR_COOP_G forces the split (the library picks G from
+the batch size: G > 1 only when the pairs alone cannot fill the CUs, e.g. 32 pairs
+per GPU at 8 GPUs).  Also: ICP past its position checkpoint (> 8 iterations) and
+clouds with more points than a split's threads."""
 import os
 
 import numpy as np
@@ -38,11 +46,30 @@ def coop_g():
         os.environ["PCR_COOP_G"] = old
 
 
-@pytest.mark.parametrize("G", [1, 2, 4, 8])
-def test_ransac_split_bitexact_vs_oracle(oracle, coop_g, G):
+@pytest.fixture()
+def ransac_sched():
+    keys = ("PCR_RANSAC_WGS", "PCR_RANSAC_SLOTS")
+    old = {k: os.environ.get(k) for k in keys}
+
+    def set_sched(wgs, slots):
+        for k, v in zip(keys, (wgs, slots)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+    yield set_sched
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+@pytest.mark.parametrize("wgs,slots", [(None, None), (1, None), (2, 1), (None, 0), (3, 2)])
+def test_ransac_speculative_bitexact_vs_oracle(oracle, ransac_sched, wgs, slots):
     P, n = 3, 4096
     B = synth.make_batch(P, n=n, m=n, d=32, base_seed=2000, feat_noise=1.0)
-    coop_g(G)
+    ransac_sched(wgs, slots)
     prm = reg.RansacParams(max_correspondence_distance=0.04, seed=7)
     res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm,
                                             pair_ids=np.arange(P, dtype=np.int32) + 9)
@@ -61,13 +88,13 @@ def test_ransac_split_bitexact_vs_oracle(oracle, coop_g, G):
         assert np.array_equal(np.nonzero(bits)[0], cs[:, 0]) and st[p, 4] == len(cs)
 
 
-def test_ransac_multi_round_low_inlier_ratio(oracle, coop_g):
+def test_ransac_multi_round_low_inlier_ratio(oracle, ransac_sched):
     """Noisy descriptors -> a low inlier ratio -> est_k beyond the first round of
     1024 hypotheses: the later rounds continue the same sequential loop."""
     P, n = 2, 2048
     B = synth.make_batch(P, n=n, m=n, d=32, base_seed=3100, feat_noise=2.2)
-    for G in (1, 4):
-        coop_g(G)
+    for wgs, slots in ((None, None), (1, 0), (5, 3)):
+        ransac_sched(wgs, slots)
         prm = reg.RansacParams(max_correspondence_distance=0.04, seed=3, max_iteration=6000)
         res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm)
         st = _np(res.stats)
@@ -77,6 +104,9 @@ def test_ransac_multi_round_low_inlier_ratio(oracle, coop_g):
             r = oracle.ransac(B.src[p], B.tgt[p], co, 0.04, seed=3, pair_id=p, max_iteration=6000)
             assert _bits(_np(res.transformation)[p], r["T"])
             assert (st[p, 0], st[p, 1], st[p, 2]) == (r["iters"], r["validated"], r["best_itr"])
+            cs, ct = r["correspondence_set"], _np(res.corr_tgt)
+            got = np.nonzero(ct[p] >= 0)[0]
+            assert np.array_equal(got, cs[:, 0]) and np.array_equal(ct[p, got], cs[:, 1])
         assert st[:, 0].max() > 1024, st[:, 0]
 
 
