@@ -36,6 +36,7 @@
 #include "geom.h"
 #include "grid.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -75,6 +76,7 @@ struct RHeader {
     int maxtask;       // max tasks of one pair in this round
     int active_count;  // pairs still active after the round
     int bad;           // replay met a task it needed that was never swept (bug guard)
+    int n_done, n_cut, n_skip, n_chunks;  // diagnostics (PCR_RANSAC_STATS=1 prints them)
 };
 
 struct RArgs {
@@ -248,11 +250,16 @@ __device__ inline bool apply_result(RState &s, int itr, const TaskRes &r, const 
 
 // One workgroup sweeps every source point of pair p under Te: inliers, exact
 // fixed-point error sum and (unless cut) the inlier correspondences, in
-// 64-query chunks of the spatial order taken from an LDS counter.  The sweep
-// stops once its misses exceed lim_miss.  cbuf (may be null): target per source.
+// 64-query chunks of the spatial order taken from an LDS counter.  Cut bound:
+// sh.lb (set by the caller; 0 = none) -- the sweep stops once its misses exceed
+// n - lb.  With prs (the pair's tasks of lower rank, npr of them) every wave
+// polls their finished inlier counts every 4 chunks and raises the bound.
+// cbuf (may be null): target per point, by position k in the sweep order
+// (coalesced stores) when by_order, else by source index.
 template <bool kLds, int RN, typename Grid>
 __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p, int n, int K,
-                              const double *Te, int lim_miss, int32_t *cbuf) {
+                              const double *Te, const TaskRes *prs, int npr, int32_t *cbuf,
+                              bool by_order) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
@@ -262,7 +269,8 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
     const int nch = (n + 63) >> 6;
     unsigned long long acc = 0;
     int cnt = 0, cin = 0;
-    for (;;) {
+    int lb = sh.lb;
+    for (int nc = 1;; ++nc) {
         int c = 0;
         if (lane == 0) c = atomicAdd(&sh.chunk, 1);
         c = __shfl(c, 0, 64);
@@ -275,16 +283,30 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
             xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
             j = grid_query(gr, a.d, a.thr, px, py, pz, d2);
             if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
-            if (cbuf) cbuf[i] = j;
+            if (cbuf) cbuf[by_order ? k : i] = j;
         }
         const int miss = __popcll(__ballot(k < n && j < 0));
         int tot = 0;
         if (lane == 0) tot = atomicAdd(&sh.misses, miss) + miss;
         tot = __shfl(tot, 0, 64);
-        if (tot > lim_miss) break;
+        if ((nc & 3) == 0 && npr > 0) {  // earlier tasks finished meanwhile: a higher bound
+            int c2 = 0;
+            if (lane < npr &&
+                __hip_atomic_load(&prs[lane].status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == kDone)
+                c2 = prs[lane].cnt;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) c2 = max(c2, __shfl_xor(c2, o, 64));
+            if (c2 > lb) {
+                lb = c2;
+                if (lane == 0) atomicMax(&sh.lb, lb);
+            }
+        }
+        if (lb > 0 && tot > n - lb) break;
     }
-    __syncthreads();  // every wave's misses are in: one cut decision for all
-    const bool cut = sh.misses > lim_miss;
+    // every wave's misses and bound are in: one cut decision for all (a wave
+    // that stopped saw misses above n - its bound >= n - the final bound)
+    __syncthreads();
+    const bool cut = sh.lb > 0 && sh.misses > n - sh.lb;
     // (not unrolled: an unrolled copy of this loop spilled ~260 VGPRs)
     if (!cut)  // the inlier ratio over the correspondences (est_k of a new best)
 #pragma unroll 1
@@ -303,6 +325,7 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
     }
     if (lane == 0) { sh.racc[wid] = acc; sh.rcnt[wid] = cnt; sh.rcin[wid] = cin; }
     __syncthreads();
+    if (tid == 0) atomicAdd(&a.hdr->n_chunks, min(sh.chunk, nch));
     TaskRes r{};
     for (int w = 0; w < kWaves; ++w) { r.acc += sh.racc[w]; r.cnt += sh.rcnt[w]; r.cin += sh.rcin[w]; }
     r.status = cut ? kCut : kDone;
@@ -430,7 +453,10 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
         if (tid < 12) sh.Te[tid] = a.hypT[((size_t)p * a.hcap + (itr - a.b0)) * 12 + tid];
         __syncthreads();
         if (sh.skip) {
-            if (tid == 0) __hip_atomic_store(&rs[r].status, kSkipped, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) {
+                __hip_atomic_store(&rs[r].status, kSkipped, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd(&a.hdr->n_skip, 1);
+            }
             continue;
         }
         char *glds = dsm + ((sizeof(Shared) + 15) & ~size_t(15));
@@ -441,12 +467,12 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
         double Te[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) Te[k] = sh.Te[k];
-        const int lim_miss = sh.lb > 0 ? n - sh.lb : 0x7fffffff;
         int32_t *cbuf = r < a.nslots ? a.slots + ((size_t)p * a.nslots + r) * a.Nmax : nullptr;
         TaskRes out;
-        if constexpr (kLds) out = sweep_pair<kLds, RN>(a, sh, grid_lds_view(a.grid, glds), p, n, K, Te, lim_miss, cbuf);
-        else out = sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, lim_miss, cbuf);
+        if constexpr (kLds) out = sweep_pair<kLds, RN>(a, sh, grid_lds_view(a.grid, glds), p, n, K, Te, rs, r, cbuf, true);
+        else out = sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, rs, r, cbuf, true);
         if (tid == 0) {
+            atomicAdd(out.status == kCut ? &a.hdr->n_cut : &a.hdr->n_done, 1);
             rs[r].acc = out.acc;
             rs[r].cnt = out.cnt;
             rs[r].cin = out.cin;
@@ -505,13 +531,15 @@ __global__ __launch_bounds__(kThreads) void ransac_replay_kernel(RArgs a) {
         sh.done = (was_active && fin) ? 1 : 0;
         sh.chunk = 0;
         sh.misses = 0;
+        sh.lb = 0;
     }
     __syncthreads();
     const int best_r = sh.best_r;
     int32_t *bb = a.bestbuf + (size_t)p * a.Nmax;
     if (best_r >= 0 && best_r < a.nslots) {  // the new best's targets leave the round's slots
         const int32_t *sl = a.slots + ((size_t)p * a.nslots + best_r) * a.Nmax;
-        for (int i = tid; i < n; i += kThreads) bb[i] = sl[i];
+        const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
+        for (int k = tid; k < n; k += kThreads) bb[ord ? ord[k] : k] = sl[k];  // slots are in sweep order
     }
     if (!sh.done) return;
     const RState &s = sh.st;
@@ -521,9 +549,9 @@ __global__ __launch_bounds__(kThreads) void ransac_replay_kernel(RArgs a) {
         for (int k = 0; k < 12; ++k) Te[k] = s.bestT[k];
         if constexpr (kLds) {
             const GridT<uint16_t> gl = grid_to_lds(a.grid, p, m, dsm + ((sizeof(Shared) + 15) & ~size_t(15)));
-            (void)sweep_pair<kLds, RN>(a, sh, gl, p, n, K, Te, 0x7fffffff, bb);
+            (void)sweep_pair<kLds, RN>(a, sh, gl, p, n, K, Te, nullptr, 0, bb, false);
         } else {
-            (void)sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, 0x7fffffff, bb);
+            (void)sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, nullptr, 0, bb, false);
         }
     }
     __syncthreads();
@@ -656,6 +684,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     }
     const int nwg = std::max(1, env_int("PCR_RANSAC_WGS", std::max(1, per_cu) * std::max(1, cus)));
     const int rnarg = a.rn;
+    const bool stats_env = env_int("PCR_RANSAC_STATS", 0) != 0;
     prof_begin(s, kProfRansacValidate);
     // rounds: [0, kRound0), then kRoundN at a time while a pair is still running
     a.b0 = 0;
@@ -682,6 +711,10 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
         PCR_HIP_CHECK(hipMemcpyAsync(&h, a.hdr, sizeof(RHeader), hipMemcpyDeviceToHost, s));
         PCR_HIP_CHECK(hipStreamSynchronize(s));
         PCR_REQUIRE(h.bad == 0, PCR_ERR_HIP, "ransac: %d pairs met an unswept task", h.bad);
+        if (stats_env)
+            fprintf(stderr, "ransac round [%d,%d): tasks done %d cut %d skipped %d, chunks %d (%.2f full sweeps)\n",
+                    a.b0, a.b1, h.n_done, h.n_cut, h.n_skip, h.n_chunks,
+                    h.n_chunks / (double)std::max(1, (Nmax + 63) / 64));
         if (a.b1 >= a.max_iter || h.active_count == 0) break;
         a.b0 = a.b1;
         a.b1 = std::min(a.max_iter, a.b0 + kRoundN);
