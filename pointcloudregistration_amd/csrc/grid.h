@@ -78,16 +78,24 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
         // a wave runs as long as its longest lane's TOTAL, not the sum over cells
         // of each cell's longest lane (the nested cell / slot loops did that).
         // q[k] = (lo | hi << 16) of the k-th non-empty range, queued from q[0].
+        // per-axis box gaps and hash terms of the (up to) two cells per axis, computed
+        // once (the cell test below adds them in the same order, (gx + gy) + gz)
+        const double gx[2] = {cell_gap(px, x0, g.cell), cell_gap(px, x0 + 1, g.cell)};
+        const double gy[2] = {cell_gap(py, y0, g.cell), cell_gap(py, y0 + 1, g.cell)};
+        const double gz[2] = {cell_gap(pz, z0, g.cell), cell_gap(pz, z0 + 1, g.cell)};
+        const unsigned hx[2] = {(unsigned)x0 * 73856093u, (unsigned)(x0 + 1) * 73856093u};
+        const unsigned hy[2] = {(unsigned)y0 * 19349663u, (unsigned)(y0 + 1) * 19349663u};
+        const unsigned hz[2] = {(unsigned)z0 * 83492791u, (unsigned)(z0 + 1) * 83492791u};
         unsigned q[8];
         int nq = 0, total = 0;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const int x = x0 + (c >> 2), y = y0 + ((c >> 1) & 1), z = z0 + (c & 1);
-            const bool in = x <= x1 && y <= y1 && z <= z1 &&
-                            cell_gap(px, x, g.cell) + cell_gap(py, y, g.cell) + cell_gap(pz, z, g.cell) <= lim;
+            const int ix = c >> 2, iy = (c >> 1) & 1, iz = c & 1;
+            const bool in = x0 + ix <= x1 && y0 + iy <= y1 && z0 + iz <= z1 &&
+                            gx[ix] + gy[iy] + gz[iz] <= lim;
             q[c] = 0u;
             if (in) {
-                const unsigned h = cell_hash(x, y, z, g.S);
+                const unsigned h = (hx[ix] ^ hy[iy] ^ hz[iz]) & (unsigned)(g.S - 1);
                 const int lo = (int)g.start[h], hi = (int)g.start[h + 1];
                 if (hi > lo) {
                     // compact: the k-th non-empty range goes to q[k]
@@ -100,29 +108,22 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
             }
         }
         int s = (int)(q[0] & 0xffffu), e = (int)(q[0] >> 16);
-        auto advance = [&]() {  // next range: shift the queue down by one
-#pragma unroll
-            for (int k = 0; k < 7; ++k) q[k] = q[k + 1];
-            q[7] = 0u;
-            s = (int)(q[0] & 0xffffu);
-            e = (int)(q[0] >> 16);
-        };
+        // up to two candidates per step, both from the current range (one site
+        // shifts the queue: a wave pays the shift once per step, not twice)
         while (total > 0) {
-            // two candidates: (s, s + 1) in this range, or s and the next range's first
             const int sa = s;
-            int sb;
-            if (s + 1 < e) {
-                sb = s + 1;
-                s += 2;
-            } else {
-                advance();
-                sb = s;
-                ++s;
+            const bool hb = s + 1 < e;
+            const int sbb = hb ? s + 1 : s;
+            s += hb ? 2 : 1;
+            total -= hb ? 2 : 1;
+            if (s >= e) {  // next range: shift the queue down by one
+#pragma unroll
+                for (int k = 0; k < 7; ++k) q[k] = q[k + 1];
+                q[7] = 0u;
+                s = (int)(q[0] & 0xffffu);
+                e = (int)(q[0] >> 16);
             }
-            const bool hb = total >= 2;
-            if (s >= e && total > 2) advance();
             const float ax = g.x[sa], ay = g.y[sa], az = g.z[sa];
-            const int sbb = hb ? sb : sa;
             const float bx = g.x[sbb], by = g.y[sbb], bz = g.z[sbb];
             const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
             const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
@@ -134,7 +135,6 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
                 const int j = (int)g.idx[sbb];
                 if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = sbb; }
             }
-            total -= hb ? 2 : 1;
         }
     } else {
         for (int x = x0; x <= x1; ++x) {
