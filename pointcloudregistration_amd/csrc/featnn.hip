@@ -338,6 +338,13 @@ __device__ __forceinline__ float vmin(float a, float b) {
     asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
     return d;
 }
+// a NaN operand yields the other value: the pair's second value then equals its
+// first (a tie), which only fails certification (exact rescan)
+__device__ __forceinline__ float vmax(float a, float b) {
+    float d;
+    asm("v_max_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
 __device__ __forceinline__ float vmed3(float a, float b, float c) {
     float d;
     asm("v_med3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
@@ -409,7 +416,9 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
             const int q = r & 3;
             if (r < 4) {
                 c1[q] = vc;
-                c2[q] = __builtin_inff();
+            } else if (r < 8) {  // top-2 of two values: no +inf to stage (4 v_mov per tile)
+                c2[q] = vmax(c1[q], vc);
+                c1[q] = vmin(c1[q], vc);
             } else {
                 c2[q] = vmed3(c1[q], c2[q], vc);
                 c1[q] = vmin(c1[q], vc);
@@ -424,17 +433,20 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
         float m2 = vmin(c2[0], c2[2]);
         c2[0] = vmed3(c1[0], c1[2], m2);
         c1[0] = vmin(c1[0], c1[2]);
-        // the other half-wave's column state without LDS (a ds_bpermute here
-        // would share lgkmcnt with the B-fragment reads in flight): after the
-        // swap, lanes 0-31 of s1[1] / s2[1] hold lanes 32-63 of c1 / c2
-        const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(c1[0]),
-                                                         __float_as_uint(c1[0]), false, false);
-        const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(c2[0]),
+        // merge with the other half-wave without LDS (a ds_bpermute here would share
+        // lgkmcnt with the B-fragment reads in flight).  One swap of (c1, c2)
+        // leaves lanes 0-31 with (own c1, other c1) and lanes 32-63 with
+        // (own c2, other c2): their min is the new c1 below and min(c2, c2')
+        // above, which a second swap brings down for the med3 -- 5 VALU, where
+        // swapping c1 and c2 separately needed 4 copies more.
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(c1[0]),
                                                          __float_as_uint(c2[0]), false, false);
-        const float o1 = __uint_as_float(s1[1]), o2 = __uint_as_float(s2[1]);
-        m2 = vmin(c2[0], o2);
-        c2[0] = vmed3(c1[0], o1, m2);
-        c1[0] = vmin(c1[0], o1);
+        const float lo = __uint_as_float(sw[0]), up = __uint_as_float(sw[1]);
+        const float mm = vmin(lo, up);
+        const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mm), __float_as_uint(mm),
+                                                          false, false);
+        c2[0] = vmed3(lo, up, __uint_as_float(sw2[1]));
+        c1[0] = mm;
         if (h == 0) {
             const int e = pe * (W * 32) + wid * 32 + l;
             Pc1[e] = c1[0];
