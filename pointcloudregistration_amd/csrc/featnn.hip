@@ -366,9 +366,11 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
     constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
     constexpr int kP = G * W * 32;
     __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 2 * 2 * kP * 4];
-    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem);
-    float *Pc1 = reinterpret_cast<float *>(smem + 2 * kB * 16);  // [2][G][W waves][32 cols]
+    // column partials first: their per-tile stores then fit the ds_write
+    // immediate offset (below 64 KiB), the B buffers follow
+    float *Pc1 = reinterpret_cast<float *>(smem);  // [2][G][W waves][32 cols]
     float *Pc2 = Pc1 + 2 * kP;
+    f16x8 *Bs = reinterpret_cast<f16x8 *>(smem + 2 * 2 * kP * 4);
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
     if (p >= a.P) return;  // whole block
@@ -403,9 +405,9 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
                 (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
         }
     };
-    auto epilogue = [&](const f32x16 &acc, unsigned ct, int pe) {
+    auto epilogue = [&](const f32x16 &acc, unsigned ct, int pbase, int pe) {
         asm("" : "+s"(ct));
-        float c1[4], c2[4];
+        float c1[2], c2[2];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const unsigned ub = __float_as_uint(acc[r]);
@@ -413,10 +415,12 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
             const float vc = __uint_as_float((ub & 0xFFFFFF00u) | ccode[r]);
             b2[r] = vmed3(b1[r], b2[r], vr);
             b1[r] = vmin(b1[r], vr);
-            const int q = r & 3;
-            if (r < 4) {
+            // column top-2 of the lane's 16 values in two interleaved chains
+            // (one merge; no +inf staged: the first two values give min / max)
+            const int q = r & 1;
+            if (r < 2) {
                 c1[q] = vc;
-            } else if (r < 8) {  // top-2 of two values: no +inf to stage (4 v_mov per tile)
+            } else if (r < 4) {
                 c2[q] = vmax(c1[q], vc);
                 c1[q] = vmin(c1[q], vc);
             } else {
@@ -424,15 +428,11 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
                 c1[q] = vmin(c1[q], vc);
             }
         }
-#pragma unroll
-        for (int q = 0; q < 4; q += 2) {
-            const float m2 = vmin(c2[q], c2[q + 1]);
-            c2[q] = vmed3(c1[q], c1[q + 1], m2);
-            c1[q] = vmin(c1[q], c1[q + 1]);
+        {
+            const float m2 = vmin(c2[0], c2[1]);
+            c2[0] = vmed3(c1[0], c1[1], m2);
+            c1[0] = vmin(c1[0], c1[1]);
         }
-        float m2 = vmin(c2[0], c2[2]);
-        c2[0] = vmed3(c1[0], c1[2], m2);
-        c1[0] = vmin(c1[0], c1[2]);
         // merge with the other half-wave without LDS (a ds_bpermute here would share
         // lgkmcnt with the B-fragment reads in flight).  One swap of (c1, c2)
         // leaves lanes 0-31 with (own c1, other c1) and lanes 32-63 with
@@ -446,9 +446,9 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
         const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mm), __float_as_uint(mm),
                                                           false, false);
         c2[0] = vmed3(lo, up, __uint_as_float(sw2[1]));
-        c1[0] = mm;
+        c1[0] = __uint_as_float(sw2[0]);  // lanes 0-31 of the swapped mm: mm itself
         if (h == 0) {
-            const int e = pe * (W * 32) + wid * 32 + l;
+            const int e = pbase + pe * (W * 32);  // pe: compile-time tile of the group
             Pc1[e] = c1[0];
             Pc2[e] = c2[0];
         }
@@ -461,6 +461,7 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
         const int buf = grp & 1;
         if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
         const f16x8 *Bb = Bs + buf * kB + l;
+        const int pbase = buf * (G * W * 32) + wid * 32 + l;  // this group's column partials
         f16x8 Bf[2][NCH];
         f32x16 acc[2];
 #pragma unroll
@@ -477,7 +478,7 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NCH + c) * 64];
             }
-            if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1), buf * G + g - 1);
+            if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1), pbase, g - 1);
             // one region per iteration: MFMA : LDS read : VALU = 1 : 1 : 18
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
                 if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, 18, 0);
             }
         }
-        epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1), buf * G + G - 1);
+        epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1), pbase, G - 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const int t = threadIdx.x;
