@@ -135,3 +135,40 @@ def test_icp_split_bitexact_vs_oracle(oracle, coop_g, G, n, noise_init, r, relf)
         assert int((_np(res.corr_tgt)[p] >= 0).sum()) == o["n_corr"]
     if relf == 0.0:
         assert _np(res.stats)[:, 0].max() == 30
+
+
+@pytest.mark.parametrize("wgs,slots", [(None, None), (1, 0), (4, 1)])
+def test_ransac_speculative_mixed_batch(oracle, ransac_sched, wgs, slots):
+    """One launch holding an invalid pair (K < ransac_n), ragged clouds and
+    correspondence counts, and an iteration cap that is not a multiple of 64:
+    the task list, the skip/cut shortcuts and the replay must still give every
+    pair the oracle's sequential result (invalid pair: identity, status -1)."""
+    P, n = 4, 2048
+    B = synth.make_batch(P, n=n, m=n, d=32, base_seed=4400, feat_noise=1.0)
+    cos, ns, ms = [], [1800, 2048, 2048, 1500], [2048, 1700, 2048, 2048]
+    for p in range(P):
+        nn12 = oracle.featnn(B.src_feat[p, :ns[p]], B.tgt_feat[p, :ms[p]])
+        nn21 = oracle.featnn(B.tgt_feat[p, :ms[p]], B.src_feat[p, :ns[p]])
+        cos.append(oracle.corres(nn12, nn21, True, 3))
+    cos[2] = cos[2][:2]  # K = 2 < ransac_n: invalid
+    K = max(len(c) for c in cos)
+    C = np.zeros((P, K, 2), np.int32)
+    for p, c in enumerate(cos):
+        C[p, :len(c)] = c
+    nc = np.array([len(c) for c in cos], np.int32)
+    ransac_sched(wgs, slots)
+    prm = reg.RansacParams(max_correspondence_distance=0.04, seed=5, max_iteration=333)
+    res = reg.ransac_batch(B.src, B.tgt, C, nc, prm, n_src=np.array(ns, np.int32),
+                           n_tgt=np.array(ms, np.int32), pair_ids=np.arange(P, dtype=np.int32))
+    T, st, ct = _np(res.transformation), _np(res.stats), _np(res.corr_tgt)
+    for p in range(P):
+        if p == 2:
+            assert np.array_equal(T[p], np.eye(4)) and st[p, 3] == -1
+            continue
+        r = oracle.ransac(B.src[p, :ns[p]], B.tgt[p, :ms[p]], cos[p], 0.04, seed=5, pair_id=p,
+                          max_iteration=333)
+        assert _bits(T[p], r["T"])
+        assert (st[p, 0], st[p, 1], st[p, 2]) == (r["iters"], r["validated"], r["best_itr"])
+        cs = r["correspondence_set"]
+        got = np.nonzero(ct[p] >= 0)[0]
+        assert np.array_equal(got, cs[:, 0]) and np.array_equal(ct[p, got], cs[:, 1])
