@@ -236,7 +236,10 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     int count = 0;
     // correspondences of the current points, their count / error sum and the
     // Umeyama means
-    auto evaluate = [&]() {
+    // with_u: this iteration's update U is applied to the working copy inside
+    // the sweep (each point read, transformed, written back and queried by the
+    // same thread), which saves the separate transform pass and a pair barrier
+    auto evaluate = [&](bool with_u) {
         unsigned long long acc = 0;
         int cnt = 0;
         {  // 64-query chunks of the spatial order taken from a counter (dense and
@@ -251,7 +254,17 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                 const int k = (c << 6) + lane;
                 if (k < n) {
                     const int i = ord ? ord[k] : k;
-                    const double x = P3[3 * i], y = P3[3 * i + 1], z = P3[3 * i + 2];
+                    double x = P3[3 * i], y = P3[3 * i + 1], z = P3[3 * i + 2];
+                    if (with_u) {  // U from LDS per chunk (volatile: not held across the query)
+                        const volatile double *Uv = sh.U;
+                        double U[12];
+#pragma unroll
+                        for (int q = 0; q < 12; ++q) U[q] = Uv[q];
+                        double ox, oy, oz;
+                        xform12(U, x, y, z, ox, oy, oz);
+                        x = ox; y = oy; z = oz;
+                        P3[3 * i] = x; P3[3 * i + 1] = y; P3[3 * i + 2] = z;
+                    }
                     double d2;
                     int q, s;
                     float qx = 0.f, qy = 0.f, qz = 0.f;
@@ -308,7 +321,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     };
     int it = 0;
     if (valid) {
-        evaluate();
+        evaluate(false);
         for (it = 0; it < a.max_iter;) {
             if (count == 0) break;
             {  // --- cross covariance of the centred correspondences, per lane in order
@@ -345,20 +358,9 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             }
             __syncthreads();
             mark(3);
-            {  // the points transformed in place
-                double U[12];
-                for (int q = 0; q < 12; ++q) U[q] = sh.U[q];
-                for (int i = base; i < n; i += stride) {
-                    double ox, oy, oz;
-                    xform12(U, P3[3 * i], P3[3 * i + 1], P3[3 * i + 2], ox, oy, oz);
-                    P3[3 * i] = ox; P3[3 * i + 1] = oy; P3[3 * i + 2] = oz;
-                }
-            }
-            // the next sweep reads any point: every new position visible pair-wide
-            sync_pair();
-            mark(4);
+            // (the points are transformed in place by the next sweep)
             const double pf = fit, pr = rmse;
-            evaluate();
+            evaluate(true);
             ++it;
             if (__builtin_fabs(pf - fit) < a.rel_fit && __builtin_fabs(pr - rmse) < a.rel_rmse) break;
         }
