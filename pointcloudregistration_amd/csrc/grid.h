@@ -7,7 +7,9 @@
 // touches at most 2x2x2 cells.  Hash collisions only add candidates; the exact
 // distance test decides, so results are independent of slot order and equal to
 // brute force.  Consumers that own a pair (RANSAC, ICP) copy the grid into LDS
-// with u16 idx/start (14 B per point + 2 B per slot; 128 KiB at 8192 points).
+// as one float4 per point (x, y, z, index bits) and u16 slot starts (GridP4,
+// 16 B per point + 2 B per slot: 144 KiB at 8192 points); grid_to_lds keeps the
+// 14 B SoA form (GridT<uint16_t>).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "geom.h"
@@ -32,6 +34,29 @@ struct GridT {
     int S;
     double cell;
     double inv_cell;  // queries use v * inv_cell: the 1.001 r margin covers the rounding
+    // candidate access shared with GridP4: coordinates of slot s, then (only for
+    // candidates inside the radius) its point index
+    __device__ __forceinline__ void load(int s, float &ax, float &ay, float &az, float &aw) const {
+        ax = x[s]; ay = y[s]; az = z[s]; aw = 0.0f;
+    }
+    __device__ __forceinline__ int index_of(int s, float) const { return (int)idx[s]; }
+};
+
+// LDS copy for the consumers that own a pair (RANSAC, ICP): one float4 per
+// point (x, y, z, index bits) -- one ds_read_b128 and one address per
+// candidate instead of four reads at four addresses -- and u16 slot starts
+// (16 B per point + 2 B per slot: 144 KiB at 8192 points)
+struct GridP4 {
+    const float4 *pts;
+    const uint16_t *start;
+    int S;
+    double cell;
+    double inv_cell;
+    __device__ __forceinline__ void load(int s, float &ax, float &ay, float &az, float &aw) const {
+        const float4 v = pts[s];
+        ax = v.x; ay = v.y; az = v.z; aw = v.w;
+    }
+    __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
 };
 using GridView = GridT<uint32_t>;
 
@@ -51,8 +76,8 @@ __device__ __forceinline__ double cell_gap(double p, int c, double cell) {
 // LDS loads overlap.  The update order (slot order, strict < then lower index
 // on ties) makes the result independent of both.
 // kSlot: also report the winner's slot (its coordinates are g.x/y/z[slot])
-template <typename IdxT, bool kSlot = false>
-__device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double thr, double px,
+template <typename View, bool kSlot = false>
+__device__ __forceinline__ int grid_query(const View &g, double r, double thr, double px,
                                           double py, double pz, double &d2out, int *slot = nullptr) {
     // The build assigns cells by floor(v / cell); here floor(v * inv_cell) over
     // [p - 1.001 r, p + 1.001 r]: the 0.1 % margin exceeds the rounding
@@ -65,9 +90,11 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
     double best = __builtin_inf();
     int bj = -1, bs = -1;
     auto take = [&](int s) {
-        const double d2 = dist2(px, py, pz, (double)g.x[s], (double)g.y[s], (double)g.z[s]);
+        float ax, ay, az, aw;
+        g.load(s, ax, ay, az, aw);
+        const double d2 = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
         if (d2 < thr) {
-            const int j = (int)g.idx[s];
+            const int j = g.index_of(s, aw);
             if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; if constexpr (kSlot) bs = s; }
         }
     };
@@ -123,16 +150,17 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
                 s = (int)(q[0] & 0xffffu);
                 e = (int)(q[0] >> 16);
             }
-            const float ax = g.x[sa], ay = g.y[sa], az = g.z[sa];
-            const float bx = g.x[sbb], by = g.y[sbb], bz = g.z[sbb];
+            float ax, ay, az, aw, bx, by, bz, bw;
+            g.load(sa, ax, ay, az, aw);
+            g.load(sbb, bx, by, bz, bw);
             const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
             const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
             if (da < thr) {
-                const int j = (int)g.idx[sa];
+                const int j = g.index_of(sa, aw);
                 if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = sa; }
             }
             if (hb && db < thr) {
-                const int j = (int)g.idx[sbb];
+                const int j = g.index_of(sbb, bw);
                 if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = sbb; }
             }
         }
@@ -150,16 +178,17 @@ __device__ __forceinline__ int grid_query(const GridT<IdxT> &g, double r, double
                     const int s1 = (int)g.start[h + 1];
                     for (; s + 1 < s1; s += 2) {
                         // both loads first, then the two updates in slot order
-                        const float ax = g.x[s], ay = g.y[s], az = g.z[s];
-                        const float bx = g.x[s + 1], by = g.y[s + 1], bz = g.z[s + 1];
+                        float ax, ay, az, aw, bx, by, bz, bw;
+                        g.load(s, ax, ay, az, aw);
+                        g.load(s + 1, bx, by, bz, bw);
                         const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
                         const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
                         if (da < thr) {
-                            const int j = (int)g.idx[s];
+                            const int j = g.index_of(s, aw);
                             if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = s; }
                         }
                         if (db < thr) {
-                            const int j = (int)g.idx[s + 1];
+                            const int j = g.index_of(s + 1, bw);
                             if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = s + 1; }
                         }
                     }
@@ -193,6 +222,34 @@ inline size_t grid_lds_bytes(int mstride, int S, size_t budget) {
     const size_t b = (size_t)mstride * 14 + (size_t)(S + 1) * 2;
     const size_t a = (b + 15) & ~size_t(15);
     return a <= budget ? a : 0;
+}
+
+// bytes of the float4 LDS copy of one pair's grid (0 if it does not fit)
+inline size_t grid_lds4_bytes(int mstride, int S, size_t budget) {
+    if (mstride > 65535 || S + 1 > 65536) return 0;
+    const size_t b = (size_t)mstride * 16 + (size_t)(S + 1) * 2;
+    const size_t a = (b + 15) & ~size_t(15);
+    return a <= budget ? a : 0;
+}
+
+// cooperative float4 copy of pair p's grid into LDS (all threads of the block
+// call; ends with a barrier); layout: pts[m] (x, y, z, index bits), start16[S+1]
+__device__ inline GridP4 grid_to_lds4(const GridBatch &gb, int p, int m, char *lds) {
+    const size_t o = (size_t)p * gb.mstride;
+    float4 *lp = (float4 *)lds;
+    uint16_t *ls = (uint16_t *)(lp + gb.mstride);
+    for (int i = threadIdx.x; i < m; i += blockDim.x)
+        lp[i] = make_float4(gb.x[o + i], gb.y[o + i], gb.z[o + i], __int_as_float((int)gb.idx[o + i]));
+    const uint32_t *st = gb.start + (size_t)p * (gb.S + 1);
+    for (int i = threadIdx.x; i <= gb.S; i += blockDim.x) ls[i] = (uint16_t)st[i];
+    __syncthreads();
+    return GridP4{lp, ls, gb.S, gb.cell, 1.0 / gb.cell};
+}
+
+// view of a float4 copy that grid_to_lds4 placed at `lds` (no data movement)
+__device__ inline GridP4 grid_lds4_view(const GridBatch &gb, char *lds) {
+    const float4 *lp = (const float4 *)lds;
+    return GridP4{lp, (const uint16_t *)(lp + gb.mstride), gb.S, gb.cell, 1.0 / gb.cell};
 }
 
 // view of a grid copy that grid_to_lds placed at `lds` (no data movement)

@@ -204,10 +204,10 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         }
         if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);  // (G = 1: the barrier below)
     }
-    GridT<uint16_t> gl{};
+    GridP4 gl{};
     GridView gg{};
     if (valid) {
-        if constexpr (kLds) gl = grid_to_lds(a.grid, p, m, dsm + ((sizeof(IShared) + 15) & ~size_t(15)));
+        if constexpr (kLds) gl = grid_to_lds4(a.grid, p, m, dsm + ((sizeof(IShared) + 15) & ~size_t(15)));
         else gg = a.grid.view(p);
     }
     __syncthreads();
@@ -269,10 +269,10 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                     int q, s;
                     float qx = 0.f, qy = 0.f, qz = 0.f;
                     if constexpr (kLds) {
-                        q = grid_query<uint16_t, true>(gl, a.d, a.thr, x, y, z, d2, &s);
-                        if (q >= 0) { qx = gl.x[s]; qy = gl.y[s]; qz = gl.z[s]; }
+                        q = grid_query<GridP4, true>(gl, a.d, a.thr, x, y, z, d2, &s);
+                        if (q >= 0) { float w; gl.load(s, qx, qy, qz, w); }
                     } else {
-                        q = grid_query<uint32_t, true>(gg, a.d, a.thr, x, y, z, d2, &s);
+                        q = grid_query<GridView, true>(gg, a.d, a.thr, x, y, z, d2, &s);
                         if (q >= 0) { qx = gg.x[s]; qy = gg.y[s]; qz = gg.z[s]; }
                     }
                     TQ[i] = make_float4(qx, qy, qz, __int_as_float(q));
@@ -418,7 +418,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     }
     a.T_out = T_out; a.fit_out = fit_out; a.stats = stats; a.corr_tgt = corr_tgt;
     const size_t hdr = (sizeof(IShared) + 15) & ~size_t(15);
-    const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds_bytes(Mmax, a.grid.S, 160 * 1024 - hdr) : 0;
+    const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds4_bytes(Mmax, a.grid.S, 160 * 1024 - hdr) : 0;
     const bool lds = gbytes > 0;
     const size_t sm = lds ? hdr + gbytes : hdr;
     const void *fn = icp_fn(lds);

@@ -461,7 +461,7 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
         }
         char *glds = dsm + ((sizeof(Shared) + 15) & ~size_t(15));
         if (kLds && sh.gp != p) {  // this pair's grid into LDS (kept while the next task is the same pair)
-            (void)grid_to_lds(a.grid, p, cnt_of(a.n_tgt, p, a.Mmax), glds);
+            (void)grid_to_lds4(a.grid, p, cnt_of(a.n_tgt, p, a.Mmax), glds);
             if (tid == 0) sh.gp = p;
         }
         double Te[12];
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
         for (int k = 0; k < 12; ++k) Te[k] = sh.Te[k];
         int32_t *cbuf = r < a.nslots ? a.slots + ((size_t)p * a.nslots + r) * a.Nmax : nullptr;
         TaskRes out;
-        if constexpr (kLds) out = sweep_pair<kLds, RN>(a, sh, grid_lds_view(a.grid, glds), p, n, K, Te, rs, r, cbuf, true);
+        if constexpr (kLds) out = sweep_pair<kLds, RN>(a, sh, grid_lds4_view(a.grid, glds), p, n, K, Te, rs, r, cbuf, true);
         else out = sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, rs, r, cbuf, true);
         if (tid == 0) {
             atomicAdd(out.status == kCut ? &a.hdr->n_cut : &a.hdr->n_done, 1);
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kThreads) void ransac_replay_kernel(RArgs a) {
         double Te[12];
         for (int k = 0; k < 12; ++k) Te[k] = s.bestT[k];
         if constexpr (kLds) {
-            const GridT<uint16_t> gl = grid_to_lds(a.grid, p, m, dsm + ((sizeof(Shared) + 15) & ~size_t(15)));
+            const GridP4 gl = grid_to_lds4(a.grid, p, m, dsm + ((sizeof(Shared) + 15) & ~size_t(15)));
             (void)sweep_pair<kLds, RN>(a, sh, gl, p, n, K, Te, nullptr, 0, bb, false);
         } else {
             (void)sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, nullptr, 0, bb, false);
@@ -658,7 +658,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     }
     const size_t hdr = (sizeof(Shared) + 15) & ~size_t(15);
     const size_t budget = 160 * 1024 - hdr;
-    const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds_bytes(Mmax, a.grid.S, budget) : 0;
+    const size_t gbytes = (a.d > 0.0 && Mmax > 0) ? grid_lds4_bytes(Mmax, a.grid.S, budget) : 0;
     const bool lds = gbytes > 0;
     const size_t sm = lds ? hdr + gbytes : hdr;
     const void *hfn = nullptr, *sfn = nullptr, *rfn = nullptr;
