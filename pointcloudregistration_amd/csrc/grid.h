@@ -8,8 +8,7 @@
 // distance test decides, so results are independent of slot order and equal to
 // brute force.  Consumers that own a pair (RANSAC, ICP) copy the grid into LDS
 // as one float4 per point (x, y, z, index bits) and u16 slot starts (GridP4,
-// 16 B per point + 2 B per slot: 144 KiB at 8192 points); grid_to_lds keeps the
-// 14 B SoA form (GridT<uint16_t>).
+// 16 B per point + 2 B per slot: 144 KiB at 8192 points).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "geom.h"
@@ -216,14 +215,6 @@ struct GridBatch {
     }
 };
 
-// bytes of the LDS copy of one pair's grid (0 if it does not fit the budget)
-inline size_t grid_lds_bytes(int mstride, int S, size_t budget) {
-    if (mstride > 65535 || S + 1 > 65536) return 0;
-    const size_t b = (size_t)mstride * 14 + (size_t)(S + 1) * 2;
-    const size_t a = (b + 15) & ~size_t(15);
-    return a <= budget ? a : 0;
-}
-
 // bytes of the float4 LDS copy of one pair's grid (0 if it does not fit)
 inline size_t grid_lds4_bytes(int mstride, int S, size_t budget) {
     if (mstride > 65535 || S + 1 > 65536) return 0;
@@ -250,35 +241,6 @@ __device__ inline GridP4 grid_to_lds4(const GridBatch &gb, int p, int m, char *l
 __device__ inline GridP4 grid_lds4_view(const GridBatch &gb, char *lds) {
     const float4 *lp = (const float4 *)lds;
     return GridP4{lp, (const uint16_t *)(lp + gb.mstride), gb.S, gb.cell, 1.0 / gb.cell};
-}
-
-// view of a grid copy that grid_to_lds placed at `lds` (no data movement)
-__device__ inline GridT<uint16_t> grid_lds_view(const GridBatch &gb, char *lds) {
-    float *lx = (float *)lds;
-    uint16_t *li = (uint16_t *)(lx + 3 * (size_t)gb.mstride);
-    return GridT<uint16_t>{lx, lx + gb.mstride, lx + 2 * (size_t)gb.mstride, li, li + gb.mstride,
-                           gb.S, gb.cell, 1.0 / gb.cell};
-}
-
-// cooperative copy of pair p's grid into LDS (all threads of the block call);
-// layout: x[m] y[m] z[m] idx16[m] start16[S+1]
-__device__ inline GridT<uint16_t> grid_to_lds(const GridBatch &gb, int p, int m, char *lds) {
-    const size_t o = (size_t)p * gb.mstride;
-    float *lx = (float *)lds;
-    float *ly = lx + gb.mstride;
-    float *lz = ly + gb.mstride;
-    uint16_t *li = (uint16_t *)(lz + gb.mstride);
-    uint16_t *ls = li + gb.mstride;
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        lx[i] = gb.x[o + i];
-        ly[i] = gb.y[o + i];
-        lz[i] = gb.z[o + i];
-        li[i] = (uint16_t)gb.idx[o + i];
-    }
-    const uint32_t *st = gb.start + (size_t)p * (gb.S + 1);
-    for (int i = threadIdx.x; i <= gb.S; i += blockDim.x) ls[i] = (uint16_t)st[i];
-    __syncthreads();
-    return GridT<uint16_t>{lx, ly, lz, li, ls, gb.S, gb.cell, 1.0 / gb.cell};
 }
 
 // host: spatial (Morton-of-cell) order of each cloud's points, (P, Nmax) i32 in a
