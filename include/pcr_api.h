@@ -132,7 +132,12 @@ typedef struct pcr_ransac_params {
  * stats (P,5) = {iterations, validated, best_itr, status(1 ok/0 none/-1 bad
  * input), n_correspondences}, corr_tgt (P,Nmax) target index per source point
  * or -1 (optional), inlier_mask (P, ceil(Nmax/32)) bitset (optional).
- * Blocks the host between hypothesis waves (one 4-byte readback per wave).
+ * Blocks the host between rounds of hypotheses (one 32-byte readback per
+ * round: [0,1024), then 4096 at a time while a pair's bound est_k lies beyond).
+ * Verification runs speculatively on persistent workgroups, the sequential rule
+ * is replayed afterwards: results do not depend on the scheduling.  Workspace:
+ * up to 256 MB of per-hypothesis target slots per device (fewer slots only add
+ * one sweep per pair).
  * ------------------------------------------------------------------------- */
 int pcr_ransac_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t Nmax,
                      int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt,
