@@ -66,7 +66,17 @@ struct TaskRes {
     unsigned long long acc;  // fixed-point sum of the inliers' d2
     int cnt, cin;            // inliers, inlier correspondences
     int status;              // kPending / kDone / kCut / kSkipped
+    int misses;              // split sweeps: misses of both halves so far
+    int hdone;               // split sweeps: halves finished
     int pad;
+};
+
+// one half of a split sweep (the second half to finish combines them)
+struct TaskPart {
+    unsigned long long acc;
+    int cnt, cin;
+    int flag;  // kDone / kCut / kSkipped as this half saw it
+    int lb;    // its final cut bound
 };
 constexpr int kPending = 0, kDone = 1, kCut = 2, kSkipped = 3;
 
@@ -106,6 +116,8 @@ struct RArgs {
     int nslots;
     int32_t *bestbuf;       // (P, Nmax) targets of the best hypothesis so far
     RHeader *hdr;
+    int split;              // workgroups per task (1, or 2 when the tasks are few)
+    TaskPart *parts;        // (P, hcap, 2) when split == 2
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -259,20 +271,21 @@ __device__ inline bool apply_result(RState &s, int itr, const TaskRes &r, const 
 template <bool kLds, int RN, typename Grid>
 __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p, int n, int K,
                               const double *Te, const TaskRes *prs, int npr, int32_t *cbuf,
-                              bool by_order) {
+                              bool by_order, int c_lo = 0, int c_hi = 0x7fffffff,
+                              int *gmiss = nullptr, int h = 0, int nh = 1) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
     const int32_t *co = a.corres + (size_t)p * a.Kmax * 2;
     const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
     const double scale = fx_scale(a.thr);
-    const int nch = (n + 63) >> 6;
+    const int nch = min((n + 63) >> 6, c_hi);
     unsigned long long acc = 0;
     int cnt = 0, cin = 0;
     int lb = sh.lb;
     for (int nc = 1;; ++nc) {
         int c = 0;
-        if (lane == 0) c = atomicAdd(&sh.chunk, 1);
+        if (lane == 0) c = c_lo + atomicAdd(&sh.chunk, 1);
         c = __shfl(c, 0, 64);
         if (c >= nch) break;
         const int k = (c << 6) + lane;
@@ -287,7 +300,11 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
         }
         const int miss = __popcll(__ballot(k < n && j < 0));
         int tot = 0;
-        if (lane == 0) tot = atomicAdd(&sh.misses, miss) + miss;
+        if (lane == 0) {
+            tot = atomicAdd(&sh.misses, miss) + miss;
+            if (gmiss)  // split sweep: the task's total over both halves
+                tot = __hip_atomic_fetch_add(gmiss, miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + miss;
+        }
         tot = __shfl(tot, 0, 64);
         if ((nc & 3) == 0 && npr > 0) {  // earlier tasks finished meanwhile: a higher bound
             int c2 = 0;
@@ -306,11 +323,12 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
     // every wave's misses and bound are in: one cut decision for all (a wave
     // that stopped saw misses above n - its bound >= n - the final bound)
     __syncthreads();
-    const bool cut = sh.lb > 0 && sh.misses > n - sh.lb;
+    const int msum = gmiss ? __hip_atomic_load(gmiss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sh.misses;
+    const bool cut = sh.lb > 0 && msum > n - sh.lb;
     // (not unrolled: an unrolled copy of this loop spilled ~260 VGPRs)
     if (!cut)  // the inlier ratio over the correspondences (est_k of a new best)
 #pragma unroll 1
-        for (int q = tid; q < K; q += kThreads) {
+        for (int q = h * kThreads + tid; q < K; q += nh * kThreads) {
             const int si = co[2 * q], ti = co[2 * q + 1];
             double px, py, pz;
             xform12(Te, (double)S[3 * si], (double)S[3 * si + 1], (double)S[3 * si + 2], px, py, pz);
@@ -325,7 +343,7 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
     }
     if (lane == 0) { sh.racc[wid] = acc; sh.rcnt[wid] = cnt; sh.rcin[wid] = cin; }
     __syncthreads();
-    if (tid == 0) atomicAdd(&a.hdr->n_chunks, min(sh.chunk, nch));
+    if (tid == 0) atomicAdd(&a.hdr->n_chunks, min(sh.chunk, max(nch - c_lo, 0)));
     TaskRes r{};
     for (int w = 0; w < kWaves; ++w) { r.acc += sh.racc[w]; r.cnt += sh.rcnt[w]; r.cin += sh.rcin[w]; }
     r.status = cut ? kCut : kDone;
@@ -386,6 +404,43 @@ __global__ __launch_bounds__(64) void ransac_task_kernel(RArgs a, int RN) {
     }
 }
 
+// Publish a sweep result (thread 0).  Unsplit: the status store is released
+// after the fields.  Split: each half parks its partial; the half that finishes
+// second adds both and publishes -- skipped if either half proved the task
+// beyond est_k, cut if either half stopped or the summed misses exceed n - the
+// larger bound (a stopped half saw misses above n - its bound), else done.
+__device__ inline void finish_task(const RArgs &a, TaskRes *rt, int p, int r, int h, TaskRes out,
+                                   int lb) {
+    if (a.split > 1) {
+        TaskPart *pp = a.parts + ((size_t)p * a.hcap + r) * 2;
+        pp[h].acc = out.acc;
+        pp[h].cnt = out.cnt;
+        pp[h].cin = out.cin;
+        pp[h].flag = out.status;
+        pp[h].lb = lb;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int before = __hip_atomic_fetch_add(&rt->hdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (before != a.split - 1) return;  // the other half publishes
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const TaskPart q0 = pp[0], q1 = pp[1];
+        out.acc = q0.acc + q1.acc;
+        out.cnt = q0.cnt + q1.cnt;
+        out.cin = q0.cin + q1.cin;
+        const int n = cnt_of(a.n_src, p, a.Nmax);
+        const int lbm = max(q0.lb, q1.lb);
+        const int ms = __hip_atomic_load(&rt->misses, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (q0.flag == kSkipped || q1.flag == kSkipped) out.status = kSkipped;
+        else if (q0.flag == kCut || q1.flag == kCut || (lbm > 0 && ms > n - lbm)) out.status = kCut;
+        else out.status = kDone;
+    }
+    atomicAdd(out.status == kSkipped ? &a.hdr->n_skip : out.status == kCut ? &a.hdr->n_cut : &a.hdr->n_done, 1);
+    rt->acc = out.acc;
+    rt->cnt = out.cnt;
+    rt->cin = out.cin;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&rt->status, out.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Persistent sweep workgroups take tasks t = (rank r = t / P, pair p = t % P)
 // from a global counter: every pair's first hypothesis, then every pair's
 // second, ...  Each sweep is independent of the others; the sequential rule is
@@ -409,7 +464,9 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
         if (tid == 0) sh.task = atomicAdd(&a.hdr->task_ctr, 1);
         __syncthreads();
         const int t = sh.task;
-        const int r = t / a.P, p = t - r * a.P;
+        // t = (r * P + p) * split + h: the halves of a split task are taken together
+        const int tq = t / a.split, h = t - tq * a.split;
+        const int r = tq / a.P, p = tq - r * a.P;
         if (r >= maxtask) break;
         const int nt = a.ntask[p];
         if (r >= nt) continue;
@@ -454,8 +511,9 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
         __syncthreads();
         if (sh.skip) {
             if (tid == 0) {
-                __hip_atomic_store(&rs[r].status, kSkipped, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd(&a.hdr->n_skip, 1);
+                TaskRes out{};
+                out.status = kSkipped;
+                finish_task(a, rs + r, p, r, h, out, 0);
             }
             continue;
         }
@@ -468,22 +526,20 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) Te[k] = sh.Te[k];
         int32_t *cbuf = r < a.nslots ? a.slots + ((size_t)p * a.nslots + r) * a.Nmax : nullptr;
+        const int nch = (n + 63) >> 6;
+        const int c_lo = h * nch / a.split, c_hi = (h + 1) * nch / a.split;
+        int *gm = a.split > 1 ? &rs[r].misses : nullptr;
         TaskRes out;
-        if constexpr (kLds) out = sweep_pair<kLds, RN>(a, sh, grid_lds4_view(a.grid, glds), p, n, K, Te, rs, r, cbuf, true);
-        else out = sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, rs, r, cbuf, true);
-        if (tid == 0) {
-            atomicAdd(out.status == kCut ? &a.hdr->n_cut : &a.hdr->n_done, 1);
-            rs[r].acc = out.acc;
-            rs[r].cnt = out.cnt;
-            rs[r].cin = out.cin;
-        }
-        // every thread's target stores and thread 0's result before the status
+        if constexpr (kLds)
+            out = sweep_pair<kLds, RN>(a, sh, grid_lds4_view(a.grid, glds), p, n, K, Te, rs, r, cbuf, true,
+                                       c_lo, c_hi, gm, h, a.split);
+        else
+            out = sweep_pair<kLds, RN>(a, sh, a.grid.view(p), p, n, K, Te, rs, r, cbuf, true, c_lo, c_hi,
+                                       gm, h, a.split);
+        // every thread's target stores have completed before the result is published
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_store(&rs[r].status, out.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (tid == 0) finish_task(a, rs + r, p, r, h, out, sh.lb);
     }
 }
 
@@ -683,6 +739,13 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
         cus = 1;
     }
     const int nwg = std::max(1, env_int("PCR_RANSAC_WGS", std::max(1, per_cu) * std::max(1, cus)));
+    // few pairs (a multi-GPU shard): two workgroups per task, each half the points
+    a.split = std::min(2, std::max(1, env_int("PCR_RANSAC_SPLIT", 2 * P <= nwg ? 2 : 1)));
+    a.parts = nullptr;
+    if (a.split > 1) {
+        a.parts = (TaskPart *)workspace(32, sizeof(TaskPart) * 2 * (size_t)P * a.hcap);
+        PCR_REQUIRE(a.parts, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
+    }
     const int rnarg = a.rn;
     const bool stats_env = env_int("PCR_RANSAC_STATS", 0) != 0;
     prof_begin(s, kProfRansacValidate);

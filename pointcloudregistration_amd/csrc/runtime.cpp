@@ -27,7 +27,7 @@ struct Slot {
     size_t bytes = 0;
 };
 constexpr int kMaxDevices = 64;
-constexpr int kMaxSlots = 32;
+constexpr int kMaxSlots = 40;
 std::mutex g_mu;
 Slot g_slots[kMaxDevices][kMaxSlots];
 // superseded buffers: kept until pcr_workspace_release (a graph captured before a

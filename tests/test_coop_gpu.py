@@ -3,9 +3,11 @@
 RANSAC: the verification sweeps of all pairs run speculatively on persistent
 workgroups (ransac.hip); the sequential rule is replayed afterwards.  Whatever the
 number of workgroups (PCR_RANSAC_WGS: 1 = every task in order on one workgroup,
-where the skip/cut shortcuts see every earlier result) and of target slots
+where the skip/cut shortcuts see every earlier result), of target slots
 (PCR_RANSAC_SLOTS: 0 = the best hypothesis' targets always come from one more
-sweep), the results equal the oracle's sequential loop bit for bit.
+sweep) and of workgroups per task (PCR_RANSAC_SPLIT: 2 = each sweep in two
+halves combined by the second to finish), the results equal the oracle's
+sequential loop bit for bit.
 
 ICP: iterations split over G = 1, 2, 4, 8 workgroups of a cooperative launch
 (coop.h) must give the oracle's results bit for bit -- the split only changes who
@@ -48,11 +50,11 @@ def coop_g():
 
 @pytest.fixture()
 def ransac_sched():
-    keys = ("PCR_RANSAC_WGS", "PCR_RANSAC_SLOTS")
+    keys = ("PCR_RANSAC_WGS", "PCR_RANSAC_SLOTS", "PCR_RANSAC_SPLIT")
     old = {k: os.environ.get(k) for k in keys}
 
-    def set_sched(wgs, slots):
-        for k, v in zip(keys, (wgs, slots)):
+    def set_sched(wgs, slots, split=None):
+        for k, v in zip(keys, (wgs, slots, split)):
             if v is None:
                 os.environ.pop(k, None)
             else:
@@ -65,11 +67,12 @@ def ransac_sched():
             os.environ[k] = v
 
 
-@pytest.mark.parametrize("wgs,slots", [(None, None), (1, None), (2, 1), (None, 0), (3, 2)])
-def test_ransac_speculative_bitexact_vs_oracle(oracle, ransac_sched, wgs, slots):
+@pytest.mark.parametrize("wgs,slots,split", [(None, None, None), (None, None, 1), (1, None, 2),
+                                             (2, 1, 1), (None, 0, 2), (3, 2, 2), (5, 2, 1)])
+def test_ransac_speculative_bitexact_vs_oracle(oracle, ransac_sched, wgs, slots, split):
     P, n = 3, 4096
     B = synth.make_batch(P, n=n, m=n, d=32, base_seed=2000, feat_noise=1.0)
-    ransac_sched(wgs, slots)
+    ransac_sched(wgs, slots, split)
     prm = reg.RansacParams(max_correspondence_distance=0.04, seed=7)
     res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm,
                                             pair_ids=np.arange(P, dtype=np.int32) + 9)
@@ -93,8 +96,8 @@ def test_ransac_multi_round_low_inlier_ratio(oracle, ransac_sched):
     1024 hypotheses: the later rounds continue the same sequential loop."""
     P, n = 2, 2048
     B = synth.make_batch(P, n=n, m=n, d=32, base_seed=3100, feat_noise=2.2)
-    for wgs, slots in ((None, None), (1, 0), (5, 3)):
-        ransac_sched(wgs, slots)
+    for wgs, slots, split in ((None, None, None), (1, 0, 2), (5, 3, 1), (3, 1, 2)):
+        ransac_sched(wgs, slots, split)
         prm = reg.RansacParams(max_correspondence_distance=0.04, seed=3, max_iteration=6000)
         res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm)
         st = _np(res.stats)
@@ -137,8 +140,8 @@ def test_icp_split_bitexact_vs_oracle(oracle, coop_g, G, n, noise_init, r, relf)
         assert _np(res.stats)[:, 0].max() == 30
 
 
-@pytest.mark.parametrize("wgs,slots", [(None, None), (1, 0), (4, 1)])
-def test_ransac_speculative_mixed_batch(oracle, ransac_sched, wgs, slots):
+@pytest.mark.parametrize("wgs,slots,split", [(None, None, None), (1, 0, 2), (4, 1, 1), (6, 1, 2)])
+def test_ransac_speculative_mixed_batch(oracle, ransac_sched, wgs, slots, split):
     """One launch holding an invalid pair (K < ransac_n), ragged clouds and
     correspondence counts, and an iteration cap that is not a multiple of 64:
     the task list, the skip/cut shortcuts and the replay must still give every
@@ -156,7 +159,7 @@ def test_ransac_speculative_mixed_batch(oracle, ransac_sched, wgs, slots):
     for p, c in enumerate(cos):
         C[p, :len(c)] = c
     nc = np.array([len(c) for c in cos], np.int32)
-    ransac_sched(wgs, slots)
+    ransac_sched(wgs, slots, split)
     prm = reg.RansacParams(max_correspondence_distance=0.04, seed=5, max_iteration=333)
     res = reg.ransac_batch(B.src, B.tgt, C, nc, prm, n_src=np.array(ns, np.int32),
                            n_tgt=np.array(ms, np.int32), pair_ids=np.arange(P, dtype=np.int32))
