@@ -71,7 +71,7 @@ struct TaskRes {
     int pad;
 };
 
-// one half of a split sweep (the second half to finish combines them)
+// one part of a split sweep (the last part to finish combines them)
 struct TaskPart {
     unsigned long long acc;
     int cnt, cin;
@@ -116,8 +116,8 @@ struct RArgs {
     int nslots;
     int32_t *bestbuf;       // (P, Nmax) targets of the best hypothesis so far
     RHeader *hdr;
-    int split;              // workgroups per task (1, or 2 when the tasks are few)
-    TaskPart *parts;        // (P, hcap, 2) when split == 2
+    int split;              // workgroups per task (1, 2, 4 or 8: more when the pairs are few)
+    TaskPart *parts;        // (P, hcap, split) when split > 1
 };
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
@@ -405,14 +405,14 @@ __global__ __launch_bounds__(64) void ransac_task_kernel(RArgs a, int RN) {
 }
 
 // Publish a sweep result (thread 0).  Unsplit: the status store is released
-// after the fields.  Split: each half parks its partial; the half that finishes
-// second adds both and publishes -- skipped if either half proved the task
-// beyond est_k, cut if either half stopped or the summed misses exceed n - the
-// larger bound (a stopped half saw misses above n - its bound), else done.
+// after the fields.  Split: each part parks its partial; the part that finishes
+// last adds them and publishes -- skipped if any part proved the task beyond
+// est_k, cut if any part stopped or the summed misses exceed n - the largest
+// bound (a stopped part saw misses above n - its bound), else done.
 __device__ inline void finish_task(const RArgs &a, TaskRes *rt, int p, int r, int h, TaskRes out,
                                    int lb) {
     if (a.split > 1) {
-        TaskPart *pp = a.parts + ((size_t)p * a.hcap + r) * 2;
+        TaskPart *pp = a.parts + ((size_t)p * a.hcap + r) * a.split;
         pp[h].acc = out.acc;
         pp[h].cnt = out.cnt;
         pp[h].cin = out.cin;
@@ -420,17 +420,26 @@ __device__ inline void finish_task(const RArgs &a, TaskRes *rt, int p, int r, in
         pp[h].lb = lb;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int before = __hip_atomic_fetch_add(&rt->hdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (before != a.split - 1) return;  // the other half publishes
+        if (before != a.split - 1) return;  // another part publishes
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const TaskPart q0 = pp[0], q1 = pp[1];
-        out.acc = q0.acc + q1.acc;
-        out.cnt = q0.cnt + q1.cnt;
-        out.cin = q0.cin + q1.cin;
+        out.acc = 0ull;
+        out.cnt = 0;
+        out.cin = 0;
+        int lbm = 0;
+        bool skipped = false, stopped = false;
+        for (int q = 0; q < a.split; ++q) {
+            const TaskPart pq = pp[q];
+            out.acc += pq.acc;
+            out.cnt += pq.cnt;
+            out.cin += pq.cin;
+            lbm = max(lbm, pq.lb);
+            skipped = skipped || pq.flag == kSkipped;
+            stopped = stopped || pq.flag == kCut;
+        }
         const int n = cnt_of(a.n_src, p, a.Nmax);
-        const int lbm = max(q0.lb, q1.lb);
         const int ms = __hip_atomic_load(&rt->misses, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (q0.flag == kSkipped || q1.flag == kSkipped) out.status = kSkipped;
-        else if (q0.flag == kCut || q1.flag == kCut || (lbm > 0 && ms > n - lbm)) out.status = kCut;
+        if (skipped) out.status = kSkipped;
+        else if (stopped || (lbm > 0 && ms > n - lbm)) out.status = kCut;
         else out.status = kDone;
     }
     atomicAdd(out.status == kSkipped ? &a.hdr->n_skip : out.status == kCut ? &a.hdr->n_cut : &a.hdr->n_done, 1);
@@ -739,11 +748,19 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
         cus = 1;
     }
     const int nwg = std::max(1, env_int("PCR_RANSAC_WGS", std::max(1, per_cu) * std::max(1, cus)));
-    // few pairs (a multi-GPU shard): two workgroups per task, each half the points
-    a.split = std::min(2, std::max(1, env_int("PCR_RANSAC_SPLIT", 2 * P <= nwg ? 2 : 1)));
+    // few pairs (multi-GPU shards, single-pair calls): up to 8 workgroups per
+    // task, each a slice of the chunks -- the largest power of two with
+    // split * P <= workgroups / 4 (256 CUs: 2 at 32 pairs, 8 at 8 or fewer;
+    // every part loads the pair's grid, so slices are kept long)
+    int split = 1;
+    while (split < 8 && 2 * split * P * 4 <= nwg) split <<= 1;
+    split = env_int("PCR_RANSAC_SPLIT", split);
+    PCR_REQUIRE(split == 1 || split == 2 || split == 4 || split == 8, PCR_ERR_ARG,
+                "ransac: PCR_RANSAC_SPLIT=%d (1, 2, 4 or 8)", split);
+    a.split = split;
     a.parts = nullptr;
     if (a.split > 1) {
-        a.parts = (TaskPart *)workspace(32, sizeof(TaskPart) * 2 * (size_t)P * a.hcap);
+        a.parts = (TaskPart *)workspace(32, sizeof(TaskPart) * (size_t)a.split * P * a.hcap);
         PCR_REQUIRE(a.parts, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
     }
     const int rnarg = a.rn;

@@ -67,7 +67,7 @@ def ransac_sched():
             os.environ[k] = v
 
 
-@pytest.mark.parametrize("wgs,slots,split", [(None, None, None), (None, None, 1), (1, None, 2),
+@pytest.mark.parametrize("wgs,slots,split", [(None, None, None), (None, None, 1), (1, None, 2), (None, None, 8), (2, 0, 4),
                                              (2, 1, 1), (None, 0, 2), (3, 2, 2), (5, 2, 1)])
 def test_ransac_speculative_bitexact_vs_oracle(oracle, ransac_sched, wgs, slots, split):
     P, n = 3, 4096
