@@ -450,10 +450,12 @@ __device__ inline void finish_task(const RArgs &a, TaskRes *rt, int p, int r, in
     __hip_atomic_store(&rt->status, out.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Persistent sweep workgroups take tasks t = (rank r = t / P, pair p = t % P)
-// from a global counter: every pair's first hypothesis, then every pair's
-// second, ...  Each sweep is independent of the others; the sequential rule is
-// applied afterwards (ransac_replay_kernel).  Two exact shortcuts from the
+// Persistent sweep workgroups take tasks t = ((r * P + p) * split + part) from a
+// global counter: every pair's first hypothesis (rank r = 0), then every
+// pair's second, ...; with split > 1 a task's chunks are shared by `split`
+// consecutive parts (finish_task combines them).  Each sweep is independent of
+// the others; the sequential rule is applied afterwards
+// (ransac_replay_kernel).  Two exact shortcuts from the
 // tasks of the same pair that are already finished:
 //  * cut bound: a hypothesis with more than n - c misses, c = the inliers of
 //    any earlier finished hypothesis, is below the best at its turn (whose
