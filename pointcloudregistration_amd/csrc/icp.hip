@@ -84,9 +84,7 @@ __device__ __forceinline__ void wave_park(IShared &sh, const xs_t *v, int q0) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        xs_t x = v[q];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) x += xs_shfl_xor(x, o);
+        const xs_t x = xs_wave_sum(v[q]);
         if (lane == 0) sh.ws[wid][q0 + q] = x;
     }
 }
@@ -100,9 +98,7 @@ __device__ __forceinline__ void wave_park_f64(IShared &sh, const double *v, int 
         double d = v[0];
 #pragma unroll
         for (int t = 1; t < NQ; ++t) d = (q == t) ? v[t] : d;
-        xs_t x = xs_term(d);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) x += xs_shfl_xor(x, o);
+        const xs_t x = xs_wave_sum(xs_term(d));
         if (lane == 0) sh.ws[wid][q0 + q] = x;
     }
 }

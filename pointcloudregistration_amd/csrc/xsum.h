@@ -58,6 +58,38 @@ __device__ inline double xs_to_double(xs_t v) {
     return neg ? -r : r;
 }
 
+// one DPP row rotation of a 128-bit value (ctrl 0x120 + n: row_ror:n)
+template <int kCtrl>
+__device__ __forceinline__ xs_t xs_dpp(xs_t v) {
+    const unsigned __int128 u = (unsigned __int128)v;
+    unsigned l[4] = {(unsigned)u, (unsigned)(u >> 32), (unsigned)(u >> 64), (unsigned)(u >> 96)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) l[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)l[k], kCtrl, 0xf, 0xf, false);
+    return (xs_t)(((unsigned __int128)l[3] << 96) | ((unsigned __int128)l[2] << 64) |
+                  ((unsigned __int128)l[1] << 32) | (unsigned __int128)l[0]);
+}
+
+__device__ __forceinline__ xs_t xs_readlane(xs_t v, int lane) {
+    const unsigned __int128 u = (unsigned __int128)v;
+    const unsigned l0 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned l1 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    const unsigned l2 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 64), lane);
+    const unsigned l3 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 96), lane);
+    return (xs_t)(((unsigned __int128)l3 << 96) | ((unsigned __int128)l2 << 64) |
+                  ((unsigned __int128)l1 << 32) | (unsigned __int128)l0);
+}
+
+// the wave's total of one 128-bit value per lane (uniform result).  Integer
+// sums are exact, so the tree shape is free: rotate-add within each row of 16
+// lanes by 1, 2, 4, 8 (DPP, no LDS round trips), then the four row sums.
+__device__ __forceinline__ xs_t xs_wave_sum(xs_t x) {
+    x += xs_dpp<0x121>(x);
+    x += xs_dpp<0x122>(x);
+    x += xs_dpp<0x124>(x);
+    x += xs_dpp<0x128>(x);
+    return (xs_readlane(x, 0) + xs_readlane(x, 16)) + (xs_readlane(x, 32) + xs_readlane(x, 48));
+}
+
 __device__ __forceinline__ xs_t xs_shfl_xor(xs_t v, int o) {
     const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
     const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
