@@ -75,7 +75,7 @@ __device__ __forceinline__ double cell_gap(double p, int c, double cell) {
 // LDS loads overlap.  The update order (slot order, strict < then lower index
 // on ties) makes the result independent of both.
 // kSlot: also report the winner's slot (its coordinates are g.x/y/z[slot])
-template <typename View, bool kSlot = false>
+template <typename View, bool kSlot = false, int kW = 2>
 __device__ __forceinline__ int grid_query(const View &g, double r, double thr, double px,
                                           double py, double pz, double &d2out, int *slot = nullptr) {
     // The build assigns cells by floor(v / cell); here floor(v * inv_cell) over
@@ -137,11 +137,19 @@ __device__ __forceinline__ int grid_query(const View &g, double r, double thr, d
         // up to two candidates per step, both from the current range (one site
         // shifts the queue: a wave pays the shift once per step, not twice)
         while (total > 0) {
-            const int sa = s;
-            const bool hb = s + 1 < e;
-            const int sbb = hb ? s + 1 : s;
-            s += hb ? 2 : 1;
-            total -= hb ? 2 : 1;
+            // up to kW candidates per step, all from the current range
+            int sl[kW];
+            bool ok[kW];
+#pragma unroll
+            for (int u = 0; u < kW; ++u) {
+                ok[u] = u == 0 || s + u < e;
+                sl[u] = ok[u] ? s + u : s;
+            }
+            int took = 1;
+#pragma unroll
+            for (int u = 1; u < kW; ++u) took += ok[u] ? 1 : 0;
+            s += took;
+            total -= took;
             if (s >= e) {  // next range: shift the queue down by one
 #pragma unroll
                 for (int k = 0; k < 7; ++k) q[k] = q[k + 1];
@@ -149,18 +157,18 @@ __device__ __forceinline__ int grid_query(const View &g, double r, double thr, d
                 s = (int)(q[0] & 0xffffu);
                 e = (int)(q[0] >> 16);
             }
-            float ax, ay, az, aw, bx, by, bz, bw;
-            g.load(sa, ax, ay, az, aw);
-            g.load(sbb, bx, by, bz, bw);
-            const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
-            const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
-            if (da < thr) {
-                const int j = g.index_of(sa, aw);
-                if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = sa; }
-            }
-            if (hb && db < thr) {
-                const int j = g.index_of(sbb, bw);
-                if (db < best || (db == best && j < bj)) { best = db; bj = j; if constexpr (kSlot) bs = sbb; }
+            float cx[kW], cy[kW], cz[kW], cw[kW];
+#pragma unroll
+            for (int u = 0; u < kW; ++u) g.load(sl[u], cx[u], cy[u], cz[u], cw[u]);
+            double dd[kW];
+#pragma unroll
+            for (int u = 0; u < kW; ++u) dd[u] = dist2(px, py, pz, (double)cx[u], (double)cy[u], (double)cz[u]);
+#pragma unroll
+            for (int u = 0; u < kW; ++u) {
+                if (ok[u] && dd[u] < thr) {
+                    const int j = g.index_of(sl[u], cw[u]);
+                    if (dd[u] < best || (dd[u] == best && j < bj)) { best = dd[u]; bj = j; if constexpr (kSlot) bs = sl[u]; }
+                }
             }
         }
     } else {

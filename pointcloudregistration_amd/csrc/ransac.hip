@@ -40,6 +40,10 @@
 #include <cstdlib>
 #include <vector>
 
+#ifndef PCR_RANSAC_KW
+#define PCR_RANSAC_KW 4  // candidates per grid-walk step in the RANSAC sweeps
+#endif
+
 namespace pcr {
 namespace {
 
@@ -294,7 +298,7 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
             const int i = ord ? ord[k] : k;
             double px, py, pz, d2;
             xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
-            j = grid_query(gr, a.d, a.thr, px, py, pz, d2);
+            j = grid_query<Grid, false, PCR_RANSAC_KW>(gr, a.d, a.thr, px, py, pz, d2);
             if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
             if (cbuf) cbuf[by_order ? k : i] = j;
         }
