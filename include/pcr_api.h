@@ -406,6 +406,16 @@ int pcr_ndp_control(const float *loss, double *state, double break_threshold_rat
 int pcr_adam_masked(const pcr_adam_tensor *tensors, int32_t n_tensors, int32_t max_numel,
                     const double *state, double lr, double beta1, double beta2, double eps,
                     pcr_stream_t stream);
+/* pcr_set_gate: the early stop that stops the work (registration.py:250-256
+ *   `break`s out of the level).  While a gate is set on the calling thread
+ *   (gate = the level's state, a device pointer), every kernel that
+ *   pcr_nnd_forward / pcr_nnd_backward / pcr_ndp_train_forward /
+ *   pcr_ndp_train_backward / pcr_ndp_chamfer_glue launch reads gate[0] at entry
+ *   and returns at once when it is 0 -- so the replays of a captured level graph
+ *   left after the rule fired cost only their launches.  pcr_set_gate(NULL)
+ *   restores ungated launches.  Thread-local; captured launches keep the pointer
+ *   they were recorded with. */
+int pcr_set_gate(const double *gate);
 
 /* ---------------------------------------------------------------------------
  * f4 -- fused NDP level training step (one level of

@@ -77,6 +77,7 @@ SIGNATURES = {
     "pcr_transform_batch": [_p, _i32, _i32, _p, _p, _p],
     "pcr_ndp_control": [_p, _p, _f64, _i32, _f64, _p],
     "pcr_adam_masked": [_p, _i32, _i32, _p, _f64, _f64, _f64, _f64, _p],
+    "pcr_set_gate": [_p],
     "pcr_ndp_train_forward": [_p, _p],
     "pcr_ndp_train_backward": [_p, _p, _i32, _p, _p],
     "pcr_ndp_chamfer_glue": [_p, _i32, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _p, _p, _i32, _p],

@@ -183,9 +183,11 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     for (int k = 0; k < 16; ++k) ident = ident && (sh.T[k] == ((k % 5 == 0) ? 1.0 : 0.0));
     const int stride = G * kThreads, base = g * kThreads + tid;
     // Umeyama lanes (lane l: source indices l, l + 1024, ... summed in order in
-    // f64): workgroup g owns lanes [g*LG, (g+1)*LG), one per thread
-    const int LG = kLanes / G;
-    const int my_lane = tid < LG ? g * LG + tid : -1;
+    // f64): workgroup g owns lanes [g*LG, min((g+1)*LG, kLanes)), one per
+    // thread; LG rounds up so every lane has an owner for any G (G = 3: 342,
+    // 342, 340).  The lane sums are exact, so ownership never changes a bit.
+    const int LG = (kLanes + G - 1) / G;
+    const int my_lane = (tid < LG && g * LG + tid < kLanes) ? g * LG + tid : -1;
     if (valid) {  // working copy = init applied to the f32 input (Open3D's Transform)
         double T0[12];
         for (int q = 0; q < 12; ++q) T0[q] = sh.T[q];

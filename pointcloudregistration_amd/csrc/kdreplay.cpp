@@ -15,9 +15,40 @@
 // std::sort and the same comparator -- libstdc++'s introsort is deterministic
 // given its input sequence, so the output equals the reference's.
 //
-// The tree restates nanoflann's algorithm (KDTreeBaseClass::divideTree /
-// middleSplit_ / planeSplit, KDTreeSingleIndexAdaptor::searchLevel); it is not
-// a copy of its code.
+// The tree build and search below follow nanoflann 1.3.0's divideTree /
+// middleSplit_ / planeSplit and searchLevel closely (their order of operations
+// is what fixes the output order), so nanoflann's licence applies to those
+// parts.  Its notice, as the vendored header carries it:
+//
+//   Software License Agreement (BSD License)
+//
+//   Copyright 2008-2009  Marius Muja (mariusm@cs.ubc.ca). All rights reserved.
+//   Copyright 2008-2009  David G. Lowe (lowe@cs.ubc.ca). All rights reserved.
+//   Copyright 2011-2016  Jose Luis Blanco (joseluisblancoc@gmail.com).
+//     All rights reserved.
+//
+//   THE BSD LICENSE
+//
+//   Redistribution and use in source and binary forms, with or without
+//   modification, are permitted provided that the following conditions
+//   are met:
+//
+//   1. Redistributions of source code must retain the above copyright
+//      notice, this list of conditions and the following disclaimer.
+//   2. Redistributions in binary form must reproduce the above copyright
+//      notice, this list of conditions and the following disclaimer in the
+//      documentation and/or other materials provided with the distribution.
+//
+//   THIS SOFTWARE IS PROVIDED BY THE AUTHOR ``AS IS'' AND ANY EXPRESS OR
+//   IMPLIED WARRANTIES, INCLUDING, BUT NOT LIMITED TO, THE IMPLIED WARRANTIES
+//   OF MERCHANTABILITY AND FITNESS FOR A PARTICULAR PURPOSE ARE DISCLAIMED.
+//   IN NO EVENT SHALL THE AUTHOR BE LIABLE FOR ANY DIRECT, INDIRECT,
+//   INCIDENTAL, SPECIAL, EXEMPLARY, OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT
+//   NOT LIMITED TO, PROCUREMENT OF SUBSTITUTE GOODS OR SERVICES; LOSS OF USE,
+//   DATA, OR PROFITS; OR BUSINESS INTERRUPTION) HOWEVER CAUSED AND ON ANY
+//   THEORY OF LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT
+//   (INCLUDING NEGLIGENCE OR OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF
+//   THIS SOFTWARE, EVEN IF ADVISED OF THE POSSIBILITY OF SUCH DAMAGE.
 #include <cstddef>
 #include <algorithm>
 #include <utility>

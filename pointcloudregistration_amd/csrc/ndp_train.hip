@@ -63,12 +63,14 @@ struct TrainArgs {
     const int32_t *inv;
     float *xs;
     const float *gsub;
+    const double *gate;             // f4 early stop (pcr_internal.h), or null
 };
 
 __device__ __forceinline__ float sgn_mask(float a, float d) { return a > 0.0f ? d : 0.0f; }
 
 // ---- forward of one level, saving what the backward needs -------------------
 __global__ __launch_bounds__(64 * kNT) void ndp_train_fwd(TrainArgs a) {
+    if (gated_off(a.gate)) return;
     constexpr int W = 32 * kNT;
     __shared__ TileX X[kNT];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5, j = l & 31;
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_fwd(TrainArgs a) {
 
 // ---- backward of one level: dL/dx' -> branch gradients -> layer deltas -----
 __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
+    if (gated_off(a.gate)) return;
     constexpr int W = 32 * kNT;
     __shared__ TileX X[kNT];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5, j = l & 31;
@@ -299,6 +302,7 @@ struct WgradJob {
 struct WgradArgs {
     WgradJob job[8];
     int N, chunk;     // points per chunk (multiple of 64)
+    const double *gate;
 };
 
 constexpr int kWgT = 64;  // points per LDS stage
@@ -306,6 +310,7 @@ constexpr int kWgT = 64;  // points per LDS stage
 // 16 waves: wave t owns output tile t of the job (a 128 x 128 weight is 4 x 4
 // tiles); the chains and the bias sums keep their point order
 __global__ __launch_bounds__(1024) void ndp_wgrad(WgradArgs a) {
+    if (gated_off(a.gate)) return;
     __shared__ float Ds[128][kWgT + 1], Xs[128][kWgT + 1];
     const WgradJob jb = a.job[blockIdx.y];
     const int c = blockIdx.x, nchunk = gridDim.x;
@@ -361,9 +366,11 @@ struct ReduceJob {
 struct ReduceArgs {
     ReduceJob job[8];
     int nchunk;
+    const double *gate;
 };
 
 __global__ __launch_bounds__(256) void ndp_wgrad_reduce(ReduceArgs a) {
+    if (gated_off(a.gate)) return;
     const ReduceJob jb = a.job[blockIdx.y];
     const int e = blockIdx.x * 256 + threadIdx.x;
     const int nw = jb.FO * jb.FI;
@@ -391,9 +398,11 @@ struct GlueArgs {
     float trunc, w_reg, g1, g2;
     float *gd1, *gd2, *loss, *log;
     long long *ctr;
+    const double *gate = nullptr;
 };
 
 __global__ __launch_bounds__(1024) void ndp_chamfer_glue(GlueArgs a) {
+    if (gated_off(a.gate)) return;
     __shared__ float red[3][16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
@@ -459,6 +468,7 @@ static int fill_train(const pcr_ndp_train *t, pcr::TrainArgs &a) {
     a.pe = t->pe; a.H = t->H; a.aux = t->aux; a.x_out = t->x_out;
     a.g = t->g; a.bce_scale = t->bce_scale; a.dO = t->dO; a.D = t->D;
     a.inv = t->inv; a.xs = t->xs; a.gsub = t->gsub;
+    a.gate = pcr::current_gate();
     return PCR_OK;
 }
 
@@ -494,6 +504,7 @@ extern "C" int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32
     pcr::WgradArgs wa{};
     pcr::ReduceArgs ra{};
     wa.N = N; wa.chunk = chunk; ra.nchunk = nchunk;
+    wa.gate = a.gate; ra.gate = a.gate;
     int nj = 0;
     size_t off = 0;
     auto add = [&](const float *D, const float *X, int FO, int FI, float *gw, float *gb) {
@@ -533,6 +544,7 @@ extern "C" int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2,
     pcr::GlueArgs g{d1, d2, s, K, M, N, log_last, (float)trunc, (float)w_reg,
                     (float)(1.0 / (double)K), (float)(1.0 / (double)M), gd1, gd2, loss, log,
                     (long long *)ctr};
+    g.gate = pcr::current_gate();
     hipLaunchKernelGGL(pcr::ndp_chamfer_glue, dim3(1), dim3(1024), 0, pcr::as_stream(stream), g);
     PCR_LAUNCH_CHECK();
     return PCR_OK;

@@ -48,6 +48,7 @@ struct NndArgs {
     int b, n, m;
     int slice_len;  // candidates per blockIdx.y slice (multiple of kTileK)
     int split;      // 1 if gridDim.y > 1
+    const double *gate = nullptr;  // f4 early stop (pcr_internal.h)
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -57,6 +58,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // 4 packed arithmetic instructions + compare/select per pair-evaluation.
 template <int QP>
 __global__ __launch_bounds__(kThreads) void nnd_fwd_kernel(NndArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     constexpr int Q = 2 * QP;
     __shared__ float4 sx[kTileK / 4], sy[kTileK / 4], sz[kTileK / 4];
 
@@ -155,6 +157,7 @@ __global__ __launch_bounds__(kThreads) void nnd_fwd_kernel(NndArgs a) {
 }
 
 __global__ __launch_bounds__(kThreads) void nnd_finalize_kernel(NndArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     const int dir = blockIdx.z & 1;
     const int bat = blockIdx.z >> 1;
     const int nq = dir ? a.m : a.n;
@@ -188,6 +191,7 @@ struct BwdArgs {
     int *uns1, *uns2;      // bucketed sources (unordered)
     int *srt1, *srt2;      // bucketed sources (increasing)
     int b, n, m;
+    const double *gate;    // f4 early stop (pcr_internal.h)
 };
 
 __device__ __forceinline__ bool bw_dir(const BwdArgs &a, int dir, int &nsrc, int &ntgt,
@@ -204,6 +208,7 @@ __device__ __forceinline__ bool bw_dir(const BwdArgs &a, int dir, int &nsrc, int
 }
 
 __global__ void bw_count(BwdArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     int nsrc, ntgt; const int32_t *tidx; int *cnt, *start, *uns, *srt;
     const int dir = blockIdx.z & 1, bat = blockIdx.z >> 1;
     bw_dir(a, dir, nsrc, ntgt, tidx, cnt, start, uns, srt);
@@ -217,6 +222,7 @@ __global__ void bw_count(BwdArgs a) {
 // one block per (dir, batch): exclusive scan of counts; counts reset to 0 to be
 // reused as fill cursors
 __global__ __launch_bounds__(1024) void bw_scan(BwdArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     int nsrc, ntgt; const int32_t *tidx; int *cnt, *start, *uns, *srt;
     const int dir = blockIdx.z & 1, bat = blockIdx.z >> 1;
     bw_dir(a, dir, nsrc, ntgt, tidx, cnt, start, uns, srt);
@@ -224,6 +230,7 @@ __global__ __launch_bounds__(1024) void bw_scan(BwdArgs a) {
 }
 
 __global__ void bw_fill(BwdArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     int nsrc, ntgt; const int32_t *tidx; int *cnt, *start, *uns, *srt;
     const int dir = blockIdx.z & 1, bat = blockIdx.z >> 1;
     bw_dir(a, dir, nsrc, ntgt, tidx, cnt, start, uns, srt);
@@ -237,6 +244,7 @@ __global__ void bw_fill(BwdArgs a) {
 
 // rank each bucketed source among its bucket (sources are distinct) -> sorted slot
 __global__ void bw_rank(BwdArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     int nsrc, ntgt; const int32_t *tidx; int *cnt, *start, *uns, *srt;
     const int dir = blockIdx.z & 1, bat = blockIdx.z >> 1;
     bw_dir(a, dir, nsrc, ntgt, tidx, cnt, start, uns, srt);
@@ -254,6 +262,7 @@ __global__ void bw_rank(BwdArgs a) {
 
 // per xyz1 point j (dir=0 targets are xyz2 points ... see header comment)
 __global__ void bw_chain(BwdArgs a) {
+    if (pcr::gated_off(a.gate)) return;
     const int which = blockIdx.z & 1;  // 0: grad1 over xyz1 points, 1: grad2 over xyz2 points
     const int bat = blockIdx.z >> 1;
     const int n = a.n, m = a.m;
@@ -358,6 +367,7 @@ extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, 
         slices *= 2;
     NndArgs a{xyz1, xyz2, dist1, dist2, idx1, idx2, nullptr, nullptr, b, n, m, 0, slices > 1};
     a.slice_len = cdiv(cdiv(nmax, slices), kTileK) * kTileK;
+    a.gate = pcr::current_gate();
     const int ys = cdiv(nmax, a.slice_len);
     PCR_REQUIRE(2LL * b <= 65535, PCR_ERR_ARG, "nnd_forward: b=%d too large (max 32767)", b);
     if (a.split) {
@@ -400,6 +410,7 @@ extern "C" int pcr_nnd_backward(const float *xyz1, const float *xyz2, const floa
     BwdArgs a;
     a.xyz1 = xyz1; a.xyz2 = xyz2; a.gd1 = gd1; a.gd2 = gd2; a.idx1 = idx1; a.idx2 = idx2;
     a.g1 = g1; a.g2 = g2; a.b = b; a.n = n; a.m = m;
+    a.gate = pcr::current_gate();
     int *p = ws;
     a.cnt1 = p; p += bm;
     a.cnt2 = p; p += bn;

@@ -40,6 +40,7 @@ struct NgArgs {
     float4 *pts;          // [2][B][nmax]
     float *dist[2];       // dist[0] = dist1: queries of set 0 against the grid of set 1
     int32_t *idx[2];
+    const double *gate;   // f4 early stop (pcr_internal.h), or null
 };
 
 __device__ __forceinline__ unsigned nhash(int x, int y, int z, int S) {
@@ -50,6 +51,7 @@ __device__ __forceinline__ unsigned nhash(int x, int y, int z, int S) {
 __device__ __forceinline__ int ccoord(float v, double ic) { return (int)__builtin_floor((double)v * ic); }
 
 __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
+    if (gated_off(a.gate)) return;
     const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x, n = a.n[s];
     const float *P = a.xyz[s] + (size_t)b * n * 3;
     float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
@@ -100,6 +102,7 @@ __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
 }
 
 __global__ void nng_count(NgArgs a) {
+    if (gated_off(a.gate)) return;
     const int s = blockIdx.z, b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n[s] || a.flag[b]) return;
     const float *p = a.xyz[s] + ((size_t)b * a.n[s] + i) * 3;
@@ -109,6 +112,7 @@ __global__ void nng_count(NgArgs a) {
 }
 
 __global__ __launch_bounds__(1024) void nng_scan(NgArgs a) {
+    if (gated_off(a.gate)) return;
     const int s = blockIdx.y, b = blockIdx.x;
     if (a.flag[b]) return;
     const size_t g = (size_t)s * a.B + b;
@@ -116,6 +120,7 @@ __global__ __launch_bounds__(1024) void nng_scan(NgArgs a) {
 }
 
 __global__ void nng_scatter(NgArgs a) {
+    if (gated_off(a.gate)) return;
     const int s = blockIdx.z, b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n[s] || a.flag[b]) return;
     const float *p = a.xyz[s] + ((size_t)b * a.n[s] + i) * 3;
@@ -133,6 +138,7 @@ __global__ void nng_scatter(NgArgs a) {
 constexpr int kLdsSlots = 32768;
 
 __global__ __launch_bounds__(1024) void nng_build(NgArgs a) {
+    if (gated_off(a.gate)) return;
     extern __shared__ int cnt[];  // S + 1: counts -> exclusive starts -> cursors
     const int s = blockIdx.x, b = blockIdx.y, S = a.S, n = a.n[s];
     if (a.flag[b]) return;  // nng_bbox ran before on this stream
@@ -179,6 +185,7 @@ __device__ __forceinline__ int xcd_slot(int L, int total) {
 // answer.
 template <int LPQ>
 __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
+    if (gated_off(a.gate)) return;
     constexpr int QPB = 256 / LPQ;
     const int w = xcd_slot(blockIdx.x, gridDim.x);
     const int grp = w / nchunk, chunk = w - grp * nchunk;
@@ -295,6 +302,7 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
     a.hcnt = a.flag + b;
     a.start = a.hcnt + hc;
     a.dist[0] = dist1; a.dist[1] = dist2; a.idx[0] = idx1; a.idx[1] = idx2;
+    a.gate = current_gate();
     const bool lds_build = S <= kLdsSlots;
     PCR_HIP_CHECK(hipMemsetAsync(a.flag, 0, sizeof(int) * (lds_build ? (size_t)b : b + hc), s));
     hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(1024), 0, s, a);

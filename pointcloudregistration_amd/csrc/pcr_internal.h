@@ -26,6 +26,13 @@ enum ProfId { kProfFeatScreen = 0, kProfNndFwd = 1, kProfRansacValidate = 2, kPr
 void prof_begin(hipStream_t s, int id);
 void prof_end(hipStream_t s, int id);
 
+// f4 early stop: a thread-local gate pointer (pcr_set_gate).  Kernels that an
+// NDP level graph captures carry it and return at entry once gate[0] == 0 (the
+// level's early-stop rule fired, pcr_ndp_control's state[0]), so the replays
+// left after the break do no work.  Null: ungated (every other caller).
+const double *current_gate();
+__device__ __forceinline__ bool gated_off(const double *g) { return g != nullptr && *g == 0.0; }
+
 constexpr int kWave = 64;
 constexpr int kCUs = 256;
 

@@ -126,7 +126,17 @@ void prof_end(hipStream_t s, int id) {
     t_begin[id] = nullptr;
 }
 
+namespace {
+thread_local const double *t_gate = nullptr;
+}
+const double *current_gate() { return t_gate; }
+
 }  // namespace pcr
+
+extern "C" int pcr_set_gate(const double *gate) {
+    pcr::t_gate = gate;
+    return PCR_OK;
+}
 
 extern "C" void pcr_profile_enable(int32_t on) {
     std::lock_guard<std::mutex> lk(pcr::g_pmu);

@@ -169,6 +169,8 @@ def _bce_to_zero(p):
 
 
 class _Level:
+    CHECK = 8  # replays between the host's looks at the early-stop flag
+
     def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig):
         dev = s_sample.device
         self.layer, self.level, self.cfg = layer, level, cfg
@@ -240,8 +242,13 @@ class _Level:
             self.step()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
-        for _ in range(iters):
+        for k in range(iters):
             g.replay()
+            # the replays after the rule fired are no-ops (gated kernels); every
+            # CHECK replays the host looks whether the level has stopped and
+            # skips the rest (one 8-byte read; the results do not depend on it)
+            if (k + 1) % self.CHECK == 0 and k + 1 < iters and self.state[0].item() == 0.0:
+                break
         ev[1].record()
         self.replay_events = ev
 
@@ -355,6 +362,16 @@ class _LevelFused(_Level):
         self.table = torch.from_numpy(raw).to(self.s.device)
 
     def step(self):
+        # every libpcr kernel of the iteration is gated on state[0]: after the
+        # early-stop rule fired, the remaining replays of the level graph return
+        # at once (registration.py:250-256 breaks out of the level)
+        _lib.call("pcr_set_gate", _lib.ptr(self.state))
+        try:
+            self._step()
+        finally:
+            _lib.call("pcr_set_gate", None)
+
+    def _step(self):
         from .nndistance import nnd_backward_cuda, nnd_forward_cuda
         cfg = self.cfg
         st = _lib.stream_handle(self.s.device)

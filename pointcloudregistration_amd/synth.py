@@ -83,6 +83,30 @@ def make_pair(seed, n=8192, m=8192, d=32, overlap_pool=1.45, max_angle_deg=45.0,
     return src, tgt, fs, ft, R, t, ids.astype(np.int32), idt.astype(np.int32)
 
 
+def deform_field(u, amp):
+    """A smooth non-rigid displacement (C5: the intra-operative surface is a
+    deformed copy of the pre-operative one): sinusoids of ~2.5 rad per unit,
+    faded in along x by a logistic ramp, so one end of the blob stays rigid
+    (RANSAC finds its inliers there) and the other moves by up to ~amp."""
+    u = np.asarray(u, np.float64)
+    ramp = 1.0 / (1.0 + np.exp(-6.0 * u[:, 0]))
+    f = np.stack([np.sin(2.5 * u[:, 1] + 0.3), np.sin(2.5 * u[:, 2] + 1.1),
+                  np.sin(2.5 * u[:, 0] + 2.0)], axis=1)
+    return amp * ramp[:, None] * f
+
+
+def make_c5_pair(seed, n=20000, m=20000, d=32, deform=0.15, feat_noise=0.5, **kw):
+    """make_pair with the target deformed by deform_field before the rigid
+    motion is undone on the source: tgt = U + f(U) + jitter, src = R^-1 (U - t) +
+    jitter.  Returns a PairBatch of one pair (R, t = the rigid part)."""
+    src, tgt, fs, ft, R, t, ids, idt = make_pair(seed, n, m, d, feat_noise=feat_noise, **kw)
+    rng = np.random.default_rng(seed)
+    pool_n = int(max(n, m) * kw.get("overlap_pool", 1.45))
+    U = surface_points(rng, pool_n)
+    tgt = (tgt + deform_field(U[idt], deform)).astype(np.float32)
+    return PairBatch(*[np.stack([x]) for x in (src, tgt, fs, ft, R, t, ids, idt)])
+
+
 def make_batch(pairs, n=8192, m=8192, d=32, base_seed=1000, first_pair=0, **kw):
     outs = [make_pair(base_seed + first_pair + p, n, m, d, **kw) for p in range(pairs)]
     return PairBatch(*[np.stack([o[k] for o in outs]) for k in range(8)])

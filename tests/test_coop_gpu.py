@@ -113,7 +113,7 @@ def test_ransac_multi_round_low_inlier_ratio(oracle, ransac_sched):
         assert st[:, 0].max() > 1024, st[:, 0]
 
 
-@pytest.mark.parametrize("G", [1, 2, 8])
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
 @pytest.mark.parametrize("n,noise_init,r,relf", [(3000, 0.01, 0.02, 1e-6), (4096, 0.08, 0.1, 0.0),
                                                  (20000, 0.03, 0.05, 1e-6)])
 def test_icp_split_bitexact_vs_oracle(oracle, coop_g, G, n, noise_init, r, relf):
@@ -138,6 +138,28 @@ def test_icp_split_bitexact_vs_oracle(oracle, coop_g, G, n, noise_init, r, relf)
         assert int((_np(res.corr_tgt)[p] >= 0).sum()) == o["n_corr"]
     if relf == 0.0:
         assert _np(res.stats)[:, 0].max() == 30
+
+
+def test_icp_library_chosen_uneven_split(oracle):
+    """85 pairs (a 256-pair job's shard on 3 GPUs): the library picks G itself
+    (3 on a 256-CU part), which does not divide the 1024 sum lanes -- every
+    lane must still have an owner (a lane without one dropped its points from
+    the means while they stayed in the count)."""
+    os.environ.pop("PCR_COOP_G", None)
+    P, n = 85, 2500
+    B = synth.make_batch(P, n=n, m=n, d=8, base_seed=850, feat_noise=1.0)
+    rng = np.random.default_rng(85)
+    init = np.zeros((P, 4, 4))
+    for p in range(P):
+        init[p, :3, :3] = synth.rotation_xyz(*rng.normal(0, 0.02, 3)) @ B.R[p]
+        init[p, :3, 3] = B.t[p] + rng.normal(0, 0.02, 3)
+        init[p, 3, 3] = 1
+    prm = reg.IcpParams(0.05)
+    res = reg.icp_batch(B.src, B.tgt, init, prm)
+    for p in range(P):
+        o = oracle.icp(B.src[p], B.tgt[p], 0.05, init=init[p])
+        assert _bits(_np(res.transformation)[p], o["T"]), p
+        assert tuple(_np(res.stats)[p]) == (o["iters"], o["n_corr"])
 
 
 @pytest.mark.parametrize("wgs,slots,split", [(None, None, None), (1, 0, 2), (4, 1, 1), (6, 1, 2)])
