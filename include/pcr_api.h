@@ -54,6 +54,9 @@ int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset
  * certify and sent to the exact f64 rescan since the last reset.  Synchronizes
  * the device. */
 int pcr_featnn_rescan_rows(int64_t *rows12, int64_t *rows21, int32_t reset);
+/* diagnostic: copy `bytes` of pcr_feature_correspondences' scratch from its
+ * last call (device to device, on `stream`) */
+int pcr_featmut_debug_copy(void *dst, int64_t bytes, pcr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * a1 -- brute-force bidirectional 1-NN ("nnd" / Chamfer building block).
@@ -110,6 +113,20 @@ int pcr_correspondences(const int32_t *nn12, const int32_t *nn21, int32_t P, int
                         int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt,
                         int32_t mutual_filter, int32_t ransac_n, int32_t *corres,
                         int32_t *n_corres, pcr_stream_t stream);
+
+/* feature matching + mutual filter in one call: the correspondences the
+ * two calls above produce (bit-identical corres / n_corres, and nn12), without
+ * computing nn21 for every target -- the filter reads nn21 only at j = nn12[i]
+ * (Open3D 0.13 RegistrationRANSACBasedOnFeatureMatching with mutual_filter,
+ * DataPreparation/RANSAC.py:43-52).  The column direction is screened only for
+ * the targets some source picked, and decided from certified screen values
+ * (csrc/featnn.hip featnn_row7).  With mutual_filter == 0 only nn12 is
+ * computed.  nn12 (P,Nmax) out; corres (P,Nmax,2), n_corres (P) out. */
+int pcr_feature_correspondences(const float *src_feat, const float *tgt_feat, int32_t P,
+                                int32_t Nmax, int32_t Mmax, int32_t D, const int32_t *n_src,
+                                const int32_t *n_tgt, int32_t mutual_filter, int32_t ransac_n,
+                                int32_t *nn12, int32_t *corres, int32_t *n_corres,
+                                pcr_stream_t stream);
 
 /* RANSAC parameters (Open3D names; RANSAC.py:43-52). */
 typedef struct pcr_ransac_params {

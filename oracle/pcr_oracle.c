@@ -765,46 +765,68 @@ double oracle_xs_sum(const double *v, int n)
     return xs_to_double(a);
 }
 
-/* Umeyama over the correspondences of an ICP iteration.  Sums: 1024 lane      */
-/* partials (lane = source index mod 1024, f64 in increasing index), then the  */
-/* exact fixed-point sum of the lane partials (xs_* above), rounded once.      */
-#define ICP_LANES 1024
-static void lane_sums(const double *P, const double *Tg, const int32_t *cj, int n,
-                      const double *ms, const double *mt, int nq, double *out)
+/* Umeyama over the correspondences of an ICP iteration (round 3), one pass of   */
+/* EXACT sums.  Per pair: a reference point c0 = the first target point and a   */
+/* quantum 2^-k with k = 52 - e_n - e_max, where every inlier term below is at   */
+/* most 2^e_max in magnitude (|s - c0|, |t - c0| <= B = max_j |t_j - c0|_inf +   */
+/* 2d, since an inlier lies within d of its target; e_max = max(e_B, 2 e_B),     */
+/* B < 2^e_B) and n <= 2^e_n.  Each term -- s' = s - c0, t' = t - c0 and the 9  */
+/* products s'_a t'_b, all in f64 -- is truncated to a multiple of 2^-k; any    */
+/* partial sum of them is then an integer multiple of 2^-k below 2^52 * 2^-k, so */
+/* every f64 addition is exact and the sums do not depend on the order (the GPU  */
+/* adds them in any split over threads, waves and workgroups).  Then            */
+/*   ms' = Ss * (1/K), mt' = St * (1/K), C_ab = Sst_ab - ms'_a * St_b,          */
+/*   ms = ms' + c0, mt = mt' + c0, R = Horn(C), t = mt - R ms.                  */
+double oracle_icp_quantum(const double *Tg, int m, int n, double d, double c0[3])
 {
-    /* nq = 6: source xyz, target xyz; nq = 9: centred products (a, b) */
-    xs_t tot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int l = 0; l < ICP_LANES; l++) {
-        double part[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = l; i < n; i += ICP_LANES) {
-            if (cj[i] < 0) continue;
-            const double *p = P + 3 * i, *t = Tg + 3 * cj[i];
-            if (nq == 6) {
-                for (int c = 0; c < 3; c++) { part[c] = part[c] + p[c]; part[3 + c] = part[3 + c] + t[c]; }
-            } else {
-                for (int a = 0; a < 3; a++)
-                    for (int b = 0; b < 3; b++)
-                        part[3 * a + b] = part[3 * a + b] + (p[a] - ms[a]) * (t[b] - mt[b]);
-            }
+    c0[0] = Tg[0]; c0[1] = Tg[1]; c0[2] = Tg[2];
+    double bt = 0.0;
+    for (int j = 0; j < m; j++)
+        for (int a = 0; a < 3; a++) {
+            const double v = fabs(Tg[3 * j + a] - c0[a]);
+            if (v > bt) bt = v;
         }
-        for (int q = 0; q < nq; q++) tot[q] += xs_term(part[q]);
-    }
-    for (int q = 0; q < nq; q++) out[q] = xs_to_double(tot[q]);
+    const double B = bt + 2.0 * d;
+    int eb = 0;
+    frexp(B, &eb);                        /* B < 2^eb */
+    const int emax = eb > 2 * eb ? eb : 2 * eb;
+    int en = 0;
+    while ((1LL << en) < (long long)(n > 1 ? n : 1)) en++;
+    int k = 52 - en - emax;
+    if (k > 200) k = 200;
+    if (k < -200) k = -200;
+    return ldexp(1.0, k);                 /* 2^k */
 }
 
-static void umeyama_masked(const double *P, const double *Tg, const int32_t *cj, int n, double T[12])
+static inline double icp_q(double x, double sk, double isk) { return trunc(x * sk) * isk; }
+
+static void umeyama_masked(const double *P, const double *Tg, const int32_t *cj, int n,
+                           const double c0[3], double sk, double T[12])
 {
+    const double isk = 1.0 / sk;  /* exact: a power of two */
+    double Ss[3] = {0, 0, 0}, St[3] = {0, 0, 0}, Sst[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int K = 0;
-    for (int i = 0; i < n; i++) K += cj[i] >= 0;
-    const double one_over_n = 1.0 / (double)K;
-    double sums[6], ms[3], mt[3];
-    lane_sums(P, Tg, cj, n, NULL, NULL, 6, sums);
-    for (int c = 0; c < 3; c++) {
-        ms[c] = sums[c] * one_over_n;
-        mt[c] = sums[3 + c] * one_over_n;
+    for (int i = 0; i < n; i++) {
+        if (cj[i] < 0) continue;
+        K++;
+        const double *p = P + 3 * i, *t = Tg + 3 * cj[i];
+        double sp[3], tp[3];
+        for (int a = 0; a < 3; a++) { sp[a] = p[a] - c0[a]; tp[a] = t[a] - c0[a]; }
+        for (int a = 0; a < 3; a++) {
+            Ss[a] = Ss[a] + icp_q(sp[a], sk, isk);
+            St[a] = St[a] + icp_q(tp[a], sk, isk);
+            for (int b = 0; b < 3; b++) Sst[3 * a + b] = Sst[3 * a + b] + icp_q(sp[a] * tp[b], sk, isk);
+        }
     }
-    double S[9];
-    lane_sums(P, Tg, cj, n, ms, mt, 9, S);
+    const double one_over_n = 1.0 / (double)K;
+    double ms[3], mt[3], msp[3], S[9];
+    for (int c = 0; c < 3; c++) {
+        msp[c] = Ss[c] * one_over_n;
+        ms[c] = msp[c] + c0[c];
+        mt[c] = St[c] * one_over_n + c0[c];
+    }
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) S[3 * a + b] = Sst[3 * a + b] - msp[a] * St[b];
     double R[9];
     oracle_horn_rotation(S, R);
     for (int a = 0; a < 3; a++) {
@@ -840,13 +862,14 @@ int oracle_icp(const float *srcf, int n, const float *tgtf, int m, const double 
         for (int k = 0; k < 12; k++) T12[k] = T[k];
         for (int i = 0; i < n; i++) { double p[3]; xform(T12, P + 3 * i, p); memcpy(P + 3 * i, p, sizeof(p)); }
     }
-    double fit, rmse;
+    double fit, rmse, c0[3];
+    const double sk = oracle_icp_quantum(Tg, m, n, d, c0);
     int cnt = evaluate(&g, P, n, I12, d, thr, &fit, &rmse, cj);
     int it;
     for (it = 0; it < max_iter; it++) {
         if (cnt == 0) break; /* Umeyama on an empty set is undefined in Eigen; stop */
         double U[12], U16[16], Tn[16];
-        umeyama_masked(P, Tg, cj, n, U);
+        umeyama_masked(P, Tg, cj, n, c0, sk, U);
         t12_to_16(U, U16);
         mat4_mul(U16, T, Tn);
         memcpy(T, Tn, sizeof(T));

@@ -55,6 +55,7 @@ SIGNATURES = {
     "pcr_nnd_forward": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p],
     "pcr_nnd_backward": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p],
     "pcr_feature_match": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p],
+    "pcr_feature_correspondences": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p, _p],
     "pcr_correspondences": [_p, _p, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p],
     "pcr_ransac_batch": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _rp, _p, _p, _p,
                          _p, _p, _p],
@@ -78,6 +79,7 @@ SIGNATURES = {
     "pcr_ndp_control": [_p, _p, _f64, _i32, _f64, _p],
     "pcr_adam_masked": [_p, _i32, _i32, _p, _f64, _f64, _f64, _f64, _p],
     "pcr_set_gate": [_p],
+    "pcr_featmut_debug_copy": [_p, _i64, _p],
     "pcr_ndp_train_forward": [_p, _p],
     "pcr_ndp_train_backward": [_p, _p, _i32, _p, _p],
     "pcr_ndp_chamfer_glue": [_p, _i32, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _p, _p, _i32, _p],
@@ -131,7 +133,7 @@ def exported_symbols():
 
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
-PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID = 5, 6, 7
+PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID, PROF_FEAT_SCREEN2 = 5, 6, 7, 8
 
 
 def profile_enable(on=True):

@@ -94,11 +94,13 @@ inline Split5 split5_params(int D) {
 }
 
 // max |element| of each pair's clouds (f32 bits; both clouds -> same slot):
-// one 1024-thread block per (pair, cloud), float4 loads, one atomic per block
+// gridDim.z 1024-thread blocks per (pair, cloud), each a contiguous slice of
+// float4 loads (several in flight per thread), one atomic per block -- with few
+// pairs one block per cloud was a chain of ~64 dependent load round trips
 __global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_t *nf, int Nmax,
                                                     const float *G, const int32_t *ng, int Mmax,
                                                     int D, unsigned *mx) {
-    const int p = blockIdx.x, which = blockIdx.y, t = threadIdx.x;
+    const int p = blockIdx.x, which = blockIdx.y, t = threadIdx.x, z = blockIdx.z, Z = gridDim.z;
     const float *X = which ? G : F;
     const int cnt = which ? count_of(ng, p, Mmax) : count_of(nf, p, Nmax);
     const size_t tot = (size_t)cnt * D;
@@ -107,13 +109,16 @@ __global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_
     if (((uintptr_t)x & 15) == 0) {
         const float4 *x4 = reinterpret_cast<const float4 *>(x);
         const size_t t4 = tot >> 2;
-        for (size_t i = t; i < t4; i += 1024) {
+        const size_t per = (t4 + Z - 1) / Z, lo = min(t4, per * z), hi = min(t4, lo + per);
+#pragma unroll 4
+        for (size_t i = lo + t; i < hi; i += 1024) {
             const float4 v = x4[i];
             m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         }
-        for (size_t i = (t4 << 2) + t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
+        if (z == Z - 1)
+            for (size_t i = (t4 << 2) + t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
     } else {
-        for (size_t i = t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
+        for (size_t i = (size_t)z * 1024 + t; i < tot; i += (size_t)Z * 1024) m = fmaxf(m, fabsf(x[i]));
     }
 #pragma unroll
     for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
@@ -595,7 +600,24 @@ struct RescanArgs5 {
     int cap;
     double *sd;
     int *sj;
+    // mutual path (feature_corres_v5): the exact distance of a rescanned F row,
+    // in the screen's scaled units (x s^2, s = pair_scale5(mx[p], T): a power of
+    // two, exact), and its error 0; null elsewhere
+    double *v12;
+    float *e12;
+    const unsigned *mx;
+    int T;
 };
+
+__device__ __forceinline__ void rescan_out(const RescanArgs5 &a, int dir, int p, int row, double best,
+                                           int bj, int32_t *nn) {
+    nn[row] = (bj == 0x7fffffff) ? 0 : bj;
+    if (dir == 0 && a.v12) {
+        const double sc = (double)pair_scale5(a.mx[p], a.T);
+        a.v12[(size_t)p * a.Nmax + row] = best * sc * sc;
+        a.e12[(size_t)p * a.Nmax + row] = 0.0f;
+    }
+}
 
 template <int DV, bool V4>
 __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
@@ -740,7 +762,7 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
                 a.sd[slot] = best;
                 a.sj[slot] = bj;
             } else {
-                nn[row] = (bj == 0x7fffffff) ? 0 : bj;
+                rescan_out(a, dir, p, row, best, bj, nn);
             }
         }
     }
@@ -762,68 +784,440 @@ __global__ __launch_bounds__(256) void featnn_rescan_merge(RescanArgs5 a, int S)
             const int j = a.sj[slot + s];
             if (d < best || (d == best && j < bj)) { best = d; bj = j; }
         }
-        nn[list[e]] = (bj == 0x7fffffff) ? 0 : bj;
+        rescan_out(a, dir, p, list[e], best, bj, nn);
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Mutual correspondences without the column screen (feature_corres_v5).
+//
+// corres_build reads nn21 only at j = nn12[i], and nn12 hits ~half of the
+// targets, so the column direction is screened only for those: pass 1 screens
+// the rows (F against every G column, a top-2 per row with the column-tile
+// index packed into the value: 3 VALU per distance instead of dual7's ~6.6),
+// the uncertified rows are rescanned exactly, then pass 2 screens the rows
+// J = {nn12[i]} of G against every F column keeping top-2 VALUES only (2 VALU
+// per distance, no index), and the candidate i of column j = nn12[i] is decided
+// from values:
+//   pass 2 certifies column j when its top-2 gap exceeds 2 (e2 + e1_i), e2 the
+//   screen's bound for column j, e1_i that of row i's own value v_i (its pass-1
+//   b1 with the code bits' perturbation, or 0 when the row was rescanned); then
+//   the exact column argmin w has the screen minimum w1, D_w <= w1 + e2 and
+//   every other row is >= w2 - e2, so i is mutual iff v_i <= w1 + e2 + e1_i.
+//   A column that cannot be decided is rescanned exactly (featnn_rescan3,
+//   direction 1) and its candidates compared with that argmin.
+// The result is the same set corres_build forms from the exact nn12 / nn21.
+// ---------------------------------------------------------------------------
+struct RowArgs5 {
+    const f16x8 *Ap;            // row operand (register-resident): [P][ntr][NCH][64]
+    const f16x8 *Bp;            // column operand (LDS-streamed): [P][ntc][NCH][64]
+    const float *rnr;           // scaled row norms, [P][ntr * 32] by original row index
+    const unsigned *cmax;       // per pair max scaled column norm (f32 bits)
+    const int32_t *n_rows, *n_cols;
+    const int *rlist, *rcount;  // pass 2: rows rlist[p][0 .. rcount[p]) (original indices)
+    int P, Rmax, Cmax, ntr, ntc, nrb, D, ctbits;
+    int32_t *nn;                // pass 1: argmin (screened), value, its error, uncertified rows
+    double *v;
+    float *e;
+    int *list, *count;
+    float *w1, *w2;             // pass 2: top-2 values by original row index
+};
+
+template <int NCH, int G, bool kIdx>
+__global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
+    constexpr int W = 8;              // waves per workgroup, one 32-row tile each
+    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
+    __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
+    if (p >= a.P) return;  // whole block
+    const int nr = a.rlist ? a.rcount[p] : count_of(a.n_rows, p, a.Rmax);
+    if (rb * W * 32 >= nr) return;  // whole block: no rows here
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int m = count_of(a.n_cols, p, a.Cmax);
+    const int qt = rb * W + wid;
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    const unsigned ctmask = (1u << a.ctbits) - 1u;
+    unsigned keep_r = ~ctmask;
+    asm("" : "+v"(keep_r));
+    f16x8 A[NCH];
+    if (a.rlist) {  // gathered rows: lane l holds row slot qt*32 + (l & 31), half h
+        const int k = qt * 32 + (l & 31);
+        if (k < nr) {
+            const int j = a.rlist[(size_t)p * a.Rmax + k];
+            const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + (j >> 5)) * NCH * 64 + (j & 31) + 32 * h;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
+        } else {
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) A[c][q] = (_Float16)0.0f;
+        }
+    } else {
+        const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt) * NCH * 64 + l;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
+    }
+    float b1[16], b2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NCH * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * NCH; c += W) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
+        }
+    };
+    // row top-2 of the tile's 16 values per lane: pass 1 with the column tile
+    // index in the low ctbits bits (3 VALU per value), pass 2 values only (2)
+    auto epilogue = [&](const f32x16 &acc, unsigned ct) {
+        asm("" : "+s"(ct));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float vr;
+            if constexpr (kIdx) vr = __uint_as_float((__float_as_uint(acc[r]) & keep_r) | ct);
+            else vr = acc[r];
+            b2[r] = vmed3(b1[r], b2[r], vr);
+            b1[r] = vmin(b1[r], vr);
+        }
+    };
+    constexpr int kV = kIdx ? 7 : 5;  // VALU per MFMA slot in the schedule below
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = grp & 1;
+        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        const f16x8 *Bb = Bs + buf * kB + l;
+        f16x8 Bf[2][NCH];
+        f32x16 acc[2];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) Bf[0][c] = Bb[c * 64];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int cur = g & 1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[cur][r] = 0.0f;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+                acc[cur] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bf[cur][c], acc[cur], 0, 0, 0);
+            if (g + 1 < G) {
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NCH + c) * 64];
+            }
+            if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1));
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
+            }
+        }
+        epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1));
+        // the next group's DMA has landed for every wave, and every wave is done
+        // reading this buffer before the group after next overwrites it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (qt * 32 >= nr) return;
+    const int lr = l & 31;
+    if constexpr (kIdx) {
+        int i1[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + lr;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float ob1 = __shfl_xor(b1[r], o, 64);
+                const float ob2 = __shfl_xor(b2[r], o, 64);
+                const int oi1 = __shfl_xor(i1[r], o, 64);
+                top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+            }
+        }
+        if (lr >= 16) return;
+        float mb1 = 0.f, mb2 = 0.f;
+        int mi1 = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
+        const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+        if (row >= nr) return;
+        const size_t o = (size_t)p * a.Rmax + row;
+        if (m == 0) {
+            a.nn[o] = 0;
+            a.v[o] = __builtin_inf();
+            a.e[o] = 0.0f;
+            return;
+        }
+        a.nn[o] = mi1;
+        const double Gm = (double)__uint_as_float(a.cmax[p]);
+        const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+        const double bnd = bound5(qn, Gm, 16 * NCH, a.D);
+        const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
+        a.v[o] = (double)mb1;
+        a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
+        if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
+            a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
+    } else {
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float ob1 = __shfl_xor(b1[r], o, 64);
+                const float ob2 = __shfl_xor(b2[r], o, 64);
+                b2[r] = vmin(vmax(b1[r], ob1), vmin(b2[r], ob2));
+                b1[r] = vmin(b1[r], ob1);
+            }
+        }
+        if (lr >= 16) return;
+        float mb1 = 0.f, mb2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; }
+        const int k = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+        if (k >= nr) return;
+        const int j = a.rlist[(size_t)p * a.Rmax + k];
+        a.w1[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb1;
+        a.w2[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb2;
+    }
+}
+
+struct MutArgs {
+    const int32_t *nn12, *n_src, *n_tgt;
+    int Nmax, Mmax, mutual, ransac_n, Kt, D, ntm;
+    int *used;        // [P][Mmax + 1]: 1 = some i has nn12[i] = j (2: listed for the rescan)
+    int *pos;         // [P][Mmax + 1] scan scratch
+    int *jlist, *nj;  // [P][Mmax], [P]: the rows of pass 2, ascending
+    const double *v12;
+    const float *e12;
+    const float *w1, *w2, *gnr;
+    const unsigned *fmax;
+    int *flag;        // [P][Nmax + 1]: mutual 0 / 1, 2 = decided by the exact column
+    int *list21, *cnt21;
+    const int32_t *nn21x;
+    int32_t *corres, *n_corres;
+};
+
+// J = {nn12[i]} of each pair, ascending (one workgroup per pair)
+__global__ __launch_bounds__(1024) void featmut_jbuild(MutArgs a) {
+    const int p = blockIdx.x;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    int *u = a.used + (size_t)p * (a.Mmax + 1);
+    int *ps = a.pos + (size_t)p * (a.Mmax + 1);
+    int *jl = a.jlist + (size_t)p * a.Mmax;
+    const int32_t *nn = a.nn12 + (size_t)p * a.Nmax;
+    for (int j = threadIdx.x; j < m; j += 1024) u[j] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const int j = nn[i];
+        if (j >= 0 && j < m) u[j] = 1;  // plain stores of one value: no race on the result
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < m; j += 1024) ps[j] = u[j];
+    __syncthreads();
+    block_exclusive_scan_1024(ps, ps, m, false);
+    for (int j = threadIdx.x; j < m; j += 1024)
+        if (u[j]) jl[ps[j]] = j;
+    if (threadIdx.x == 0) a.nj[p] = ps[m];
+}
+
+// decide each candidate from the pass-2 values, list the undecidable columns
+// (once each) for the exact rescan
+__global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
+    const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    if (i >= n) return;
+    const int j = a.nn12[(size_t)p * a.Nmax + i];
+    int f = 0;
+    if (j >= 0 && j < m) {
+        const size_t oj = (size_t)p * a.Mmax + j, oi = (size_t)p * a.Nmax + i;
+        const double w1 = (double)a.w1[oj], w2 = (double)a.w2[oj];
+        const double e2 = 0.5 * bound5((double)a.gnr[(size_t)p * a.ntm * 32 + j],
+                                       (double)__uint_as_float(a.fmax[p]), a.Kt, a.D);
+        const double vi = a.v12[oi], e1 = (double)a.e12[oi];
+        // slack: the f64 sums of a rescanned value vs the exact real distance
+        const double sl = 1e-9 * (__builtin_fabs(w1) + __builtin_fabs(vi));
+        if (w2 - w1 > 2.0 * (e2 + e1 + sl)) {
+            f = (vi <= w1 + e2 + e1 + sl) ? 1 : 0;
+        } else {
+            f = 2;
+            if (atomicCAS(a.used + (size_t)p * (a.Mmax + 1) + j, 1, 2) == 1)
+                a.list21[(size_t)p * a.Mmax + atomicAdd(a.cnt21 + p, 1)] = j;
+        }
+    }
+    a.flag[(size_t)p * (a.Nmax + 1) + i] = f;
+}
+
+// the flags (undecided ones from the exact column argmin) -> corres_build's
+// ordered compaction and fallback (one workgroup per pair)
+__global__ __launch_bounds__(1024) void featmut_corres(MutArgs a) {
+    const int p = blockIdx.x;
+    const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
+    const int32_t *a12 = a.nn12 + (size_t)p * a.Nmax;
+    int *f = a.flag + (size_t)p * (a.Nmax + 1);
+    int32_t *co = a.corres + (size_t)p * a.Nmax * 2;
+    if (a.mutual) {
+        for (int i = threadIdx.x; i < n; i += 1024) {
+            const int v = f[i];
+            if (v == 2) f[i] = (a.nn21x[(size_t)p * a.Mmax + a12[i]] == i) ? 1 : 0;
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += 1024) f[i] = 0;
+    }
+    (void)m;
+    __syncthreads();
+    block_exclusive_scan_1024(f, f, n, false);
+    const int total = f[n];
+    const bool use_mutual = a.mutual && total >= 3 * a.ransac_n;
+    if (use_mutual) {
+        for (int i = threadIdx.x; i < n; i += 1024) {
+            const int pos = f[i];
+            if (f[i + 1] != pos) { co[2 * pos] = i; co[2 * pos + 1] = a12[i]; }
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += 1024) { co[2 * i] = i; co[2 * i + 1] = a12[i]; }
+    }
+    if (threadIdx.x == 0) a.n_corres[p] = use_mutual ? total : n;
 }
 
 }  // namespace
 
-static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
-                            const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12,
-                            int32_t *nn21, hipStream_t s) {
-    const int NCH = cdiv(3 * D + 6, 16);
-    constexpr int G5 = 4;
-    const Split5 sp = split5_params(D);
-    constexpr int W = 8;                           // waves (32-row tiles) per workgroup
-    const int nrb = cdiv(cdiv(Nmax, 32), W);
-    const int ntn = nrb * W;                       // row tiles, padded to whole blocks
-    const int ntm = cdiv(cdiv(Mmax, 32), 8) * 8;   // column tiles, padded to whole groups (G | 8)
-    int ctbits = 1;
-    while ((1 << ctbits) < ntm) ++ctbits;
-    PCR_REQUIRE(ctbits <= 16, PCR_ERR_ARG, "feature_match: M=%d too large", Mmax);
+// packed operands, norms and per-pair maxima of both clouds (shared by the
+// dual screen and the mutual path)
+struct V5Buf {
+    int NCH, W, nrb, ntn, ntm, ctbits;
+    Split5 sp;
+    f16x8 *Ap, *Bp;
+    float *fnr, *gnr;
+    unsigned *gmax, *fmax, *mx;
+    int *cnt12, *cnt21, *list12, *list21;
+};
+
+static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                      const int32_t *n_src, const int32_t *n_tgt, hipStream_t s, V5Buf &v) {
+    v.NCH = cdiv(3 * D + 6, 16);
+    v.sp = split5_params(D);
+    v.W = 8;                                          // waves (32-row tiles) per workgroup
+    v.nrb = cdiv(cdiv(Nmax, 32), v.W);
+    v.ntn = v.nrb * v.W;                              // row tiles, padded to whole blocks
+    v.ntm = cdiv(cdiv(Mmax, 32), 8) * 8;              // column tiles, padded to whole groups (G | 8)
+    v.ctbits = 1;
+    while ((1 << v.ctbits) < std::max(v.ntm, v.ntn)) ++v.ctbits;
+    PCR_REQUIRE(v.ctbits <= 16, PCR_ERR_ARG, "feature_match: N=%d / M=%d too large", Nmax, Mmax);
+    const int NCH = v.NCH, ntn = v.ntn, ntm = v.ntm;
     const size_t ap = (size_t)P * ntn * NCH * 64, bp = (size_t)P * ntm * NCH * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
         16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax));
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
-    f16x8 *Ap = (f16x8 *)ws;
-    f16x8 *Bp = Ap + ap;
-    float *fnr = (float *)(Bp + bp);
-    float *gnr = fnr + nn_n;
+    v.Ap = (f16x8 *)ws;
+    v.Bp = v.Ap + ap;
+    v.fnr = (float *)(v.Bp + bp);
+    v.gnr = v.fnr + nn_n;
     // [0,P): max|y|  [P,2P): max|x|  [2P,3P): max|elem|  [3P,4P): cnt12  [4P,5P): cnt21
-    unsigned *gmax = (unsigned *)(gnr + nn_m);
-    unsigned *mx = gmax + 2 * P;
-    int *cnt12 = (int *)(gmax + 3 * P);
-    int *cnt21 = cnt12 + P;
-    int *list12 = cnt21 + P;                  // per pair, stride Nmax
-    int *list21 = list12 + (size_t)P * Nmax;  // per pair, stride Mmax
-    PCR_HIP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned) * 5 * P, s));
+    v.gmax = (unsigned *)(v.gnr + nn_m);
+    v.fmax = v.gmax + P;
+    v.mx = v.gmax + 2 * P;
+    v.cnt12 = (int *)(v.gmax + 3 * P);
+    v.cnt21 = v.cnt12 + P;
+    v.list12 = v.cnt21 + P;                    // per pair, stride Nmax
+    v.list21 = v.list12 + (size_t)P * Nmax;    // per pair, stride Mmax
+    PCR_HIP_CHECK(hipMemsetAsync(v.gmax, 0, sizeof(unsigned) * 5 * P, s));
     prof_begin(s, kProfFeatPack);
-    hipLaunchKernelGGL(feat_maxabs, dim3(P, 2), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax, D,
-                       mx);
+    // ~1024 blocks whatever the batch (each >= 16 KB of a cloud)
+    const long long cloud_f4 = ((long long)std::max(Nmax, Mmax) * D + 3) / 4;
+    const int zsl = (int)std::max(1LL, std::min(std::min(64LL, (cloud_f4 + 1023) / 1024),
+                                                (long long)cdiv(1024, 2 * P)));
+    hipLaunchKernelGGL(feat_maxabs, dim3(P, 2, zsl), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax,
+                       D, v.mx);
     PCR_LAUNCH_CHECK();
     if (D == 32) {  // the hot shape: register-resident pack
         hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax,
-                           ntn, 0, sp, mx, Ap, fnr, gmax + P);
+                           ntn, 0, v.sp, v.mx, v.Ap, v.fnr, v.fmax);
         PCR_LAUNCH_CHECK();
         hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax,
-                           ntm, 1, sp, mx, Bp, gnr, gmax);
+                           ntm, 1, v.sp, v.mx, v.Bp, v.gnr, v.gmax);
         PCR_LAUNCH_CHECK();
     } else {
         hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D,
-                           NCH, ntn, 0, sp, mx, Ap, fnr, gmax + P);
+                           NCH, ntn, 0, v.sp, v.mx, v.Ap, v.fnr, v.fmax);
         PCR_LAUNCH_CHECK();
         hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax, D,
-                           NCH, ntm, 1, sp, mx, Bp, gnr, gmax);
+                           NCH, ntm, 1, v.sp, v.mx, v.Bp, v.gnr, v.gmax);
         PCR_LAUNCH_CHECK();
     }
     prof_end(s, kProfFeatPack);
+    return PCR_OK;
+}
+
+static RescanArgs5 rescan_args(const float *F, const float *G, const int32_t *n_src,
+                               const int32_t *n_tgt, int Nmax, int Mmax, int D) {
+    RescanArgs5 ra;
+    ra.F = F; ra.G = G; ra.n_src = n_src; ra.n_tgt = n_tgt; ra.Nmax = Nmax; ra.Mmax = Mmax;
+    ra.D = D;
+    ra.list12 = ra.list21 = nullptr;
+    ra.cnt12 = ra.cnt21 = nullptr;
+    ra.nn12 = ra.nn21 = nullptr;
+    ra.cap = 256;
+    ra.sd = nullptr;
+    ra.sj = nullptr;
+    ra.v12 = nullptr; ra.e12 = nullptr; ra.mx = nullptr; ra.T = 0;
+    return ra;
+}
+
+// exact f64 rescan of the listed rows of both directions (a direction with a
+// zero count costs its empty blocks only)
+static int run_rescan(RescanArgs5 &ra, int P, int D, hipStream_t s) {
+    const bool v4 = (D % 4) == 0 && ((uintptr_t)ra.F & 15) == 0 && ((uintptr_t)ra.G & 15) == 0;
+    // candidate slices per (pair, direction): ~2048 blocks whatever the batch
+    const int S = std::max(1, std::min(16, 1024 / std::max(P, 1)));
+    if (S > 1) {
+        char *rw = (char *)workspace(6, (sizeof(double) + sizeof(int)) * (size_t)P * 2 * ra.cap * S + 64);
+        PCR_REQUIRE(rw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
+        ra.sd = (double *)rw;
+        ra.sj = (int *)(ra.sd + (size_t)P * 2 * ra.cap * S);
+    }
+    const dim3 rg(P, 2, S);
+    prof_begin(s, kProfFeatRescan);
+    const int dv = cdiv(D, 16) * 16;
+#define PCR_R3(DVV)                                                                    \
+    if (dv == DVV) {                                                                    \
+        if (v4) hipLaunchKernelGGL((featnn_rescan3<DVV, true>), rg, dim3(256), 0, s, ra); \
+        else hipLaunchKernelGGL((featnn_rescan3<DVV, false>), rg, dim3(256), 0, s, ra);  \
+    }
+    PCR_R3(16) PCR_R3(32) PCR_R3(48) PCR_R3(64)
+#undef PCR_R3
+    PCR_LAUNCH_CHECK();
+    if (S > 1) {
+        hipLaunchKernelGGL(featnn_rescan_merge, dim3(P, 2), dim3(256), 0, s, ra, S);
+        PCR_LAUNCH_CHECK();
+    }
+    prof_end(s, kProfFeatRescan);
+    return PCR_OK;
+}
+
+static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                            const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12,
+                            int32_t *nn21, hipStream_t s) {
+    V5Buf v;
+    int rc = v5_prepare(F, G, P, Nmax, Mmax, D, n_src, n_tgt, s, v);
+    if (rc != PCR_OK) return rc;
+    const int NCH = v.NCH, W = v.W, nrb = v.nrb, ntm = v.ntm;
     DualArgs5 d;
-    d.Ap = Ap; d.Bp = Bp; d.fnr = fnr; d.gnr = gnr; d.fmax = gmax + P; d.gmax = gmax;
-    d.n_src = n_src; d.n_tgt = n_tgt; d.P = P; d.Nmax = Nmax; d.Mmax = Mmax; d.ntn = ntn;
-    d.ntm = ntm; d.nrb = nrb; d.D = D; d.ctbits = ctbits; d.nn12 = nn12; d.list12 = list12;
-    d.count12 = cnt12;
+    d.Ap = v.Ap; d.Bp = v.Bp; d.fnr = v.fnr; d.gnr = v.gnr; d.fmax = v.fmax; d.gmax = v.gmax;
+    d.n_src = n_src; d.n_tgt = n_tgt; d.P = P; d.Nmax = Nmax; d.Mmax = Mmax; d.ntn = v.ntn;
+    d.ntm = ntm; d.nrb = nrb; d.D = D; d.nn12 = nn12; d.list12 = v.list12;
+    d.count12 = v.cnt12;
+    // the dual screen's row code: column tiles only
+    d.ctbits = 1;
+    while ((1 << d.ctbits) < ntm) ++d.ctbits;
     const size_t cpn = (size_t)P * nrb * ntm * 32;
     char *cw = (char *)workspace(11, cpn * 8 + 64);
     PCR_REQUIRE(cw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
@@ -849,42 +1243,131 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     }
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfFeatScreen);
-    hipLaunchKernelGGL(featnn_colmerge5, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, list21,
-                       cnt21, 16 * NCH, W);
+    hipLaunchKernelGGL(featnn_colmerge5, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, v.list21,
+                       v.cnt21, 16 * NCH, W);
     PCR_LAUNCH_CHECK();
-    RescanArgs5 ra;
-    ra.F = F; ra.G = G; ra.n_src = n_src; ra.n_tgt = n_tgt; ra.Nmax = Nmax; ra.Mmax = Mmax;
-    ra.D = D; ra.list12 = list12; ra.list21 = list21; ra.cnt12 = cnt12; ra.cnt21 = cnt21;
+    RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
+    ra.list12 = v.list12; ra.list21 = v.list21; ra.cnt12 = v.cnt12; ra.cnt21 = v.cnt21;
     ra.nn12 = nn12; ra.nn21 = nn21;
-    const bool v4 = (D % 4) == 0 && ((uintptr_t)F & 15) == 0 && ((uintptr_t)G & 15) == 0;
-    // candidate slices per (pair, direction): ~2048 blocks whatever the batch
-    const int S = std::max(1, std::min(16, 1024 / std::max(P, 1)));
-    ra.cap = 256;
-    ra.sd = nullptr;
-    ra.sj = nullptr;
-    if (S > 1) {
-        char *rw = (char *)workspace(6, (sizeof(double) + sizeof(int)) * (size_t)P * 2 * ra.cap * S + 64);
-        PCR_REQUIRE(rw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
-        ra.sd = (double *)rw;
-        ra.sj = (int *)(ra.sd + (size_t)P * 2 * ra.cap * S);
+    return run_rescan(ra, P, D, s);
+}
+
+// one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
+template <bool kIdx>
+static int launch_row7(const RowArgs5 &r, int NCH, hipStream_t s) {
+    const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
+    PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_match: grid too large");
+    switch (NCH) {
+#define PCR_R7CASE(K)                                                                            \
+    case K:                                                                                      \
+        hipLaunchKernelGGL((featnn_row7<K, (K <= 7 ? 8 : 4), kIdx>), dim3((unsigned)nblk),         \
+                           dim3(512), 0, s, r);                                                  \
+        break;
+        PCR_R7CASE(1) PCR_R7CASE(2) PCR_R7CASE(3) PCR_R7CASE(4) PCR_R7CASE(5) PCR_R7CASE(6)
+        PCR_R7CASE(7) PCR_R7CASE(8) PCR_R7CASE(9) PCR_R7CASE(10) PCR_R7CASE(11) PCR_R7CASE(12)
+        PCR_R7CASE(13)
+#undef PCR_R7CASE
+        default: set_error("feature dim too large for the f16 split screen"); return PCR_ERR_ARG;
     }
-    const dim3 rg(P, 2, S);
-    prof_begin(s, kProfFeatRescan);
-    const int dv = cdiv(D, 16) * 16;
-#define PCR_R3(DVV)                                                                    \
-    if (dv == DVV) {                                                                    \
-        if (v4) hipLaunchKernelGGL((featnn_rescan3<DVV, true>), rg, dim3(256), 0, s, ra); \
-        else hipLaunchKernelGGL((featnn_rescan3<DVV, false>), rg, dim3(256), 0, s, ra);  \
-    }
-    PCR_R3(16) PCR_R3(32) PCR_R3(48) PCR_R3(64)
-#undef PCR_R3
     PCR_LAUNCH_CHECK();
-    if (S > 1) {
-        hipLaunchKernelGGL(featnn_rescan_merge, dim3(P, 2), dim3(256), 0, s, ra, S);
-        PCR_LAUNCH_CHECK();
-    }
-    prof_end(s, kProfFeatRescan);
     return PCR_OK;
+}
+
+// the mutual path (see featnn_row7): nn12 and the correspondences without the
+// column screen of every target
+static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                             const int32_t *n_src, const int32_t *n_tgt, int mutual, int ransac_n,
+                             int32_t *nn12, int32_t *corres, int32_t *n_corres, hipStream_t s) {
+    V5Buf v;
+    int rc = v5_prepare(F, G, P, Nmax, Mmax, D, n_src, n_tgt, s, v);
+    if (rc != PCR_OK) return rc;
+    const int NCH = v.NCH, ntn = v.ntn, ntm = v.ntm;
+    // scratch: v12 [P][Nmax] f64 | e12 [P][Nmax] f32 | w1, w2 [P][Mmax] f32 | used, pos
+    // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P]
+    const size_t pn = (size_t)P * Nmax, pm = (size_t)P * Mmax;
+    const size_t bytes = 8 * pn + 4 * pn + 8 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P;
+    char *ws = (char *)workspace(33, bytes + 256);
+    PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
+    MutArgs ma;
+    double *v12 = (double *)ws;
+    float *e12 = (float *)(v12 + pn);
+    float *w1 = e12 + pn, *w2 = w1 + pm;
+    ma.used = (int *)(w2 + pm);
+    ma.pos = ma.used + pm + P;
+    ma.jlist = ma.pos + pm + P;
+    int *nn21x = ma.jlist + pm;
+    ma.flag = nn21x + pm;
+    ma.nj = ma.flag + pn + P;
+    int *zero = ma.nj + P;
+    PCR_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(int) * (size_t)P, s));
+    ma.nn12 = nn12; ma.n_src = n_src; ma.n_tgt = n_tgt; ma.Nmax = Nmax; ma.Mmax = Mmax;
+    ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * NCH; ma.D = D; ma.ntm = ntm;
+    ma.v12 = v12; ma.e12 = e12; ma.w1 = w1; ma.w2 = w2; ma.gnr = v.gnr; ma.fmax = v.fmax;
+    ma.list21 = v.list21; ma.cnt21 = v.cnt21; ma.nn21x = nn21x;
+    ma.corres = corres; ma.n_corres = n_corres;
+    // pass 1: F rows x all G columns
+    RowArgs5 r;
+    r.Ap = v.Ap; r.Bp = v.Bp; r.rnr = v.fnr; r.cmax = v.gmax; r.n_rows = n_src; r.n_cols = n_tgt;
+    r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
+    r.ntc = ntm; r.nrb = v.nrb; r.D = D; r.ctbits = 1;
+    while ((1 << r.ctbits) < ntm) ++r.ctbits;
+    r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
+    r.w1 = nullptr; r.w2 = nullptr;
+    prof_begin(s, kProfFeatScreen);
+    rc = launch_row7<true>(r, NCH, s);
+    if (rc != PCR_OK) return rc;
+    prof_end(s, kProfFeatScreen);
+    RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
+    ra.list12 = v.list12; ra.list21 = v.list21; ra.cnt12 = v.cnt12; ra.cnt21 = zero;
+    ra.nn12 = nn12; ra.nn21 = nn21x;
+    ra.v12 = v12; ra.e12 = e12; ra.mx = v.mx; ra.T = v.sp.T;
+    rc = run_rescan(ra, P, D, s);
+    if (rc != PCR_OK) return rc;
+    if (mutual) {
+        hipLaunchKernelGGL(featmut_jbuild, dim3(P), dim3(1024), 0, s, ma);
+        PCR_LAUNCH_CHECK();
+        // pass 2: the rows J of G (B-role fragments as the register operand) x all F
+        // columns (A-role fragments streamed): the same products, values only
+        RowArgs5 r2 = r;
+        r2.Ap = v.Bp; r2.Bp = v.Ap; r2.rnr = v.gnr; r2.cmax = v.fmax; r2.n_rows = n_tgt;
+        r2.n_cols = n_src; r2.rlist = ma.jlist; r2.rcount = ma.nj; r2.Rmax = Mmax; r2.Cmax = Nmax;
+        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W);
+        r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
+        r2.w1 = w1; r2.w2 = w2;
+        prof_begin(s, kProfFeatScreen2);
+        rc = launch_row7<false>(r2, NCH, s);
+        if (rc != PCR_OK) return rc;
+        prof_end(s, kProfFeatScreen2);
+        hipLaunchKernelGGL(featmut_resolve, dim3(cdiv(Nmax, 256), P), dim3(256), 0, s, ma);
+        PCR_LAUNCH_CHECK();
+        RescanArgs5 rb = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
+        rb.list12 = v.list12; rb.list21 = v.list21; rb.cnt12 = zero; rb.cnt21 = v.cnt21;
+        rb.nn12 = nn12; rb.nn21 = nn21x;
+        rc = run_rescan(rb, P, D, s);
+        if (rc != PCR_OK) return rc;
+    }
+    hipLaunchKernelGGL(featmut_corres, dim3(P), dim3(1024), 0, s, ma);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+int corres_impl(const int32_t *nn12, const int32_t *nn21, const int32_t *n_src,
+                const int32_t *n_tgt, int P, int Nmax, int Mmax, int mutual, int ransac_n,
+                int32_t *corres, int32_t *n_corres, hipStream_t s);
+
+int feature_corres_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                        const int32_t *n_src, const int32_t *n_tgt, int mutual, int ransac_n,
+                        int32_t *nn12, int32_t *corres, int32_t *n_corres, hipStream_t s) {
+    PCR_REQUIRE(D >= 1 && D <= 128, PCR_ERR_ARG, "feature_corres: D=%d unsupported (1..128)", D);
+    if (D <= 64)
+        return feature_corres_v5(F, G, P, Nmax, Mmax, D, n_src, n_tgt, mutual, ransac_n, nn12, corres,
+                                 n_corres, s);
+    // 64 < D <= 128: both directions from the f32 screen, then the filter
+    int32_t *nn21 = (int32_t *)workspace(34, sizeof(int32_t) * (size_t)P * Mmax + 64);
+    PCR_REQUIRE(nn21, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
+    int rc = feature_match_f32(F, G, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
+    if (rc != PCR_OK) return rc;
+    return corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, Mmax, mutual, ransac_n, corres, n_corres, s);
 }
 
 int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
@@ -919,6 +1402,39 @@ extern "C" int pcr_feature_match(const float *src_feat, const float *tgt_feat, i
     PCR_REQUIRE(P <= 65535, PCR_ERR_ARG, "feature_match: P=%d > 65535", P);
     return pcr::feature_match_impl(src_feat, tgt_feat, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21,
                                    pcr::as_stream(stream));
+}
+
+extern "C" int pcr_feature_correspondences(const float *src_feat, const float *tgt_feat, int32_t P,
+                                           int32_t Nmax, int32_t Mmax, int32_t D, const int32_t *n_src,
+                                           const int32_t *n_tgt, int32_t mutual_filter, int32_t ransac_n,
+                                           int32_t *nn12, int32_t *corres, int32_t *n_corres,
+                                           pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(P >= 0 && Nmax >= 0 && Mmax >= 0, PCR_ERR_ARG, "feature_corres: negative size");
+    if (P == 0 || Nmax == 0) return PCR_OK;
+    PCR_REQUIRE(src_feat && tgt_feat && nn12 && corres && n_corres, PCR_ERR_ARG,
+                "feature_corres: null pointer");
+    PCR_REQUIRE(P <= 65535, PCR_ERR_ARG, "feature_corres: P=%d > 65535", P);
+    hipStream_t s = pcr::as_stream(stream);
+    if (Mmax == 0) {  // no target: nn12 = 0 (the reference loop never runs), no mutual pair
+        PCR_HIP_CHECK(hipMemsetAsync(nn12, 0, sizeof(int32_t) * (size_t)P * Nmax, s));
+        int32_t *nn21 = (int32_t *)pcr::workspace(34, 64);
+        PCR_REQUIRE(nn21, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
+        return pcr::corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, 0, mutual_filter, ransac_n, corres,
+                                n_corres, s);
+    }
+    return pcr::feature_corres_impl(src_feat, tgt_feat, P, Nmax, Mmax, D, n_src, n_tgt, mutual_filter,
+                                    ransac_n, nn12, corres, n_corres, s);
+}
+
+// debug: copy the mutual path's scratch (v12 | e12 | w1 | w2 | used | pos | jlist |
+// nn21x | flag | nj, feature_corres_v5's layout) of the last call to dst
+extern "C" int pcr_featmut_debug_copy(void *dst, int64_t bytes, pcr_stream_t stream) {
+    pcr::clear_error();
+    void *src = pcr::workspace(33, 16);
+    PCR_REQUIRE(src && dst && bytes >= 0, PCR_ERR_ARG, "featmut_debug_copy: bad arguments");
+    PCR_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, pcr::as_stream(stream)));
+    return PCR_OK;
 }
 
 extern "C" int pcr_correspondences(const int32_t *nn12, const int32_t *nn21, int32_t P,

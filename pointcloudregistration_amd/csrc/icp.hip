@@ -12,16 +12,18 @@
 //    are stored by source index; the sweep takes 64-query chunks of the spatial
 //    (Morton-of-cell) order from a counter.
 //  * Per iteration: every point is queried in the grid (radius-limited 1-NN),
-//    then the Umeyama means and cross-covariance are summed in 1024 fixed lanes
-//    (lane l: indices l, l + 1024, ... in f64, in order) whose partials are added
-//    EXACTLY (xsum.h) -- so the result is the same whatever the number of
-//    workgroups a pair's lanes are spread over; Horn's quaternion solve and the
-//    T <- U*T update run redundantly in every workgroup on the same totals.
+//    then ONE pass sums the Umeyama terms of the inliers -- s - c0, t - c0 and
+//    their 9 products, each truncated to a multiple of a per-pair quantum 2^-k
+//    small enough that every partial sum is an integer multiple of 2^-k below
+//    2^52 (oracle_icp_quantum): the f64 additions are then exact, so any split
+//    over threads, waves and workgroups gives the same bits, and the means and
+//    the cross-covariance (C = Sst - ms' St^T) come out of one pass and one
+//    reduction; Horn's quaternion solve and the T <- U*T update run
+//    redundantly in every workgroup on the same totals.
 #include "pcr_internal.h"
 #include "coop.h"
 #include "geom.h"
 #include "grid.h"
-#include "xsum.h"
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -31,11 +33,11 @@ namespace {
 
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
-constexpr int kLanes = 1024;  // Umeyama sum lanes (oracle ICP_LANES): independent of G
+constexpr int kQ = 15;  // exact sums: s' (3), t' (3), s'_a t'_b (9)
 
 // one workgroup's partial of a reduction (G > 1): HBM slot per (pair, parity, g)
 struct XPart {
-    xs_t s[9];
+    double s[kQ];
     unsigned long long acc;
     int cnt, pad;
 };
@@ -66,10 +68,15 @@ __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
 }
 
 struct IShared {  // LDS header; the grid copy (if any) follows
-    xs_t ws[kWaves][9];
+    double ws[kWaves][kQ];
     unsigned long long wacc[kWaves];
     int wcnt[kWaves];
-    xs_t tot[9];
+    double tot[kQ];
+    double C[9];      // cross-covariance of the current correspondences
+    double c0[3];     // the pair's reference point (first target point)
+    double ms[3], mt[3];  // Umeyama means of the current correspondences
+    double sk, isk;   // 2^k, 2^-k: the quantum of the exact sums
+    double bt[kWaves];
     unsigned long long acc;
     int cnt;
     double T[16];     // the running transformation (init, then U * T per iteration)
@@ -78,28 +85,17 @@ struct IShared {  // LDS header; the grid copy (if any) follows
     int chunk;        // next 64-position chunk of the current sweep (G = 1)
 };
 
-// wave-level sum of NQ fixed-point values; lane 0 parks them in sh.ws[wave][q0..]
+// wave-level sums of NQ exact f64 values (integer multiples of the quantum:
+// the additions are exact, so the tree shape is free); lane 0 parks them in
+// sh.ws[wave][0..NQ)
 template <int NQ>
-__device__ __forceinline__ void wave_park(IShared &sh, const xs_t *v, int q0) {
+__device__ __forceinline__ void wave_park(IShared &sh, double *v) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const xs_t x = xs_wave_sum(v[q]);
-        if (lane == 0) sh.ws[wid][q0 + q] = x;
-    }
-}
-
-// the same for f64 lane partials, converted one at a time (few live registers)
-template <int NQ>
-__device__ __forceinline__ void wave_park_f64(IShared &sh, const double *v, int q0) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll 1
-    for (int q = 0; q < NQ; ++q) {
-        double d = v[0];
 #pragma unroll
-        for (int t = 1; t < NQ; ++t) d = (q == t) ? v[t] : d;
-        const xs_t x = xs_wave_sum(xs_term(d));
-        if (lane == 0) sh.ws[wid][q0 + q] = x;
+        for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+        if (lane == 0) sh.ws[wid][q] = v[q];
     }
 }
 
@@ -120,7 +116,7 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int cnt,
     }
     __syncthreads();
     if (tid < NV + 2) {  // thread q sums quantity q (NV: count, NV+1: error sum)
-        xs_t s = 0;
+        double s = 0.0;
         unsigned long long A = 0;
         int C = 0;
         for (int w = 0; w < kWaves; ++w) {
@@ -143,7 +139,7 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int cnt,
         pair_barrier(a.bar + 2 * (size_t)p, a.G);
         if (tid < NV + 2) {
             const XPart *all = a.part + ((size_t)p * 2 + (sh.nred & 1)) * a.G;
-            xs_t s = 0;
+            double s = 0.0;
             unsigned long long A = 0;
             int C = 0;
             for (int h = 0; h < a.G; ++h) {
@@ -182,12 +178,32 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     bool ident = true;
     for (int k = 0; k < 16; ++k) ident = ident && (sh.T[k] == ((k % 5 == 0) ? 1.0 : 0.0));
     const int stride = G * kThreads, base = g * kThreads + tid;
-    // Umeyama lanes (lane l: source indices l, l + 1024, ... summed in order in
-    // f64): workgroup g owns lanes [g*LG, min((g+1)*LG, kLanes)), one per
-    // thread; LG rounds up so every lane has an owner for any G (G = 3: 342,
-    // 342, 340).  The lane sums are exact, so ownership never changes a bit.
-    const int LG = (kLanes + G - 1) / G;
-    const int my_lane = (tid < LG && g * LG + tid < kLanes) ? g * LG + tid : -1;
+    // the pair's reference point and quantum of the exact Umeyama sums
+    // (oracle_icp_quantum): c0 = the first target point, 2^k from the largest
+    // |t - c0| (every workgroup computes the same values)
+    if (valid) {
+        const float *Tg = a.tgt + (size_t)p * a.Mmax * 3;
+        const double c0x = (double)Tg[0], c0y = (double)Tg[1], c0z = (double)Tg[2];
+        double bt = 0.0;
+        for (int j = tid; j < m; j += kThreads)
+            bt = fmax(bt, fmax(fabs((double)Tg[3 * j] - c0x),
+                               fmax(fabs((double)Tg[3 * j + 1] - c0y), fabs((double)Tg[3 * j + 2] - c0z))));
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) bt = fmax(bt, __shfl_xor(bt, o, 64));
+        if (lane == 0) sh.bt[tid >> 6] = bt;
+        if (tid == 0) { sh.c0[0] = c0x; sh.c0[1] = c0y; sh.c0[2] = c0z; }
+        __syncthreads();
+        bt = sh.bt[0];
+        for (int w = 1; w < kWaves; ++w) bt = fmax(bt, sh.bt[w]);
+        const double B = bt + 2.0 * a.d;
+        int eb = 0;
+        (void)frexp(B, &eb);
+        const int emax = eb > 2 * eb ? eb : 2 * eb;
+        int en = 0;
+        while ((1LL << en) < (long long)(n > 1 ? n : 1)) ++en;
+        const int k = min(200, max(-200, 52 - en - emax));
+        if (tid == 0) { sh.sk = ldexp(1.0, k); sh.isk = ldexp(1.0, -k); }
+    }
     if (valid) {  // working copy = init applied to the f32 input (Open3D's Transform)
         double T0[12];
         for (int q = 0; q < 12; ++q) T0[q] = sh.T[q];
@@ -230,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);
         else __syncthreads();
     };
-    double fit = 0.0, rmse = 0.0, ms[3] = {0, 0, 0}, mt[3] = {0, 0, 0};
+    double fit = 0.0, rmse = 0.0;
     int count = 0;
     // correspondences of the current points, their count / error sum and the
     // Umeyama means
@@ -289,27 +305,45 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             else sh.chunk = 0;
         }
         mark(0);
-        {  // means: each lane's source / target coordinate sums in index order
-            double v[6] = {0, 0, 0, 0, 0, 0};
-            if (my_lane >= 0)
-                for (int i = my_lane; i < n; i += kLanes) {
-                    const float4 t = TQ[i];
-                    if (__float_as_int(t.w) < 0) continue;
-                    v[0] = v[0] + P3[3 * i]; v[1] = v[1] + P3[3 * i + 1]; v[2] = v[2] + P3[3 * i + 2];
-                    v[3] = v[3] + (double)t.x; v[4] = v[4] + (double)t.y; v[5] = v[5] + (double)t.z;
+        {  // the exact Umeyama sums of the inliers, any point to any thread
+            double v[kQ];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) v[q] = 0.0;
+            const double c0x = sh.c0[0], c0y = sh.c0[1], c0z = sh.c0[2];
+            const double sk = sh.sk, isk = sh.isk;
+#pragma unroll 1
+            for (int i = base; i < n; i += stride) {
+                const float4 t = TQ[i];
+                if (__float_as_int(t.w) < 0) continue;
+                const double sp[3] = {P3[3 * i] - c0x, P3[3 * i + 1] - c0y, P3[3 * i + 2] - c0z};
+                const double tp[3] = {(double)t.x - c0x, (double)t.y - c0y, (double)t.z - c0z};
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    v[c] = v[c] + __builtin_trunc(sp[c] * sk) * isk;
+                    v[3 + c] = v[3 + c] + __builtin_trunc(tp[c] * sk) * isk;
+#pragma unroll
+                    for (int e = 0; e < 3; ++e)
+                        v[6 + 3 * c + e] = v[6 + 3 * c + e] + __builtin_trunc((sp[c] * tp[e]) * sk) * isk;
                 }
-            wave_park_f64<6>(sh, v, 0);
+            }
+            wave_park<kQ>(sh, v);
         }
-        pair_reduce<6>(a, sh, p, g, cnt, acc);
+        pair_reduce<kQ>(a, sh, p, g, cnt, acc);
         mark(1);
         count = sh.cnt;
         if (count > 0) {
             fit = (double)count / (double)n;
             rmse = __builtin_sqrt(((double)sh.acc / scale) / (double)count);
             const double inv = 1.0 / (double)count;
-            for (int c = 0; c < 3; ++c) {
-                ms[c] = xs_to_double(sh.tot[c]) * inv;
-                mt[c] = xs_to_double(sh.tot[3 + c]) * inv;
+            if (tid == 0) {
+                double msp[3];
+                for (int c = 0; c < 3; ++c) {
+                    msp[c] = sh.tot[c] * inv;
+                    sh.ms[c] = msp[c] + sh.c0[c];
+                    sh.mt[c] = sh.tot[3 + c] * inv + sh.c0[c];
+                }
+                for (int c = 0; c < 3; ++c)
+                    for (int e = 0; e < 3; ++e) sh.C[3 * c + e] = sh.tot[6 + 3 * c + e] - msp[c] * sh.tot[3 + e];
             }
         } else {
             fit = 0.0;
@@ -322,26 +356,13 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         evaluate(false);
         for (it = 0; it < a.max_iter;) {
             if (count == 0) break;
-            {  // --- cross covariance of the centred correspondences, per lane in order
-                double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-                if (my_lane >= 0)
-                    for (int i = my_lane; i < n; i += kLanes) {
-                        const float4 t = TQ[i];
-                        if (__float_as_int(t.w) < 0) continue;
-                        const double s0 = P3[3 * i] - ms[0], s1 = P3[3 * i + 1] - ms[1], s2 = P3[3 * i + 2] - ms[2];
-                        const double t0 = (double)t.x - mt[0], t1 = (double)t.y - mt[1], t2 = (double)t.z - mt[2];
-                        v[0] = v[0] + s0 * t0; v[1] = v[1] + s0 * t1; v[2] = v[2] + s0 * t2;
-                        v[3] = v[3] + s1 * t0; v[4] = v[4] + s1 * t1; v[5] = v[5] + s1 * t2;
-                        v[6] = v[6] + s2 * t0; v[7] = v[7] + s2 * t1; v[8] = v[8] + s2 * t2;
-                    }
-                wave_park_f64<9>(sh, v, 0);
-            }
-            pair_reduce<9>(a, sh, p, g, 0, 0ull);
             mark(2);
             if (tid == 0) {
                 double Sm[9], R[9], U[12];
-                for (int k = 0; k < 9; ++k) Sm[k] = xs_to_double(sh.tot[k]);
+                for (int k = 0; k < 9; ++k) Sm[k] = sh.C[k];
                 horn_rotation(Sm, R);
+                double ms[3], mt[3];
+                for (int c = 0; c < 3; ++c) { ms[c] = sh.ms[c]; mt[c] = sh.mt[c]; }
                 compose_rt(R, ms, mt, U);
                 double Tn[16];
                 for (int r = 0; r < 4; ++r)

@@ -22,7 +22,7 @@ inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream
 // per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)
 enum ProfId { kProfFeatScreen = 0, kProfNndFwd = 1, kProfRansacValidate = 2, kProfIcp = 3,
               kProfRansacHyp = 4, kProfFeatRescan = 5, kProfFeatPack = 6, kProfNndGrid = 7,
-              kProfSlots = 8 };
+              kProfFeatScreen2 = 8, kProfSlots = 9 };
 void prof_begin(hipStream_t s, int id);
 void prof_end(hipStream_t s, int id);
 

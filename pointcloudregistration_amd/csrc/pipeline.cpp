@@ -5,6 +5,9 @@ namespace pcr {
 int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
                        const int32_t *n_src, const int32_t *n_tgt, int32_t *nn12, int32_t *nn21,
                        hipStream_t s);
+int feature_corres_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
+                        const int32_t *n_src, const int32_t *n_tgt, int mutual, int ransac_n,
+                        int32_t *nn12, int32_t *corres, int32_t *n_corres, hipStream_t s);
 int corres_impl(const int32_t *nn12, const int32_t *nn21, const int32_t *n_src,
                 const int32_t *n_tgt, int P, int Nmax, int Mmax, int mutual, int ransac_n,
                 int32_t *corres, int32_t *n_corres, hipStream_t s);
@@ -37,10 +40,16 @@ extern "C" int pcr_register_feature_ransac(const float *src_xyz, const float *tg
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "register: %s", pcr_last_error());
     int32_t *nn12 = ws, *nn21 = nn12 + (size_t)P * Nmax, *corres = nn21 + (size_t)P * Mmax;
     int32_t *n_corres = corres + (size_t)P * Nmax * 2;
-    int rc = pcr::feature_match_impl(src_feat, tgt_feat, P, Nmax, Mmax, D, n_src, n_tgt, nn12, nn21, s);
-    if (rc != PCR_OK) return rc;
-    rc = pcr::corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, Mmax, params->mutual_filter,
-                          params->ransac_n, corres, n_corres, s);
+    (void)nn21;
+    int rc = PCR_OK;
+    if (Mmax > 0 && Nmax > 0) {
+        rc = pcr::feature_corres_impl(src_feat, tgt_feat, P, Nmax, Mmax, D, n_src, n_tgt,
+                                      params->mutual_filter, params->ransac_n, nn12, corres, n_corres, s);
+    } else {
+        if (Nmax > 0) PCR_HIP_CHECK(hipMemsetAsync(nn12, 0, sizeof(int32_t) * (size_t)P * Nmax, s));
+        rc = pcr::corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, Mmax, params->mutual_filter,
+                              params->ransac_n, corres, n_corres, s);
+    }
     if (rc != PCR_OK) return rc;
     return pcr::ransac_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, corres, n_corres, Nmax,
                             pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask, s);

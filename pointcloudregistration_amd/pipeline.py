@@ -69,11 +69,12 @@ class PairPipeline:
         if time_stages:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
             ev[0].record()
-        nn12, nn21 = reg.feature_match(self.src_feat, self.tgt_feat)
+        # feature NN + mutual filter (nn21 only where the filter reads it)
+        corres, ncor, _ = reg.feature_correspondences(
+            self.src_feat, self.tgt_feat, mutual_filter=self.params.ransac.mutual_filter,
+            ransac_n=self.params.ransac.ransac_n)
         if ev:
             ev[1].record()
-        corres, ncor = reg.correspondences(nn12, nn21, mutual_filter=self.params.ransac.mutual_filter,
-                                           ransac_n=self.params.ransac.ransac_n)
         rr = reg.ransac_batch(self.src, self.tgt, corres, ncor, self.params.ransac,
                               pair_ids=self.pair_ids, want_corr=False, want_mask=True)
         if ev:
@@ -91,6 +92,7 @@ class PairPipeline:
             ev[5].record()
             self.stage_events = ev
         self.last = (rr, ir, chamfer, ncor)
+        self.corres = corres
         return rr, ir, chamfer
 
     def stage_ms(self):

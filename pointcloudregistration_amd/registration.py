@@ -162,6 +162,32 @@ def correspondences(nn12, nn21, n_src=None, n_tgt=None, mutual_filter=True, rans
     return corres, ncor
 
 
+def feature_correspondences(src_feat, tgt_feat, n_src=None, n_tgt=None, mutual_filter=True,
+                            ransac_n=3):
+    """feature_match + correspondences in one call, without nn21 for every target
+    (pcr_feature_correspondences): -> (corres (P,N,2), n_corres (P,), nn12 (P,N)),
+    bit-identical to correspondences(*feature_match(...))."""
+    F = _cuda(src_feat, torch.float32)
+    if F.dim() == 2:
+        F = F.unsqueeze(0)
+    G = _cuda(tgt_feat, torch.float32, F.device)
+    if G.dim() == 2:
+        G = G.unsqueeze(0)
+    P, N, D = F.shape
+    M = G.shape[1]
+    if G.shape[0] != P or G.shape[2] != D:
+        raise ValueError("src_feat (P,N,D) and tgt_feat (P,M,D) must agree on P and D")
+    nn12 = torch.empty(P, N, dtype=torch.int32, device=F.device)
+    corres = torch.empty(P, N, 2, dtype=torch.int32, device=F.device)
+    ncor = torch.empty(P, dtype=torch.int32, device=F.device)
+    ns, nt = _counts(n_src, P, F.device), _counts(n_tgt, P, F.device)
+    with torch.cuda.device(F.device):
+        _lib.call("pcr_feature_correspondences", _lib.ptr(F), _lib.ptr(G), P, N, M, D, _lib.ptr(ns),
+                  _lib.ptr(nt), int(bool(mutual_filter)), int(ransac_n), _lib.ptr(nn12),
+                  _lib.ptr(corres), _lib.ptr(ncor), _stream(F.device))
+    return corres, ncor, nn12
+
+
 def _ransac_outputs(P, N, dev, want_corr=True, want_mask=True):
     T = torch.empty(P, 4, 4, dtype=torch.float64, device=dev)
     fr = torch.empty(P, 2, dtype=torch.float64, device=dev)

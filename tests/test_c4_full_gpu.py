@@ -32,6 +32,7 @@ def c4():
                         pair_ids=np.arange(P, dtype=np.int32))
     pipe.run()
     rec = pipe.records().cpu().numpy()
+    pipe_corres, pipe_ncor = pipe.corres.cpu().numpy(), pipe.last[3].cpu().numpy()
     # the same stages called one by one, keeping every intermediate
     nn12, nn21 = reg.feature_match(pipe.src_feat, pipe.tgt_feat)
     corres, ncor = reg.correspondences(nn12, nn21)
@@ -39,7 +40,8 @@ def c4():
                           pair_ids=pipe.pair_ids, want_corr=True, want_mask=True)
     ir = reg.icp_batch(pipe.src, pipe.tgt, rr.transformation, params.icp, want_corr=True)
     torch.cuda.synchronize()
-    out = dict(batch=batch, params=params, rec=rec, nn12=nn12.cpu().numpy(),
+    out = dict(batch=batch, params=params, rec=rec, pipe_corres=pipe_corres, pipe_ncor=pipe_ncor,
+               nn12=nn12.cpu().numpy(),
                nn21=nn21.cpu().numpy(), corres=corres.cpu().numpy(), ncor=ncor.cpu().numpy(),
                T_r=rr.transformation.cpu().numpy(), fit_r=rr.fitness.cpu().numpy(),
                rmse_r=rr.inlier_rmse.cpu().numpy(), st_r=rr.stats.cpu().numpy(),
@@ -52,6 +54,16 @@ def c4():
 def _bits(a, b):
     a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
     return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def test_mutual_path_equals_both_directions(c4):
+    """The pipeline's one-call mutual path (pcr_feature_correspondences: nn21
+    only where the filter reads it, decided from certified screen values) gives
+    every pair the correspondence set of the full nn12 / nn21 + filter."""
+    assert np.array_equal(c4["pipe_ncor"], c4["ncor"])
+    for p in range(P):
+        k = int(c4["ncor"][p])
+        assert np.array_equal(c4["pipe_corres"][p, :k], c4["corres"][p, :k]), p
 
 
 def test_records_equal_stage_outputs(c4):

@@ -1,0 +1,39 @@
+"""Debug the mutual path: dump its scratch after one call and compare with exact
+distances (oracle).  Run on the GPU box."""
+import sys, os
+import numpy as np
+import torch
+sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), "oracle"))
+import oracle as O
+from pointcloudregistration_amd import registration as reg, synth, _lib
+
+B = synth.make_batch(1, n=4096, m=4096, d=32, base_seed=77, feat_noise=1.0)
+fs, ft = B.src_feat[0], B.tgt_feat[0]
+N = M = 4096
+co, nc, nn12 = reg.feature_correspondences(fs[None], ft[None])
+pn, pm, P = N, M, 1
+nbytes = 8 * pn + 4 * pn + 8 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * P
+buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+_lib.call("pcr_featmut_debug_copy", _lib.ptr(buf), nbytes, _lib.stream_handle())
+h = buf.cpu().numpy()
+o = 0
+def take(dt, cnt):
+    global o
+    a = h[o:o + np.dtype(dt).itemsize * cnt].view(dt); o += np.dtype(dt).itemsize * cnt; return a
+v12 = take(np.float64, pn); e12 = take(np.float32, pn); w1 = take(np.float32, pm); w2 = take(np.float32, pm)
+used = take(np.int32, pm + P); pos = take(np.int32, pm + P); jl = take(np.int32, pm); nn21x = take(np.int32, pm)
+flag = take(np.int32, pn + P); nj = take(np.int32, P)
+e12o = O.featnn(fs, ft); e21o = O.featnn(ft, fs)
+mut = e21o[e12o] == np.arange(N)
+print("nj", nj, "unique nn12", len(np.unique(e12o)), "oracle mutual", mut.sum(), "gpu", int(nc[0]))
+print("flag counts", np.bincount(flag[:N], minlength=3))
+mx = float(np.abs(np.concatenate([fs, ft])).max())
+E = int(np.frexp(mx)[1]); s = 2.0 ** (12 - E)
+bad = np.nonzero(mut & (flag[:N] == 0))[0]
+print("mutual rejected:", len(bad))
+for i in bad[:10]:
+    j = e12o[i]
+    D = ((fs[i].astype(np.float64) - ft[j]) ** 2).sum() * s * s
+    dcol = ((fs.astype(np.float64) - ft[j]) ** 2).sum(1) * s * s
+    srt = np.sort(dcol)
+    print(i, j, "v12 %.6g e12 %.3g w1 %.6g w2 %.6g exactD %.6g col top2 %.6g %.6g used %d" % (v12[i], e12[i], w1[j], w2[j], D, srt[0], srt[1], used[j]))
