@@ -374,9 +374,23 @@ def measure_ndp_opt(with_cpu):
     ndp_opt.optimize_deformation_pyramid(S, G, inds, cfg, NDP=fresh())  # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ndp_opt.optimize_deformation_pyramid(S, G, inds, cfg, NDP=fresh())
+    _, _, _, info = ndp_opt.optimize_deformation_pyramid(S, G, inds, cfg, NDP=fresh())
     torch.cuda.synchronize()
     graph_ms = (time.perf_counter() - t0) * 1e3
+    replay_ms = float(sum(i.get("replay_ms", 0.0) for i in info))
+    evaluated = int(sum(i["evaluated"] for i in info))
+    # f4 roofline: per iteration the level's forward, data backward and weight
+    # gradients over all n points, each 2 * (6W + 2W^2 + 7W) = 68,864 flops per
+    # point at W = 128, on the f32 MFMA (157.3 TF)
+    flop_it = 3 * 2 * (6 * 128 + 2 * 128 * 128 + 7 * 128) * n
+    f4_roof = {"bound": "mfma", "unit": "TFLOP/s", "peak": 157.3,
+               "flop_per_iteration": flop_it, "iterations": evaluated,
+               "achieved": flop_it * evaluated / (replay_ms * 1e-3) / 1e12 if replay_ms > 0 else None,
+               "replay_ms": replay_ms,
+               "note": "algorithmic flops of the MLP forward + data backward + weight gradients "
+                       "(the Chamfer and Adam are extra) / the summed graph replay time of the levels"}
+    if f4_roof["achieved"] is not None:
+        f4_roof["frac"] = f4_roof["achieved"] / f4_roof["peak"]
 
     def reference_style(P):
         s = S - S.mean(0, keepdim=True)
@@ -411,7 +425,7 @@ def measure_ndp_opt(with_cpu):
     eager_ms = (time.perf_counter() - t0) * 1e3
     res = {"workload": "C5 NDP optimisation: 20000-pt pair, 5000 Chamfer indices, 9 levels x 40 "
                        "iterations (width 128, depth 3), wall clock",
-           "graph_ms": graph_ms, "reference_loop_on_gpu_ms": eager_ms,
+           "graph_ms": graph_ms, "reference_loop_on_gpu_ms": eager_ms, "roofline": f4_roof,
            "iterations_per_s": 9 * 40 / (graph_ms * 1e-3), "speedup_vs_reference_loop": eager_ms / graph_ms}
     if with_cpu:
         P = ndp_opt.DeformationPyramid(3, 128, "cpu", -8, 9, True)
@@ -439,13 +453,14 @@ def measure_ndp_opt(with_cpu):
 
 
 def measure_c5(with_cpu):
-    """C5 end to end (c2p-net/testScript.py:161-196) on one 20k-point pair:
-    vote over three 32-d feature levels -> mutual feature RANSAC at d = 0.025 ->
-    estimate -> NDP 9 levels x 40 iterations (width 128, early stop disabled so
-    every run does the same work) on the unique inlier sources; wall clock per
-    stage, inputs resident on the device."""
+    """C5 end to end (c2p-net/testScript.py:161-196) on one 20k-point pair (the
+    target non-rigidly deformed, synth.make_c5_pair -- the pair of
+    tests/golden/c5_golden.npz): vote over three 32-d feature levels -> mutual
+    feature RANSAC at d = 0.025 -> estimate -> NDP 9 levels x <= 40 iterations
+    (width 128, config/NDP.yaml's early stop, which now stops the work) on the
+    unique inlier sources; wall clock per stage, inputs resident on the device."""
     from pointcloudregistration_amd import c2p, ndp_opt, registration as reg, synth
-    B = synth.make_batch(1, n=20000, m=20000, d=32, base_seed=515)
+    B = synth.make_c5_pair(515, n=20000, m=20000, d=32)
     rng = np.random.default_rng(5)
 
     def lv(f):
@@ -455,7 +470,7 @@ def measure_c5(with_cpu):
     S, G = torch.from_numpy(B.src[0]).to(dev), torch.from_numpy(B.tgt[0]).to(dev)
     FS = [torch.from_numpy(f).to(dev) for f in fs]
     FT = [torch.from_numpy(f).to(dev) for f in ft]
-    cfg = ndp_opt.NDPConfig(max_break_count=10**6)
+    cfg = ndp_opt.NDPConfig()  # config/NDP.yaml
     voxel = 0.025
 
     def run():
@@ -475,16 +490,16 @@ def measure_c5(with_cpu):
         w, _, _, info = ndp_opt.optimize_deformation_pyramid(est, G, corrs, cfg, NDP=P)
         torch.cuda.synchronize()
         t.append(time.perf_counter())
-        return np.diff(t) * 1e3, br, len(corrs)
+        return np.diff(t) * 1e3, br, len(corrs), info
     run()
-    ms, br, k = run()
+    ms, br, k, info = run()
     T = br.transformation[0].cpu().numpy()
     rre, rte = synth.rre_rte(T[:3, :3], T[:3, 3], B.R[0], B.t[0])
     res = {"workload": "C5 flow: one 20000-pt pair, vote (3 x 32-d levels) -> feature RANSAC "
                        "d=0.025 -> NDP 9 x 40 on the inlier sources, wall clock",
            "ms": float(ms.sum()), "vote_ms": float(ms[0]), "ransac_ms": float(ms[1]),
            "ndp_ms": float(ms[2]), "inlier_sources": int(k), "rre_deg": float(rre),
-           "rte": float(rte)}
+           "rte": float(rte), "ndp_iterations_evaluated": [int(i["evaluated"]) for i in info]}
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O

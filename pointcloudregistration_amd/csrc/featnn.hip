@@ -878,12 +878,19 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     auto epilogue = [&](const f32x16 &acc, unsigned ct) {
         asm("" : "+s"(ct));
 #pragma unroll
+        // no inline asm here: the compiler must see every instruction that
+        // touches the accumulators (its MFMA hazard wait states are not placed
+        // around inline asm; with asm v_min / v_med3 in this kernel the first
+        // registers of some tiles read stale values).  min(a, b) is written as
+        // med3(a, b, -inf): the v_min builtin would add a NaN canonicalisation
+        // per operand.  A NaN value makes the row's top-2 NaN (uncertified: the
+        // exact rescan decides it).
         for (int r = 0; r < 16; ++r) {
             float vr;
             if constexpr (kIdx) vr = __uint_as_float((__float_as_uint(acc[r]) & keep_r) | ct);
             else vr = acc[r];
-            b2[r] = vmed3(b1[r], b2[r], vr);
-            b1[r] = vmin(b1[r], vr);
+            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], vr);
+            b1[r] = __builtin_amdgcn_fmed3f(b1[r], vr, -3.40282347e+38f);
         }
     };
     constexpr int kV = kIdx ? 7 : 5;  // VALU per MFMA slot in the schedule below
@@ -971,8 +978,11 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             for (int r = 0; r < 16; ++r) {
                 const float ob1 = __shfl_xor(b1[r], o, 64);
                 const float ob2 = __shfl_xor(b2[r], o, 64);
-                b2[r] = vmin(vmax(b1[r], ob1), vmin(b2[r], ob2));
-                b1[r] = vmin(b1[r], ob1);
+                // second of {b1, b2} u {ob1, ob2} = med3(b1, ob1, min(b2, ob2))
+                // for sorted pairs; NaN stays NaN (uncertified)
+                const float m2 = __builtin_amdgcn_fmed3f(b2[r], ob2, -3.40282347e+38f);
+                b2[r] = __builtin_amdgcn_fmed3f(b1[r], ob1, m2);
+                b1[r] = __builtin_amdgcn_fmed3f(b1[r], ob1, -3.40282347e+38f);
             }
         }
         if (lr >= 16) return;

@@ -26,7 +26,9 @@ flag = take(np.int32, pn + P); nj = take(np.int32, P)
 e12o = O.featnn(fs, ft); e21o = O.featnn(ft, fs)
 mut = e21o[e12o] == np.arange(N)
 print("nj", nj, "unique nn12", len(np.unique(e12o)), "oracle mutual", mut.sum(), "gpu", int(nc[0]))
-print("flag counts", np.bincount(flag[:N], minlength=3))
+fl = flag[1:N + 1] - flag[:N]   # the corres kernel left the exclusive scan of the flags
+print("gpu flags sum", fl.sum(), "listed columns", (used[:M] == 2).sum())
+flag = fl
 mx = float(np.abs(np.concatenate([fs, ft])).max())
 E = int(np.frexp(mx)[1]); s = 2.0 ** (12 - E)
 bad = np.nonzero(mut & (flag[:N] == 0))[0]
@@ -36,4 +38,18 @@ for i in bad[:10]:
     D = ((fs[i].astype(np.float64) - ft[j]) ** 2).sum() * s * s
     dcol = ((fs.astype(np.float64) - ft[j]) ** 2).sum(1) * s * s
     srt = np.sort(dcol)
-    print(i, j, "v12 %.6g e12 %.3g w1 %.6g w2 %.6g exactD %.6g col top2 %.6g %.6g used %d" % (v12[i], e12[i], w1[j], w2[j], D, srt[0], srt[1], used[j]))
+    print(i, j, "v12 %.6g e12 %.3g w1 %.6g w2 %.6g exactD %.6g col top2 %.6g %.6g used %d nn21x %d oracle21 %d" % (v12[i], e12[i], w1[j], w2[j], D, srt[0], srt[1], used[j], nn21x[j], e21o[j]))
+extra = np.nonzero(~mut & (flag == 1))[0]
+print("wrongly accepted:", len(extra))
+# every J column: pass-2 minimum vs the exact column minimum (scaled)
+Dall = ((fs.astype(np.float64)[:, None, :] - ft.astype(np.float64)[None, :, :]) ** 2).sum(-1) * s * s
+cmin = Dall.min(0)
+J = jl[:int(nj[0])]
+errs = np.abs(w1[J] - cmin[J]) / cmin[J]
+badj = J[errs > 1e-3]
+print("J", len(J), "bad w1", len(badj), "neg", int((w1[J] < 0).sum()))
+slots = pos[badj]
+print("bad slots mod 32:", np.bincount(slots % 32, minlength=32))
+print("bad slots tile:", np.bincount(slots // 32))
+print("bad j mod 32:", np.bincount(badj % 32, minlength=32))
+print("bad j tile:", np.bincount(badj // 32)[:40])
