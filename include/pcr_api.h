@@ -152,9 +152,11 @@ typedef struct pcr_ransac_params {
  * Blocks the host between rounds of hypotheses (one 32-byte readback per
  * round: [0,1024), then 4096 at a time while a pair's bound est_k lies beyond).
  * Verification runs speculatively on persistent workgroups, the sequential rule
- * is replayed afterwards: results do not depend on the scheduling.  Workspace:
- * up to 256 MB of per-hypothesis target slots per device (fewer slots only add
- * one sweep per pair).
+ * is replayed afterwards: results do not depend on the scheduling.  Workspace
+ * per pair: ~135 B per hypothesis of the largest round (4096 when
+ * max_iteration > 1024, else max_iteration rounded up to 256: ~540 KB / ~135 KB
+ * per pair), 2 x Nmax x 4 B of target buffers, plus up to 256 MB per device of
+ * per-hypothesis target slots (fewer slots only add one sweep per pair).
  * ------------------------------------------------------------------------- */
 int pcr_ransac_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t Nmax,
                      int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt,

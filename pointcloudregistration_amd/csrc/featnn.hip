@@ -338,6 +338,11 @@ struct DualArgs5 {
 // NaN canonicalisation (v_max x,x) per packed operand.  Inputs are never
 // signalling NaNs; a quiet NaN (NaN feature) is ignored by IEEE min, as the
 // oracle's strict < ignores it, or forces a rescan.
+// NEVER feed an MFMA accumulator straight into these: the compiler does not
+// place the MFMA read-after-write wait states in front of inline asm, and the
+// first registers read come back without the chain's last MFMA (measured:
+// featnn_row7 with asm reads of acc).  Here every operand comes from a
+// compiler-visible instruction (the index pack).
 __device__ __forceinline__ float vmin(float a, float b) {
     float d;
     asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
@@ -924,6 +929,10 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                 if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
             }
+            // one scheduling region per tile: the next tile's fragments stay
+            // prefetches (without it the scheduler sank them next to their
+            // MFMAs: an LDS round trip in front of every MFMA)
+            __builtin_amdgcn_sched_barrier(0);
         }
         epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1));
         // the next group's DMA has landed for every wave, and every wave is done

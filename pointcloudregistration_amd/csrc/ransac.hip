@@ -698,7 +698,9 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.words = (Nmax + 31) / 32;
     a.order = nullptr;
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
-    a.hcap = kRoundN;  // >= kRound0, multiple of 256
+    // hypotheses per round slot: the largest round that can run (kRound0 when
+    // max_iteration fits the first round), a multiple of 256
+    a.hcap = a.max_iter > kRound0 ? kRoundN : std::max(256, (std::max(a.max_iter, 1) + 255) / 256 * 256);
     // target slots of the first tasks of every pair (the best's are kept from
     // there; a best without one is swept again at the end): up to 32 per pair
     // within 256 MB

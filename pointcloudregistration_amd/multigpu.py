@@ -12,6 +12,8 @@ import os
 import socket
 import subprocess
 import sys
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -54,17 +56,21 @@ def gather_records(rec: torch.Tensor, world: int, rows: int | None = None):
     return torch.cat(parts, 0)
 
 
-def launch_local_ranks(cmd, world: int, timeout=None):
+def launch_local_ranks(cmd, world: int, timeout=1800.0):
     """Start `world` copies of `cmd` as rank processes of one node (RANK, LOCAL_RANK,
     WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT): what
     torchrun --nproc-per-node would do, for a parent that must not touch the GPU
     itself.  Returns (exit code, rank 0's stdout): 0 only if every rank exited 0.
-    A failed rank 0 leaves the others blocked in a collective, so they are ended."""
+    Every rank is polled: as soon as ANY rank exits non-zero the others (blocked
+    in a collective, waiting for it) are ended, and so are all of them after
+    `timeout` seconds (None: no limit)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    procs = []
+    procs, out = [], []
+    rcs = [None] * world
+    reader = None
     try:
         for r in range(world):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
@@ -72,18 +78,26 @@ def launch_local_ranks(cmd, world: int, timeout=None):
                        MASTER_PORT=str(port))
             procs.append(subprocess.Popen(cmd, env=env,
                                           stdout=subprocess.PIPE if r == 0 else None))
-        out0 = procs[0].communicate(timeout=timeout)[0] or b""
-        rcs = [procs[0].returncode]
-        for p in procs[1:]:
-            if rcs[0] != 0 and p.poll() is None:
-                p.kill()
-            rcs.append(p.wait(timeout=timeout))
+        # rank 0's stdout is drained on a thread so a full pipe never blocks it
+        reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+        reader.start()
+        deadline = None if timeout is None else time.monotonic() + timeout
+        while True:
+            rcs = [p.poll() for p in procs]
+            if all(c is not None for c in rcs) or any(c not in (None, 0) for c in rcs):
+                break
+            if deadline is not None and time.monotonic() > deadline:
+                print(f"launch_local_ranks: timeout after {timeout} s", file=sys.stderr)
+                break
+            time.sleep(0.1)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-                p.wait()
+        rcs = [p.wait() for p in procs]  # a killed rank reports a negative code
+        if reader is not None:
+            reader.join(timeout=10)
     rc = 0 if all(c == 0 for c in rcs) else 1
     if rc:
         print(f"launch_local_ranks: rank exit codes {rcs}", file=sys.stderr)
-    return rc, out0.decode("utf-8", "replace")
+    return rc, (out[0] if out else b"").decode("utf-8", "replace")
