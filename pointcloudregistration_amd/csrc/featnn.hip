@@ -829,46 +829,56 @@ struct RowArgs5 {
     float *w1, *w2;             // pass 2: top-2 values by original row index
 };
 
-template <int NCH, int G, bool kIdx>
+// RT row tiles per wave share every B fragment read (two MFMAs per ds_read):
+// a workgroup covers 8 * RT * 32 rows per pass over the pair's column stream,
+// which halves the L2 -> LDS traffic at RT = 2 (at RT = 1 the stream of the
+// packed columns ran near the chip's LDS-DMA rate: waves parked ~35 %).
+template <int NCH, int G, bool kIdx, int RT>
 __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
-    constexpr int W = 8;              // waves per workgroup, one 32-row tile each
+    constexpr int W = 8;              // waves per workgroup, RT 32-row tiles each
     constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
     __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
     if (p >= a.P) return;  // whole block
     const int nr = a.rlist ? a.rcount[p] : count_of(a.n_rows, p, a.Rmax);
-    if (rb * W * 32 >= nr) return;  // whole block: no rows here
+    if (rb * W * RT * 32 >= nr) return;  // whole block: no rows here
     const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
     const int m = count_of(a.n_cols, p, a.Cmax);
-    const int qt = rb * W + wid;
+    const int qt0 = (rb * W + wid) * RT;  // this wave's first row tile
     const int ntc = (m + 31) >> 5;
     const int ngroups = (ntc + G - 1) / G;
     const unsigned ctmask = (1u << a.ctbits) - 1u;
     unsigned keep_r = ~ctmask;
     asm("" : "+v"(keep_r));
-    f16x8 A[NCH];
-    if (a.rlist) {  // gathered rows: lane l holds row slot qt*32 + (l & 31), half h
-        const int k = qt * 32 + (l & 31);
-        if (k < nr) {
-            const int j = a.rlist[(size_t)p * a.Rmax + k];
-            const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + (j >> 5)) * NCH * 64 + (j & 31) + 32 * h;
+    f16x8 A[RT][NCH];
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
-        } else {
+    for (int t = 0; t < RT; ++t) {
+        const int qt = qt0 + t;
+        if (a.rlist) {  // gathered rows: lane l holds row slot qt*32 + (l & 31), half h
+            const int k = qt * 32 + (l & 31);
+            if (k < nr) {
+                const int j = a.rlist[(size_t)p * a.Rmax + k];
+                const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + (j >> 5)) * NCH * 64 + (j & 31) + 32 * h;
 #pragma unroll
-            for (int c = 0; c < NCH; ++c)
+                for (int c = 0; c < NCH; ++c) A[t][c] = qp[(size_t)c * 64];
+            } else {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) A[c][q] = (_Float16)0.0f;
+                for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) A[t][c][q] = (_Float16)0.0f;
+            }
+        } else {  // padded row tiles (qt < ntr) hold sentinel rows
+            const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt) * NCH * 64 + l;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) A[t][c] = qp[(size_t)c * 64];
         }
-    } else {
-        const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt) * NCH * 64 + l;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
     }
-    float b1[16], b2[16];
+    float b1[RT][16], b2[RT][16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { b1[t][r] = __builtin_inff(); b2[t][r] = __builtin_inff(); }
     const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NCH * 64 + l;
     auto issue = [&](int grp, int bufi) {
         for (int c = wid; c < G * NCH; c += W) {
@@ -879,26 +889,27 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         }
     };
     // row top-2 of the tile's 16 values per lane: pass 1 with the column tile
-    // index in the low ctbits bits (3 VALU per value), pass 2 values only (2)
-    auto epilogue = [&](const f32x16 &acc, unsigned ct) {
+    // index in the low ctbits bits (3 VALU per value), pass 2 values only (2).
+    // No inline asm here: the compiler must see every instruction that touches
+    // the accumulators (its MFMA hazard wait states are not placed around
+    // inline asm; with asm v_min / v_med3 the first registers of some tiles
+    // read stale values).  min(a, b) is written med3(a, b, -FLT_MAX): the min
+    // builtin would add a NaN canonicalisation per operand.  A NaN value makes
+    // the row's top-2 NaN (uncertified: the exact rescan decides it).
+    auto epilogue = [&](const f32x16 (&acc)[RT], unsigned ct) {
         asm("" : "+s"(ct));
 #pragma unroll
-        // no inline asm here: the compiler must see every instruction that
-        // touches the accumulators (its MFMA hazard wait states are not placed
-        // around inline asm; with asm v_min / v_med3 in this kernel the first
-        // registers of some tiles read stale values).  min(a, b) is written as
-        // med3(a, b, -inf): the v_min builtin would add a NaN canonicalisation
-        // per operand.  A NaN value makes the row's top-2 NaN (uncertified: the
-        // exact rescan decides it).
-        for (int r = 0; r < 16; ++r) {
-            float vr;
-            if constexpr (kIdx) vr = __uint_as_float((__float_as_uint(acc[r]) & keep_r) | ct);
-            else vr = acc[r];
-            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], vr);
-            b1[r] = __builtin_amdgcn_fmed3f(b1[r], vr, -3.40282347e+38f);
-        }
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float vr;
+                if constexpr (kIdx) vr = __uint_as_float((__float_as_uint(acc[t][r]) & keep_r) | ct);
+                else vr = acc[t][r];
+                b2[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], b2[t][r], vr);
+                b1[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], vr, -3.40282347e+38f);
+            }
     };
-    constexpr int kV = kIdx ? 7 : 5;  // VALU per MFMA slot in the schedule below
+    constexpr int kV = (kIdx ? 48 : 32) * RT / NCH + 1;  // VALU per MFMA slot below
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -907,17 +918,21 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
         const f16x8 *Bb = Bs + buf * kB + l;
         f16x8 Bf[2][NCH];
-        f32x16 acc[2];
+        f32x16 acc[2][RT];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) Bf[0][c] = Bb[c * 64];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int cur = g & 1;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[cur][r] = 0.0f;
+            for (int t = 0; t < RT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[cur][t][r] = 0.0f;
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
-                acc[cur] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bf[cur][c], acc[cur], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < RT; ++t)
+                    acc[cur][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t][c], Bf[cur][c], acc[cur][t], 0, 0, 0);
             if (g + 1 < G) {
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NCH + c) * 64];
@@ -925,7 +940,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1));
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, RT, 0);
                 if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
             }
@@ -940,70 +955,72 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    if (qt * 32 >= nr) return;
     const int lr = l & 31;
-    if constexpr (kIdx) {
-        int i1[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[r]) & ctmask) * 32 + lr;
+    for (int t = 0; t < RT; ++t) {
+        const int qt = qt0 + t;
+        if (qt * 32 >= nr) break;
+        if constexpr (kIdx) {
+            int i1[16];
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
+            for (int r = 0; r < 16; ++r) i1[r] = (int)(__float_as_uint(b1[t][r]) & ctmask) * 32 + lr;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float ob1 = __shfl_xor(b1[r], o, 64);
-                const float ob2 = __shfl_xor(b2[r], o, 64);
-                const int oi1 = __shfl_xor(i1[r], o, 64);
-                top2_merge(b1[r], i1[r], b2[r], ob1, oi1, ob2);
+            for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float ob1 = __shfl_xor(b1[t][r], o, 64);
+                    const float ob2 = __shfl_xor(b2[t][r], o, 64);
+                    const int oi1 = __shfl_xor(i1[r], o, 64);
+                    top2_merge(b1[t][r], i1[r], b2[t][r], ob1, oi1, ob2);
+                }
             }
-        }
-        if (lr >= 16) return;
-        float mb1 = 0.f, mb2 = 0.f;
-        int mi1 = 0;
+            float mb1 = 0.f, mb2 = 0.f;
+            int mi1 = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; mi1 = i1[r]; }
-        const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-        if (row >= nr) return;
-        const size_t o = (size_t)p * a.Rmax + row;
-        if (m == 0) {
-            a.nn[o] = 0;
-            a.v[o] = __builtin_inf();
-            a.e[o] = 0.0f;
-            return;
-        }
-        a.nn[o] = mi1;
-        const double Gm = (double)__uint_as_float(a.cmax[p]);
-        const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
-        const double bnd = bound5(qn, Gm, 16 * NCH, a.D);
-        const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
-        a.v[o] = (double)mb1;
-        a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-        if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
-            a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
-    } else {
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float ob1 = __shfl_xor(b1[r], o, 64);
-                const float ob2 = __shfl_xor(b2[r], o, 64);
-                // second of {b1, b2} u {ob1, ob2} = med3(b1, ob1, min(b2, ob2))
-                // for sorted pairs; NaN stays NaN (uncertified)
-                const float m2 = __builtin_amdgcn_fmed3f(b2[r], ob2, -3.40282347e+38f);
-                b2[r] = __builtin_amdgcn_fmed3f(b1[r], ob1, m2);
-                b1[r] = __builtin_amdgcn_fmed3f(b1[r], ob1, -3.40282347e+38f);
+            for (int r = 0; r < 16; ++r)
+                if (lr == r) { mb1 = b1[t][r]; mb2 = b2[t][r]; mi1 = i1[r]; }
+            const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+            if (lr >= 16 || row >= nr) continue;
+            const size_t o = (size_t)p * a.Rmax + row;
+            if (m == 0) {
+                a.nn[o] = 0;
+                a.v[o] = __builtin_inf();
+                a.e[o] = 0.0f;
+                continue;
             }
-        }
-        if (lr >= 16) return;
-        float mb1 = 0.f, mb2 = 0.f;
+            a.nn[o] = mi1;
+            const double Gm = (double)__uint_as_float(a.cmax[p]);
+            const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+            const double bnd = bound5(qn, Gm, 16 * NCH, a.D);
+            const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
+            a.v[o] = (double)mb1;
+            a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
+            if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
+                a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
+        } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            if (lr == r) { mb1 = b1[r]; mb2 = b2[r]; }
-        const int k = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-        if (k >= nr) return;
-        const int j = a.rlist[(size_t)p * a.Rmax + k];
-        a.w1[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb1;
-        a.w2[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb2;
+            for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float ob1 = __shfl_xor(b1[t][r], o, 64);
+                    const float ob2 = __shfl_xor(b2[t][r], o, 64);
+                    // second of {b1, b2} u {ob1, ob2} = med3(b1, ob1, min(b2, ob2))
+                    // for sorted pairs; NaN stays NaN (uncertified)
+                    const float m2 = __builtin_amdgcn_fmed3f(b2[t][r], ob2, -3.40282347e+38f);
+                    b2[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], ob1, m2);
+                    b1[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], ob1, -3.40282347e+38f);
+                }
+            }
+            float mb1 = 0.f, mb2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (lr == r) { mb1 = b1[t][r]; mb2 = b2[t][r]; }
+            const int k = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
+            if (lr >= 16 || k >= nr) continue;
+            const int j = a.rlist[(size_t)p * a.Rmax + k];
+            a.w1[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb1;
+            a.w2[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb2;
+        }
     }
 }
 
@@ -1123,8 +1140,10 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.NCH = cdiv(3 * D + 6, 16);
     v.sp = split5_params(D);
     v.W = 8;                                          // waves (32-row tiles) per workgroup
-    v.nrb = cdiv(cdiv(Nmax, 32), v.W);
-    v.ntn = v.nrb * v.W;                              // row tiles, padded to whole blocks
+    v.nrb = cdiv(cdiv(Nmax, 32), v.W);                // dual screen row blocks
+    // row tiles, padded to whole blocks of the dual screen (8 tiles) and of the
+    // row screens (8 waves x kRowTiles tiles; the sentinel rows are valid encodings)
+    v.ntn = cdiv(cdiv(Nmax, 32), 16) * 16;
     v.ntm = cdiv(cdiv(Mmax, 32), 8) * 8;              // column tiles, padded to whole groups (G | 8)
     v.ctbits = 1;
     while ((1 << v.ctbits) < std::max(v.ntm, v.ntn)) ++v.ctbits;
@@ -1271,6 +1290,9 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     return run_rescan(ra, P, D, s);
 }
 
+// row tiles per wave of the row screens (featnn_row7)
+constexpr int kRowTiles = 2;
+
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
 static int launch_row7(const RowArgs5 &r, int NCH, hipStream_t s) {
@@ -1279,7 +1301,7 @@ static int launch_row7(const RowArgs5 &r, int NCH, hipStream_t s) {
     switch (NCH) {
 #define PCR_R7CASE(K)                                                                            \
     case K:                                                                                      \
-        hipLaunchKernelGGL((featnn_row7<K, (K <= 7 ? 8 : 4), kIdx>), dim3((unsigned)nblk),         \
+        hipLaunchKernelGGL((featnn_row7<K, (K <= 7 ? 8 : 4), kIdx, kRowTiles>), dim3((unsigned)nblk), \
                            dim3(512), 0, s, r);                                                  \
         break;
         PCR_R7CASE(1) PCR_R7CASE(2) PCR_R7CASE(3) PCR_R7CASE(4) PCR_R7CASE(5) PCR_R7CASE(6)
@@ -1328,7 +1350,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     RowArgs5 r;
     r.Ap = v.Ap; r.Bp = v.Bp; r.rnr = v.fnr; r.cmax = v.gmax; r.n_rows = n_src; r.n_cols = n_tgt;
     r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
-    r.ntc = ntm; r.nrb = v.nrb; r.D = D; r.ctbits = 1;
+    r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * kRowTiles); r.D = D; r.ctbits = 1;
     while ((1 << r.ctbits) < ntm) ++r.ctbits;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;
@@ -1350,7 +1372,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         RowArgs5 r2 = r;
         r2.Ap = v.Bp; r2.Bp = v.Ap; r2.rnr = v.gnr; r2.cmax = v.fmax; r2.n_rows = n_tgt;
         r2.n_cols = n_src; r2.rlist = ma.jlist; r2.rcount = ma.nj; r2.Rmax = Mmax; r2.Cmax = Nmax;
-        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W);
+        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * kRowTiles);
         r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
         r2.w1 = w1; r2.w2 = w2;
         prof_begin(s, kProfFeatScreen2);

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--d", type=int, default=32)
     ap.add_argument("--noise", type=float, default=1.0)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--mode", choices=("full", "mutual"), default="full",
+                    help="full: feature_match (dual screen); mutual: feature_correspondences")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(7)
     pool = int(a.n * 1.45)
@@ -32,24 +34,26 @@ def main():
         a.pairs, a.n, a.d, device="cuda", generator=g)
     F, G = F.contiguous(), G.contiguous()
     del code
-    reg.feature_match(F, G)
+    run = (lambda: reg.feature_match(F, G)) if a.mode == "full" else \
+        (lambda: reg.feature_correspondences(F, G))
+    run()
     torch.cuda.synchronize()
     _lib.profile_enable(True)
-    for pid in range(7):
+    for pid in range(9):
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(a.iters):
-        reg.feature_match(F, G)
+        run()
     ev1.record()
     torch.cuda.synchronize()
     prof = {name: _lib.profile_read(pid)[0] / a.iters for name, pid in
             (("screen", _lib.PROF_FEAT_SCREEN), ("rescan", _lib.PROF_FEAT_RESCAN),
-             ("pack", _lib.PROF_FEAT_PACK))}
+             ("pack", _lib.PROF_FEAT_PACK), ("screen2", _lib.PROF_FEAT_SCREEN2))}
     rows = _lib.featnn_rescan_rows(reset=True)
     flops = 2.0 * a.pairs * a.n * a.n * a.d
-    print(json.dumps({"pairs": a.pairs,
+    print(json.dumps({"pairs": a.pairs, "mode": a.mode,
                       "n": a.n, "d": a.d, "ms_total": ev0.elapsed_time(ev1) / a.iters,
                       "ms": prof, "screen_alg_tflops": flops / prof["screen"] / 1e9,
                       "rescan_rows": [r / a.iters for r in rows]}))

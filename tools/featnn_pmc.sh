@@ -5,12 +5,13 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 P=${1:-64}
-OUT=gpurun_out/pmc_featnn
+MODE=${2:-full}
+OUT=gpurun_out/pmc_featnn_$MODE
 mkdir -p "$OUT"
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run \
-    --output-format csv -- python3 tools/featnn_bench.py --pairs "$P" --iters 2 > "$OUT/$name.log" 2>&1
+    --output-format csv -- python3 tools/featnn_bench.py --pairs "$P" --iters 2 --mode "$MODE" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   [ $rc -eq 0 ] || exit $rc
