@@ -269,9 +269,13 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
             const double gmin = fmin(gx, fmin(gy, gz)) - margin;
             if (gmin > 0.0 && gmin * gmin * (1.0 - 8.0 * 5.9604644775390625e-08) > (double)best) done = true;
         }
-        if (!done) {  // not certified within kMaxRing rings: every candidate
-            for (int j = sub; j < m; j += LPQ) {
-                const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
+        if (!done) {  // not certified within kMaxRing rings: every candidate, read
+                      // as the grid's float4 (x, y, z, index) copy (one 16-B load each)
+#pragma unroll 4
+            for (int s = sub; s < m; s += LPQ) {
+                const float4 p = pts[s];
+                const float d = d2f(p.x, p.y, p.z, qx, qy, qz);
+                const int j = __float_as_int(p.w);
                 if (d < best || (d == best && j < bj)) { best = d; bj = j; }
             }
             merge();
