@@ -152,6 +152,13 @@ def cpu_baseline(batch, params, budget_s, pair_ids):
         shutil.rmtree(tmp, ignore_errors=True)
     return ({"value": rate, "unit": "pairs/s", "cores": W, "affinity_cpus": aff,
              "cpu_model": _cpu_model(), "kind": "port",
+             "per_gpu_share": {"value": rate, "cores": W,
+                               "note": "the GPU box's host share per GPU (16 cores); the pool "
+                                       "forbids more workers than that"},
+             "whole_host_extrapolated": {"value": rate * aff / W, "cores": aff,
+                                         "note": "per-worker rate x every affinity core (pair-"
+                                                 "parallel, no shared state: linear in cores "
+                                                 "up to memory bandwidth); not measured"},
              "sample": f"{done} of the workload's pairs ({batch.src.shape[1]} pts, D="
                        f"{batch.src_feat.shape[2]}) through the oracle pipeline (featnn x2, "
                        f"mutual corres, RANSAC, ICP, Chamfer), {W} single-threaded worker "
@@ -683,16 +690,7 @@ TRAFFIC_DIR = "profiles"
 
 def _traffic_file():
     """Newest committed PMC traffic summary (profiles/rNN/vMM_pmc_traffic.json)."""
-    import glob
-    import re
-    best, key = None, None
-    for f in glob.glob(os.path.join(ROOT, TRAFFIC_DIR, "r*", "*pmc_traffic.json")):
-        m = re.search(r"r(\d+)[/\\]v(\d+)_pmc_traffic\.json$", f)
-        if m:
-            k = (int(m.group(1)), int(m.group(2)))
-            if key is None or k > key:
-                best, key = f, k
-    return best
+    return _newest("pmc_traffic.json")
 
 
 def _pmc_traffic(kernel):
@@ -717,12 +715,66 @@ def _traffic_source():
     return os.path.relpath(f, ROOT) if f else None
 
 
-def _chamfer_roofline(prof, P, N):
+L2_HIT_CYC = 200        # MI355X_MICROARCH.md: global_load_dword L2-hit latency ~180-225 cycles
+CLOCK_GHZ_PEAK = 2.4
+WAVES_PER_SIMD = 8      # nng_query<1>: 39 VGPRs -> the 8-wave cap (guide: min(8, 512/alloc))
+
+
+def grid_walk_replay(q, c, max_ring=3):
+    """Host replay of nng_query's ring walk (nnd_grid.hip:186-288) for queries q
+    against cloud c: per query the cells probed and points read before its answer
+    is certified.  Cell size as nng_bbox (nnd_grid.hip:82-97); hash collisions
+    ignored.  A query certifies after the first ring k whose (2k+1)^3 block faces
+    lie farther than its true nearest neighbour (scipy cKDTree); past max_ring it
+    reads all of c (the fallback scan, 4 loads in flight per round trip).
+    Returns per-query dependent round trips (one per probed cell for its slot
+    starts + one per point read) in the kernel's slot (cell-sorted) order."""
+    from scipy.spatial import cKDTree
+    q = q.astype(np.float64)
+    c32 = c.astype(np.float32)
+    lo, hi = c32.min(0).astype(np.float64), c32.max(0).astype(np.float64)
+    e = hi - lo
+    m = e.max()
+    cell = float(np.float32(0.6 * np.cbrt(np.prod(np.maximum(e, 1e-3 * m)) / len(c))))
+    cc = np.floor(c.astype(np.float64) / cell).astype(np.int64)
+    key = lambda x, y, z: (x * 1_000_003 + y) * 1_000_033 + z  # noqa: E731
+    uk, cnt = np.unique(key(cc[:, 0], cc[:, 1], cc[:, 2]), return_counts=True)
+    dstar = cKDTree(c.astype(np.float64)).query(q)[0]
+    qc = np.floor(q / cell).astype(np.int64)
+    f0 = np.minimum(q - qc * cell, (qc + 1) * cell - q).min(1)
+    kdone = np.maximum(np.ceil((dstar - f0) / cell), 0).astype(np.int64)
+    trips = np.zeros(len(q))
+    for k in range(max_ring + 1):
+        sel = np.nonzero(kdone == k)[0]
+        if not len(sel):
+            continue
+        pts = np.zeros(len(sel))
+        r = np.arange(-k, k + 1)
+        for dx in r:
+            for dy in r:
+                for dz in r:
+                    kk = key(qc[sel, 0] + dx, qc[sel, 1] + dy, qc[sel, 2] + dz)
+                    pos = np.clip(np.searchsorted(uk, kk), 0, len(uk) - 1)
+                    pts += np.where(uk[pos] == kk, cnt[pos], 0)
+        trips[sel] = (2 * k + 1) ** 3 + pts
+    far = kdone > max_ring
+    trips[far] = 7 ** 3 + len(c) / 4.0
+    S = 256
+    while S < len(c):
+        S <<= 1
+    qh = ((qc[:, 0] * 73856093) ^ (qc[:, 1] * 19349663) ^ (qc[:, 2] * 83492791)) & (S - 1)
+    return trips[np.argsort(qh, kind="stable")], float(far.mean())
+
+
+def _chamfer_roofline(prof, P, N, samples):
     """Second roofline line: the a1 Chamfer kernel of the step (nng_query, one
-    launch = both directions of all P pairs).  Algorithmic bytes per launch: each
-    query point read once (12 B) and its (dist, idx) written (8 B), plus one read
-    of each cloud's grid (float4 points + slot starts).  It is bound by latency
-    (dependent cell walks, L2-resident grids), not HBM: frac shows how far."""
+    launch = both directions of all P pairs).  It is bound by the latency of its
+    dependent cell walks (the grids are L2-resident), so the bound is a
+    probe-latency model: per wave the longest lane's chain of dependent L2 round
+    trips (grid_walk_replay on the sampled pairs, both directions) x the L2-hit
+    latency, 8 waves per SIMD in flight on 1,024 SIMDs.  frac = model floor /
+    measured time.  The algorithmic bytes (each query read once, its (dist, idx)
+    written, each grid read once) are kept beside it as hbm_* for reference."""
     ms, n = prof
     if not n:
         return None
@@ -732,10 +784,38 @@ def _chamfer_roofline(prof, P, N):
         S <<= 1
     nbytes = 2 * P * N * (12 + 8) + 2 * P * (N * 16 + (S + 1) * 4)
     gbs = nbytes / (per * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": "nng_query<1> (certified grid 1-NN)", "achieved": gbs,
-            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-            "traffic": _pmc_traffic("nng_query"), "bytes_per_launch": nbytes,
-            "kernel_ms_per_launch": per, "launches": n}
+    wave_trips, mean_trips, far = [], [], []
+    for qa, ca in samples:
+        t, f = grid_walk_replay(qa, ca)
+        nw = len(t) // 64
+        wave_trips.append(t[:nw * 64].reshape(nw, 64).max(1).mean())
+        mean_trips.append(t.mean())
+        far.append(f)
+    waves = 2 * P * (-(-N // 64))
+    trips_w = float(np.mean(wave_trips))
+    slots = 1024 * WAVES_PER_SIMD
+    floor_ms = -(-waves // slots) * trips_w * L2_HIT_CYC / (CLOCK_GHZ_PEAK * 1e9) * 1e3
+    floors = {"l2_latency_ms": floor_ms}
+    sq, src = _pmc_sq("nng_query<1>")
+    if sq and "SQ_INSTS_VALU" in sq:
+        f64 = sum(sq.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                             "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        floors["valu_issue_ms"] = (2.0 * sq["SQ_INSTS_VALU"] + 2.0 * f64) / 1024 / (CLOCK_GHZ_PEAK * 1e9) * 1e3
+        floors["valu_insts_per_launch"] = sq["SQ_INSTS_VALU"]
+        floors["sq_source"] = src
+    top = max(floors.get("valu_issue_ms", 0.0), floor_ms)
+    return {"bound": "l2-latency (dependent probe chain)" if top == floor_ms else "valu-issue",
+            "kernel": "nng_query<1> (certified grid 1-NN)",
+            "model_floor_ms": top, "floors": floors, "kernel_ms_per_launch": per, "launches": n,
+            "frac": top / per,
+            "model": {"round_trips_per_query_mean": float(np.mean(mean_trips)),
+                      "round_trips_per_wave_max_lane": trips_w, "fallback_fraction": float(np.mean(far)),
+                      "l2_hit_cycles": L2_HIT_CYC, "clock_ghz": CLOCK_GHZ_PEAK,
+                      "waves_per_launch": waves, "waves_in_flight": slots,
+                      "source": f"grid_walk_replay over {len(samples)} sampled (query cloud, grid) "
+                                "directions of this step"},
+            "hbm_achieved_gbs": gbs, "hbm_peak_gbs": PEAK_HBM_GBS, "hbm_frac": gbs / PEAK_HBM_GBS,
+            "traffic": _pmc_traffic("nng_query"), "bytes_per_launch": nbytes}
 
 
 def grid_candidates(src, tgt, T, d):
@@ -765,31 +845,74 @@ def grid_candidates(src, tgt, T, d):
     return float(total.mean())
 
 
-# featnn_dual7's group loop per 32 x 32 tile and wave (8 tiles per group, the
-# group's merge and barrier amortised), counted in the gfx950 ISA of the shipped
-# build: 7 v_mfma_f32_32x32x16_f16, 106 VALU (35 v_min, 31 v_med3,
-# 32 v_and_or, 2 v_max, 2 v_permlane32_swap, ~4 others), 9 LDS (7 ds_read_b128,
-# one ds_write2st64_b32, the merge's reads), ~2 s_nop.  SIMD issue cycles (MI355X
-# guide, 'vector-instruction ISSUE cost'): an MFMA holds vector issue 8 of its 32
-# cycles, VALU / LDS / s_nop 4 each.  The two waves of a SIMD share that port.
-SCREEN_TILE_ISSUE = {"mfma": 7 * 8, "valu": 106 * 4, "lds": 9 * 4, "s_nop": 2 * 4}
+# Per 32 x 32 tile and wave, the inner loop of the shipped build's screens
+# (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 8
+# column tiles, D = 32 -> NCH = 7 k-chunks of 16):
+#  pass 1 featnn_row7<7,8,true,2>:  7 v_mfma_f32_32x32x16_f16, 48 VALU (32 v_med3
+#    for the top-2 update, 16 v_and_or packing the column code), 3.5 ds_read_b128
+#    (each B fragment shared by the 2 row tiles), ~1.2 SALU;
+#  pass 2 featnn_row7<7,8,false,2>: 7 MFMA, 32 v_med3 (values only), 3.5 LDS,
+#    0.44 s_nop.
+# SIMD issue cycles (MI355X guide, 'vector-instruction ISSUE cost'): an MFMA holds
+# vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the two waves of a
+# SIMD share that port.  The MFMA pipe needs 7 x 32 = 224 cycles per tile.
+SCREEN_TILE_ISSUE = {"mfma": 7 * 8, "valu": 48 * 4, "lds": 3.5 * 4}
+SCREEN2_TILE_ISSUE = {"mfma": 7 * 8, "valu": 32 * 4, "lds": 3.5 * 4, "s_nop": 0.44 * 4}
 
 
-def _screen_issue_model(P, N, ms):
-    """Issue-bound floor of the feature screen: every tile's instructions must pass
-    the SIMD's single vector-issue port; MFMA time alone (7 x 32 cycles) is below."""
-    cyc = sum(SCREEN_TILE_ISSUE.values())
-    tiles = P * (N // 32) * (N // 32)
-    floor_ms = tiles * cyc / 1024 / 2.4e9 * 1e3   # 1,024 SIMDs at 2.4 GHz
-    return {"cycles_per_tile": cyc, "breakdown": SCREEN_TILE_ISSUE, "tiles_per_launch": tiles,
-            "mfma_pipe_cycles_per_tile": 7 * 32, "floor_ms_at_2p4ghz": floor_ms,
-            "issue_frac": floor_ms / ms if ms else None}
+def _screen_issue_model(tiles, ms, table):
+    """Floor of a feature screen launch: per tile the larger of its vector-issue
+    cycles and the MFMA pipe's 224, on 1,024 SIMDs at 2.4 GHz."""
+    issue = sum(table.values())
+    cyc = max(issue, 7 * 32)
+    floor_ms = tiles * cyc / 1024 / (CLOCK_GHZ_PEAK * 1e9) * 1e3
+    return {"issue_cycles_per_tile": issue, "breakdown": table, "tiles_per_launch": tiles,
+            "mfma_pipe_cycles_per_tile": 7 * 32,
+            "binding": "vector issue" if issue > 7 * 32 else "MFMA pipe",
+            "floor_ms_at_2p4ghz": floor_ms, "model_frac": floor_ms / ms if ms else None}
+
+
+def _newest(pattern):
+    """Newest committed profiles/rNN/vMM_<pattern> file, or None."""
+    import glob
+    import re
+    best, key = None, None
+    for f in glob.glob(os.path.join(ROOT, TRAFFIC_DIR, "r*", "*" + pattern)):
+        m = re.search(r"r(\d+)[/\\]v(\d+)_" + re.escape(pattern) + "$", f)
+        if m:
+            k = (int(m.group(1)), int(m.group(2)))
+            if key is None or k > key:
+                best, key = f, k
+    return best
+
+
+def _pmc_sq(kernel):
+    """Per-launch SQ instruction counters of `kernel` (tools/pmc_sq.sh on this
+    bench, the newest profiles/rNN/vMM_sq_pmc.json), or None."""
+    f = _newest("sq_pmc.json")
+    if f is None:
+        return None, None
+    try:
+        with open(f) as fh:
+            ks = json.load(fh)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for k, v in ks.items():
+        if kernel in k:
+            return v.get("counters", v), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
-    """HBM roofline line of a grid-sweep kernel (RANSAC verification a7 / ICP a8)
-    with SURVEY 8d's algorithmic bytes per sweep of N source points:
-    N*12 (points) + N*c_bar*12 (candidate targets) + N/8 (inlier mask bits)."""
+    """Roofline line of a grid-sweep kernel (RANSAC verification a7 / ICP a8).
+    Its candidate gathers are served from the pair's LDS copy of the target grid,
+    so the bound is VALU issue: the kernel's own executed VALU instructions (PMC
+    SQ_INSTS_VALU per launch, tools/pmc_sq.sh) at the SIMD's throughput -- a wave64
+    f32 VALU instruction takes 2 cycles of a SIMD-32, an f64 one 4 (the f64 vector
+    rate is half the f32 rate) -- on 1,024 SIMDs at 2.4 GHz.  frac = that floor /
+    measured time.  SURVEY 8d's algorithmic bytes per sweep of N source points
+    (N*12 points + N*c_bar*12 candidate targets + N/8 inlier mask bits) are kept
+    beside it, labelled LDS-served."""
     ms, n = prof
     if not n:
         return None
@@ -797,12 +920,26 @@ def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
     per_sweep = N * 12 + N * cbar * 12 + N / 8
     nbytes = sweeps * per_sweep
     gbs = nbytes / (per * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": kernel, "achieved": gbs, "peak": PEAK_HBM_GBS,
-            "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": _pmc_traffic(kernel),
-            "bytes_per_launch": nbytes, "sweeps_per_launch": sweeps, "c_bar": cbar,
-            "kernel_ms_per_launch": per, "launches": n,
-            "note": f"{name}: candidate gathers are served from the pair's LDS copy of its "
-                    "target grid, so HBM sees far less than these algorithmic bytes"}
+    sq, src = _pmc_sq(kernel)
+    out = {"bound": "valu-issue", "kernel": kernel, "kernel_ms_per_launch": per, "launches": n,
+           "sweeps_per_launch": sweeps, "c_bar": cbar,
+           "lds_served": {"algorithmic_bytes_per_launch": nbytes, "achieved_gbs": gbs,
+                          "note": f"{name}: candidate gathers read the pair's LDS copy of its "
+                                  "target grid; HBM sees the points once per launch"},
+           "traffic": _pmc_traffic(kernel), "frac": None}
+    if sq and "SQ_INSTS_VALU" in sq:
+        valu = sq["SQ_INSTS_VALU"]
+        f64 = sum(sq.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                             "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        cyc = 2.0 * (valu - f64) + 4.0 * f64
+        floor_ms = cyc / 1024 / (CLOCK_GHZ_PEAK * 1e9) * 1e3
+        lane_ops = valu * 64 + f64 * 64   # f32-equivalent lane operations (f64 = 2)
+        out.update({"achieved": lane_ops / (per * 1e-3) / 1e12,
+                    "peak": 1024 * 32 * CLOCK_GHZ_PEAK / 1e3, "unit": "T lane-op/s (f32-equivalent VALU)",
+                    "frac": floor_ms / per, "model_floor_ms": floor_ms,
+                    "valu_insts_per_launch": valu, "valu_f64_insts_per_launch": f64 if f64 else None,
+                    "lds_insts_per_launch": sq.get("SQ_INSTS_LDS"), "sq_source": src})
+    return out
 
 
 def run_timed(step, steps, warmup, world):
@@ -929,7 +1066,7 @@ def main():
         step()
     torch.cuda.synchronize()
     _lib.profile_enable(True)
-    for pid in range(8):
+    for pid in range(_lib.PROF_SLOTS):
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
     wall, rec = run_timed(step, args.steps, 0, world)
@@ -937,7 +1074,8 @@ def main():
             (("feature_screen", _lib.PROF_FEAT_SCREEN), ("nnd_fwd", _lib.PROF_NND_FWD),
              ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
              ("icp", _lib.PROF_ICP), ("feat_rescan", _lib.PROF_FEAT_RESCAN),
-             ("feat_pack", _lib.PROF_FEAT_PACK), ("nnd_grid_query", _lib.PROF_NND_GRID))}
+             ("feat_pack", _lib.PROF_FEAT_PACK), ("nnd_grid_query", _lib.PROF_NND_GRID),
+             ("feature_screen2", _lib.PROF_FEAT_SCREEN2))}
     _lib.profile_enable(False)
     rescan_rows = _lib.featnn_rescan_rows(reset=True)
 
@@ -947,16 +1085,28 @@ def main():
     stages = dict(zip(("feature_match", "corres+ransac", "icp", "transform", "chamfer"),
                       pipe.stage_ms()))
 
-    # dominant kernel: the feature-distance screen (one launch = both directions
-    # for all P pairs).  Algorithmic work: P*N*M*D MACs = 2*P*N*M*D
-    # flops.  It runs on the f16 MFMA with a 3-term split: per 32x32 tile
-    # 16*NCH k-steps (NCH = ceil((3D+6)/16)) instead of D -> executed flops.
+    # dominant kernel: pass 1 of the feature screen, featnn_row7 (one launch = the
+    # source->target row screen of all P pairs, index packed in).  Algorithmic
+    # work: the P*N*M*D MACs of the distance matrix = 2*P*N*M*D flops,
+    # which pass 1 computes in full; pass 2 re-screens only the target rows J that
+    # some source chose (the mutual check), so the screen STAGE (pass 1 + pass 2)
+    # is also reported against the same algorithmic flops.  Both run on the f16
+    # MFMA with a 3-term split: 16*NCH k-steps per tile (NCH = ceil((3D+6)/16))
+    # instead of D -> executed flops.
     ms_tot, launches = prof["feature_screen"]
     per_launch_ms = ms_tot / max(launches, 1)
+    ms2_tot, launches2 = prof["feature_screen2"]
+    per2_ms = ms2_tot / max(launches2, 1)
     flops_launch = 2.0 * P * N * N * D
     kexec = 16 * -(-(3 * D + 6) // 16)
     achieved = flops_launch / (per_launch_ms * 1e-3) / 1e12
     executed = achieved * kexec / D
+    nn12 = torch.sort(pipe.nn12, dim=1).values
+    jrows = ((nn12[:, 1:] != nn12[:, :-1]).sum(1) + 1).cpu().numpy().astype(np.int64)
+    tiles1 = P * (-(-N // 32)) * (-(-N // 32))
+    tiles2 = int(sum(-(-int(j) // 32) for j in jrows)) * (-(-N // 32))
+    stage_ms = per_launch_ms + per2_ms
+    stage_tf = flops_launch / (stage_ms * 1e-3) / 1e12
 
     recs = rec.cpu().numpy()
     mine = recs[rank * rows:rank * rows + P]
@@ -973,6 +1123,10 @@ def main():
                                           params.ransac.max_correspondence_distance) for p in samp]))
     cb_i = float(np.mean([grid_candidates(batch.src[p], batch.tgt[p], T_icp[p],
                                           params.icp.max_correspondence_distance) for p in samp]))
+    chamfer_samples = []
+    for p in samp[:2]:
+        al = (batch.src[p].astype(np.float64) @ T_icp[p, :3, :3].T + T_icp[p, :3, 3]).astype(np.float32)
+        chamfer_samples += [(al, batch.tgt[p]), (batch.tgt[p], al)]
 
     total_pairs = args.pairs * args.steps   # every pair of the job, once per step
     out = {
@@ -997,18 +1151,30 @@ def main():
                    "inputs": "resident in HBM (see host_resident for the PCIe-inclusive rate)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_F16_MFMA_TFLOPS,
-                     "traffic": _pmc_traffic("featnn_dual7"),
+                     "traffic": _pmc_traffic("featnn_row7<7, 8, true"),
                      "traffic_source": f"{_traffic_source()} (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this bench; FETCH_SIZE x2 per the "
                                        "gfx950 note)",
-                     "kernel": "featnn_dual7 (v_mfma_f32_32x32x16_f16, f16x3 split, top-2 epilogue)",
+                     "kernel": "featnn_row7<7,8,true,2> (pass 1: v_mfma_f32_32x32x16_f16, f16x3 "
+                               "split, row top-2 with packed column code)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,
                      "executed_mfma_tflops": executed,
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS,
-                     "issue_model": _screen_issue_model(P, N, per_launch_ms)},
-        "roofline_chamfer": _chamfer_roofline(prof["nnd_grid_query"], P, N),
+                     "issue_model": _screen_issue_model(tiles1, per_launch_ms, SCREEN_TILE_ISSUE),
+                     "pass2": {"kernel": "featnn_row7<7,8,false,2> (target rows J = unique(nn12), "
+                                         "values only)",
+                               "kernel_ms_per_launch": per2_ms, "launches": launches2,
+                               "j_rows_mean": float(jrows.mean()),
+                               "flops_per_launch": 2.0 * float(jrows.sum()) * N * D,
+                               "traffic": _pmc_traffic("featnn_row7<7, 8, false"),
+                               "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN2_TILE_ISSUE)},
+                     "screen_stage": {"ms_per_launch": stage_ms, "achieved": stage_tf,
+                                      "frac": stage_tf / PEAK_F16_MFMA_TFLOPS,
+                                      "note": "pass 1 + pass 2 against the distance matrix's "
+                                              "2*P*N*M*D algorithmic flops"}},
+        "roofline_chamfer": _chamfer_roofline(prof["nnd_grid_query"], P, N, chamfer_samples),
         "roofline_ransac": _sweep_roofline("a7 RANSAC verification", "ransac_sweep_kernel",
                                            prof["ransac_validate"], validated, N, cb_r),
         "roofline_icp": _sweep_roofline("a8 ICP", "icp_kernel", prof["icp"], icp_sweeps, N, cb_i),

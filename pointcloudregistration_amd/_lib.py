@@ -134,6 +134,7 @@ def exported_symbols():
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
 PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID, PROF_FEAT_SCREEN2 = 5, 6, 7, 8
+PROF_SLOTS = 9   # pcr_internal.h kProfSlots
 
 
 def profile_enable(on=True):

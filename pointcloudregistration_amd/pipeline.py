@@ -70,7 +70,7 @@ class PairPipeline:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
             ev[0].record()
         # feature NN + mutual filter (nn21 only where the filter reads it)
-        corres, ncor, _ = reg.feature_correspondences(
+        corres, ncor, nn12 = reg.feature_correspondences(
             self.src_feat, self.tgt_feat, mutual_filter=self.params.ransac.mutual_filter,
             ransac_n=self.params.ransac.ransac_n)
         if ev:
@@ -93,6 +93,7 @@ class PairPipeline:
             self.stage_events = ev
         self.last = (rr, ir, chamfer, ncor)
         self.corres = corres
+        self.nn12 = nn12
         return rr, ir, chamfer
 
     def stage_ms(self):

@@ -16,6 +16,8 @@ if [ "${STAGE:-tests}" = tests ]; then
 else
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary > gpurun_out/${T}_prof.log 2>&1 || exit 14
   timeout -k 10 700 bash tools/pmc_traffic.sh gpurun_out/${T}_pmc > gpurun_out/${T}_pmc.log 2>&1 || exit 15
+  timeout -k 10 700 bash tools/pmc_sq.sh gpurun_out/${T}_sq > gpurun_out/${T}_sq.log 2>&1 || exit 17
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_c5prof -o run -- python3 tools/c5_run.py > gpurun_out/${T}_c5prof.log 2>&1 || exit 18
   for P in 32 64; do
     timeout -k 10 200 python bench.py --pairs $P --no-secondary --no-cpu-baseline --no-host-resident > gpurun_out/${T}_bench_${P}pairs.json 2>/dev/null || exit 16
   done
