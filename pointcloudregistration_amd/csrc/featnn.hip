@@ -65,20 +65,31 @@ __global__ __launch_bounds__(1024) void corres_build(const int32_t *nn12, const 
 //          (T = 12 at D <= 64) -> every x fits f16 with room for the products.
 //   split: x = hi + lo + e_x, hi = f16(x), lo = f16(x - hi): |e_x| <= 2^-22|x|
 //          + 2^-14 (the 2^-14 covers f16 subnormals even if flushed).
-//   operands (k order): A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c]
-//                       B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo]
+//   operands (k order, each D-segment padded to S = ceil(D/16) chunks of 16):
+//          A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c]
+//          B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo]
 //          nx = |x|^2 / c split into three f16 parts, c = 2^cs fits f16.
+//          Executed: NX = 3S + 1 k-chunks (one MFMA each).  Stored: NM = 2S + 1
+//          -- A as [-2hi | -2lo | norms], B as [hi | lo | norms]; the MFMA of
+//          chunk c reads A chunk amap(c) and B chunk bmap(c) (the repeated
+//          segment is the same registers), so the packed operands, the
+//          L2 -> LDS stream and the B-fragment LDS reads are 5/7 of the
+//          executed k at D = 32.
 //   C = 0 -> d'_ij = |x_i|^2 + |y_j|^2 - 2 x_i.y_j (scaled by 2^2e) with
 //   |d' - d'_exact| <= err(q, G) (bound5 below).  Products are exact in f32;
 //   the accumulation is charged 2 (Kt + 2) u (|x| + |y|)^2 whatever the
 //   MFMA's internal summation order.  Rows/columns whose top-2 gap is not
 //   above 2 err are rescanned exactly in f64 (featnn_rescan2).
-// Packed layout: [pair][tile][chunk][lane] of 8 halves (lane l: row/col l&31,
+// Packed layout: [pair][tile][stored chunk][lane] of 8 halves (lane l: row/col l&31,
 // k = 16 chunk + 8 (l>>5) + j); padded tiles are valid encodings of +inf
 // rows, so no loop has a tail.  Grid: 1-D, XCD-aware: all row blocks of a
 // pair run on one XCD, whose L2 then holds that pair's B image (1.8 MB).
 // ---------------------------------------------------------------------------
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// executed k-chunk c -> stored A / B chunk (see the operand layout above)
+__host__ __device__ constexpr int amap(int c, int S) { return c < S ? c : (c < 3 * S ? c - S : 2 * S); }
+__host__ __device__ constexpr int bmap(int c, int S) { return c < 2 * S ? c : (c < 3 * S ? c - 2 * S : 2 * S); }
 
 struct Split5 {
     int T;   // target exponent of max|x|
@@ -141,9 +152,9 @@ __device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
 
 // role 0: rows (A), role 1: columns (B).  256-thread blocks, one wave per
 // 32-row tile; each tile is staged through LDS with coalesced loads (scaled,
-// exact) and every lane emits its NCH 16-byte operand fragments.
+// exact) and every lane emits its 2S + 1 stored 16-byte operand fragments.
 __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t *n, int Nmax, int D,
-                                                  int NCH, int ntiles, int role, Split5 sp,
+                                                  int S, int ntiles, int role, Split5 sp,
                                                   const unsigned *mx, f16x8 *Xp, float *nrm,
                                                   unsigned *nmax) {
     __shared__ float xs[4][32][65];  // D <= 64 (+1 pad: conflict-free row reads)
@@ -185,24 +196,26 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
         np[2] = (_Float16)65504.0f;
     }
     const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
-    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NCH * 64 + l;
-    for (int c = 0; c < NCH; ++c) {
+    const int NM = 2 * S + 1;
+    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NM * 64 + l;
+    for (int c = 0; c < NM; ++c) {
         f16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int k = 16 * c + 8 * h + j;
+            const int seg = c < S ? 0 : (c < 2 * S ? 1 : 2);   // hi | lo | norms
+            const int k = 16 * (c - seg * S) + 8 * h + j;      // index inside the segment
             _Float16 v = (_Float16)0.0f;
-            if (k < 3 * D) {
-                const int seg = (k >= D) + (k >= 2 * D);
-                const float xv = x[rr][k - seg * D];
-                const _Float16 hi = (_Float16)xv;
-                const _Float16 lo = (_Float16)(xv - (float)hi);
-                if (role == 0) v = (_Float16)(-2.0f * (float)(seg == 2 ? lo : hi));
-                else v = (seg == 1) ? lo : hi;
+            if (seg < 2) {
+                if (k < D) {
+                    const float xv = x[rr][k];
+                    const _Float16 hi = (_Float16)xv;
+                    const _Float16 lo = (_Float16)(xv - (float)hi);
+                    const _Float16 part = seg == 0 ? hi : lo;
+                    v = role == 0 ? (_Float16)(-2.0f * (float)part) : part;
+                }
             } else {
-                const int kk = k - 3 * D;
-                if (kk < 3) v = role == 0 ? np[kk] : cval;
-                else if (kk < 6) v = role == 0 ? cval : np[kk - 3];
+                if (k < 3) v = role == 0 ? np[k] : cval;
+                else if (k < 6) v = role == 0 ? cval : np[k - 3];
             }
             o[j] = v;
         }
@@ -226,9 +239,9 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
                                                    int ntiles, int role, Split5 sp,
                                                    const unsigned *mx, f16x8 *Xp, float *nrm,
                                                    unsigned *nmax) {
-    static_assert(D % 8 == 0, "segments must align to 8-half fragments");
-    constexpr int NCH = (3 * D + 6 + 15) / 16;
-    constexpr int G = D / 8;  // fragments per segment
+    constexpr int S = (D + 15) / 16;  // chunks per segment
+    constexpr int NM = 2 * S + 1;     // stored chunks
+    constexpr int G = 2 * S;          // 8-half fragments per segment
     const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
     const int cnt = count_of(n, p, Nmax);
@@ -268,19 +281,17 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
         np[2] = (_Float16)65504.0f;
     }
     const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
-    _Float16 s0[D], s1[D], s2[D];  // the three segments of this role
+    _Float16 s0[D], s1[D];  // the two stored segments of this role: hi | lo
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         const _Float16 hi = (_Float16)x[k];
         const _Float16 lo = (_Float16)(x[k] - (float)hi);
         if (role == 0) {
             s0[k] = (_Float16)(-2.0f * (float)hi);
-            s1[k] = s0[k];
-            s2[k] = (_Float16)(-2.0f * (float)lo);
+            s1[k] = (_Float16)(-2.0f * (float)lo);
         } else {
             s0[k] = hi;
             s1[k] = lo;
-            s2[k] = hi;
         }
     }
     auto frag = [&](int g) {  // compile-time g after unrolling
@@ -288,10 +299,10 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             _Float16 v = (_Float16)0.0f;
-            if (g < G) v = s0[8 * g + j];
-            else if (g < 2 * G) v = s1[8 * (g - G) + j];
-            else if (g < 3 * G) v = s2[8 * (g - 2 * G) + j];
-            else if (g == 3 * G) {
+            const int k0 = 8 * (g % G) + j;
+            if (g < G) v = k0 < D ? s0[k0 < D ? k0 : 0] : (_Float16)0.0f;
+            else if (g < 2 * G) v = k0 < D ? s1[k0 < D ? k0 : 0] : (_Float16)0.0f;
+            else if (g == 2 * G) {
                 if (j < 3) v = role == 0 ? np[j] : cval;
                 else if (j < 6) v = role == 0 ? cval : np[j - 3];
             }
@@ -299,9 +310,9 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
         }
         return o;
     };
-    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NCH * 64 + l;
+    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NM * 64 + l;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
+    for (int c = 0; c < NM; ++c) {
         const f16x8 a = frag(2 * c), b = frag(2 * c + 1);
         dst[(size_t)c * 64] = h ? b : a;
     }
@@ -370,10 +381,11 @@ __device__ __forceinline__ float vmed3(float a, float b, float c) {
 // 1 MFMA : 1 LDS read : V VALU by sched_group_barrier.  G = 8 tiles per LDS
 // group halves the barriers (B double buffer 2 x 57 KB + partials 32 KB).
 // ---------------------------------------------------------------------------
-template <int NCH, int G>
+template <int S, int G>
 __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
     constexpr int W = 8;  // waves per workgroup, one 32-row tile each
-    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
+    constexpr int NX = 3 * S + 1, NM = 2 * S + 1;  // executed / stored k-chunks
+    constexpr int kB = G * NM * 64;  // f16x8 per B buffer
     constexpr int kP = G * W * 32;
     __shared__ __attribute__((aligned(16))) char smem[2 * kB * 16 + 2 * 2 * kP * 4];
     // column partials first: their per-tile stores then fit the ds_write
@@ -398,18 +410,18 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
         ccode[r] = (unsigned)((wid << 5) | (h << 4) | r);
         asm("" : "+v"(ccode[r]));
     }
-    f16x8 A[NCH];
-    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NCH * 64 + l;
+    f16x8 A[NM];
+    const f16x8 *qp = a.Ap + ((size_t)p * a.ntn + qt) * NM * 64 + l;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) A[c] = qp[(size_t)c * 64];
+    for (int c = 0; c < NM; ++c) A[c] = qp[(size_t)c * 64];
     float b1[16], b2[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) { b1[r] = __builtin_inff(); b2[r] = __builtin_inff(); }
 
-    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NCH * 64 + l;
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntm * NM * 64 + l;
     auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NCH; c += W) {
-            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
+        for (int c = wid; c < G * NM; c += W) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NM + c) * 64;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)src,
                 (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
@@ -472,28 +484,29 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
         if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
         const f16x8 *Bb = Bs + buf * kB + l;
         const int pbase = buf * (G * W * 32) + wid * 32 + l;  // this group's column partials
-        f16x8 Bf[2][NCH];
+        f16x8 Bf[2][NM];
         f32x16 acc[2];
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) Bf[0][c] = Bb[c * 64];
+        for (int c = 0; c < NM; ++c) Bf[0][c] = Bb[c * 64];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int cur = g & 1;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[cur][r] = 0.0f;
 #pragma unroll
-            for (int c = 0; c < NCH; ++c)
-                acc[cur] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], Bf[cur][c], acc[cur], 0, 0, 0);
+            for (int c = 0; c < NX; ++c)
+                acc[cur] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[amap(c, S)], Bf[cur][bmap(c, S)], acc[cur],
+                                                                  0, 0, 0);
             if (g + 1 < G) {
 #pragma unroll
-                for (int c = 0; c < NCH; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NCH + c) * 64];
+                for (int c = 0; c < NM; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NM + c) * 64];
             }
             if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1), pbase, g - 1);
             // one region per iteration: MFMA : LDS read : VALU = 1 : 1 : 18
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
+            for (int c = 0; c < NX; ++c) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (g + 1 < G && c < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, 18, 0);
             }
         }
@@ -550,7 +563,7 @@ __global__ __launch_bounds__(512) void featnn_dual7(DualArgs5 a) {
     const double qn = (double)a.fnr[(size_t)p * a.ntn * 32 + row];
     const double pert = __builtin_ldexp(1.0, a.ctbits - 23) *
                         (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2));
-    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NCH, a.D) + pert))
+    if (!((double)mb2 - (double)mb1 > bound5(qn, Gm, 16 * NX, a.D) + pert))
         a.list12[(size_t)p * a.Nmax + atomicAdd(a.count12 + p, 1)] = row;
 }
 
@@ -815,8 +828,8 @@ __global__ __launch_bounds__(256) void featnn_rescan_merge(RescanArgs5 a, int S)
 // The result is the same set corres_build forms from the exact nn12 / nn21.
 // ---------------------------------------------------------------------------
 struct RowArgs5 {
-    const f16x8 *Ap;            // row operand (register-resident): [P][ntr][NCH][64]
-    const f16x8 *Bp;            // column operand (LDS-streamed): [P][ntc][NCH][64]
+    const f16x8 *Ap;            // row operand (register-resident): [P][ntr][NM][64]
+    const f16x8 *Bp;            // column operand (LDS-streamed): [P][ntc][NM][64]
     const float *rnr;           // scaled row norms, [P][ntr * 32] by original row index
     const unsigned *cmax;       // per pair max scaled column norm (f32 bits)
     const int32_t *n_rows, *n_cols;
@@ -833,10 +846,11 @@ struct RowArgs5 {
 // a workgroup covers 8 * RT * 32 rows per pass over the pair's column stream,
 // which halves the L2 -> LDS traffic at RT = 2 (at RT = 1 the stream of the
 // packed columns ran near the chip's LDS-DMA rate: waves parked ~35 %).
-template <int NCH, int G, bool kIdx, int RT>
+template <int S, int G, bool kIdx, int RT>
 __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     constexpr int W = 8;              // waves per workgroup, RT 32-row tiles each
-    constexpr int kB = G * NCH * 64;  // f16x8 per B buffer
+    constexpr int NX = 3 * S + 1, NM = 2 * S + 1;  // executed / stored k-chunks
+    constexpr int kB = G * NM * 64;   // f16x8 per B buffer
     __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
@@ -851,7 +865,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     const unsigned ctmask = (1u << a.ctbits) - 1u;
     unsigned keep_r = ~ctmask;
     asm("" : "+v"(keep_r));
-    f16x8 A[RT][NCH];
+    f16x8 A[RT][NM];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
         const int qt = qt0 + t;
@@ -859,19 +873,19 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             const int k = qt * 32 + (l & 31);
             if (k < nr) {
                 const int j = a.rlist[(size_t)p * a.Rmax + k];
-                const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + (j >> 5)) * NCH * 64 + (j & 31) + 32 * h;
+                const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + (j >> 5)) * NM * 64 + (j & 31) + 32 * h;
 #pragma unroll
-                for (int c = 0; c < NCH; ++c) A[t][c] = qp[(size_t)c * 64];
+                for (int c = 0; c < NM; ++c) A[t][c] = qp[(size_t)c * 64];
             } else {
 #pragma unroll
-                for (int c = 0; c < NCH; ++c)
+                for (int c = 0; c < NM; ++c)
 #pragma unroll
                     for (int q = 0; q < 8; ++q) A[t][c][q] = (_Float16)0.0f;
             }
         } else {  // padded row tiles (qt < ntr) hold sentinel rows
-            const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt) * NCH * 64 + l;
+            const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt) * NM * 64 + l;
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) A[t][c] = qp[(size_t)c * 64];
+            for (int c = 0; c < NM; ++c) A[t][c] = qp[(size_t)c * 64];
         }
     }
     float b1[RT][16], b2[RT][16];
@@ -879,10 +893,10 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     for (int t = 0; t < RT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { b1[t][r] = __builtin_inff(); b2[t][r] = __builtin_inff(); }
-    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NCH * 64 + l;
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
     auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NCH; c += W) {
-            const f16x8 *src = bsrc + ((size_t)grp * G * NCH + c) * 64;
+        for (int c = wid; c < G * NM; c += W) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NM + c) * 64;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)src,
                 (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
@@ -909,7 +923,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                 b1[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], vr, -3.40282347e+38f);
             }
     };
-    constexpr int kV = (kIdx ? 48 : 32) * RT / NCH + 1;  // VALU per MFMA slot below
+    constexpr int kV = (kIdx ? 48 : 32) * RT / NX + 1;  // VALU per MFMA slot below
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -917,10 +931,10 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         const int buf = grp & 1;
         if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
         const f16x8 *Bb = Bs + buf * kB + l;
-        f16x8 Bf[2][NCH];
+        f16x8 Bf[2][NM];
         f32x16 acc[2][RT];
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) Bf[0][c] = Bb[c * 64];
+        for (int c = 0; c < NM; ++c) Bf[0][c] = Bb[c * 64];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int cur = g & 1;
@@ -929,19 +943,20 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[cur][t][r] = 0.0f;
 #pragma unroll
-            for (int c = 0; c < NCH; ++c)
+            for (int c = 0; c < NX; ++c)
 #pragma unroll
                 for (int t = 0; t < RT; ++t)
-                    acc[cur][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t][c], Bf[cur][c], acc[cur][t], 0, 0, 0);
+                    acc[cur][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t][amap(c, S)], Bf[cur][bmap(c, S)],
+                                                                         acc[cur][t], 0, 0, 0);
             if (g + 1 < G) {
 #pragma unroll
-                for (int c = 0; c < NCH; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NCH + c) * 64];
+                for (int c = 0; c < NM; ++c) Bf[cur ^ 1][c] = Bb[((g + 1) * NM + c) * 64];
             }
             if (g > 0) epilogue(acc[cur ^ 1], (unsigned)(grp * G + g - 1));
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
+            for (int c = 0; c < NX; ++c) {
                 __builtin_amdgcn_sched_group_barrier(0x008, RT, 0);
-                if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (g + 1 < G && c < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 if (g > 0) __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
             }
             // one scheduling region per tile: the next tile's fragments stay
@@ -991,7 +1006,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             a.nn[o] = mi1;
             const double Gm = (double)__uint_as_float(a.cmax[p]);
             const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
-            const double bnd = bound5(qn, Gm, 16 * NCH, a.D);
+            const double bnd = bound5(qn, Gm, 16 * NX, a.D);
             const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
             a.v[o] = (double)mb1;
             a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
@@ -1127,7 +1142,7 @@ __global__ __launch_bounds__(1024) void featmut_corres(MutArgs a) {
 // packed operands, norms and per-pair maxima of both clouds (shared by the
 // dual screen and the mutual path)
 struct V5Buf {
-    int NCH, W, nrb, ntn, ntm, ctbits;
+    int S, NM, NX, W, nrb, ntn, ntm, ctbits;  // S chunks per D-segment, NM stored, NX executed
     Split5 sp;
     f16x8 *Ap, *Bp;
     float *fnr, *gnr;
@@ -1137,7 +1152,9 @@ struct V5Buf {
 
 static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
                       const int32_t *n_src, const int32_t *n_tgt, hipStream_t s, V5Buf &v) {
-    v.NCH = cdiv(3 * D + 6, 16);
+    v.S = cdiv(D, 16);
+    v.NM = 2 * v.S + 1;
+    v.NX = 3 * v.S + 1;
     v.sp = split5_params(D);
     v.W = 8;                                          // waves (32-row tiles) per workgroup
     v.nrb = cdiv(cdiv(Nmax, 32), v.W);                // dual screen row blocks
@@ -1148,8 +1165,8 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.ctbits = 1;
     while ((1 << v.ctbits) < std::max(v.ntm, v.ntn)) ++v.ctbits;
     PCR_REQUIRE(v.ctbits <= 16, PCR_ERR_ARG, "feature_match: N=%d / M=%d too large", Nmax, Mmax);
-    const int NCH = v.NCH, ntn = v.ntn, ntm = v.ntm;
-    const size_t ap = (size_t)P * ntn * NCH * 64, bp = (size_t)P * ntm * NCH * 64;  // f16x8
+    const int NM = v.NM, ntn = v.ntn, ntm = v.ntm;
+    const size_t ap = (size_t)P * ntn * NM * 64, bp = (size_t)P * ntm * NM * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
         16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax));
@@ -1185,10 +1202,10 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
         PCR_LAUNCH_CHECK();
     } else {
         hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D,
-                           NCH, ntn, 0, v.sp, v.mx, v.Ap, v.fnr, v.fmax);
+                           v.S, ntn, 0, v.sp, v.mx, v.Ap, v.fnr, v.fmax);
         PCR_LAUNCH_CHECK();
         hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax, D,
-                           NCH, ntm, 1, v.sp, v.mx, v.Bp, v.gnr, v.gmax);
+                           v.S, ntm, 1, v.sp, v.mx, v.Bp, v.gnr, v.gmax);
         PCR_LAUNCH_CHECK();
     }
     prof_end(s, kProfFeatPack);
@@ -1247,7 +1264,7 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     V5Buf v;
     int rc = v5_prepare(F, G, P, Nmax, Mmax, D, n_src, n_tgt, s, v);
     if (rc != PCR_OK) return rc;
-    const int NCH = v.NCH, W = v.W, nrb = v.nrb, ntm = v.ntm;
+    const int W = v.W, nrb = v.nrb, ntm = v.ntm;
     DualArgs5 d;
     d.Ap = v.Ap; d.Bp = v.Bp; d.fnr = v.fnr; d.gnr = v.gnr; d.fmax = v.fmax; d.gmax = v.gmax;
     d.n_src = n_src; d.n_tgt = n_tgt; d.P = P; d.Nmax = Nmax; d.Mmax = Mmax; d.ntn = v.ntn;
@@ -1266,15 +1283,13 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_match: grid too large");
     prof_begin(s, kProfFeatScreen);
     {
-        switch (NCH) {
+        switch (v.S) {
 #define PCR_D7CASE(K)                                                                        \
     case K:                                                                                  \
-        hipLaunchKernelGGL((featnn_dual7<K, (K <= 7 ? 8 : 4)>), dim3((unsigned)nblk),          \
+        hipLaunchKernelGGL((featnn_dual7<K, (K <= 2 ? 8 : 4)>), dim3((unsigned)nblk),          \
                            dim3(512), 0, s, d);                                              \
         break;
-            PCR_D7CASE(1) PCR_D7CASE(2) PCR_D7CASE(3) PCR_D7CASE(4) PCR_D7CASE(5) PCR_D7CASE(6)
-            PCR_D7CASE(7) PCR_D7CASE(8) PCR_D7CASE(9) PCR_D7CASE(10) PCR_D7CASE(11) PCR_D7CASE(12)
-            PCR_D7CASE(13)
+            PCR_D7CASE(1) PCR_D7CASE(2) PCR_D7CASE(3) PCR_D7CASE(4)
 #undef PCR_D7CASE
             default: set_error("feature dim too large for the f16 split screen"); return PCR_ERR_ARG;
         }
@@ -1282,7 +1297,7 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
     PCR_LAUNCH_CHECK();
     prof_end(s, kProfFeatScreen);
     hipLaunchKernelGGL(featnn_colmerge5, dim3(cdiv(Mmax, 256), P), dim3(256), 0, s, d, nn21, v.list21,
-                       v.cnt21, 16 * NCH, W);
+                       v.cnt21, 16 * v.NX, W);
     PCR_LAUNCH_CHECK();
     RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
     ra.list12 = v.list12; ra.list21 = v.list21; ra.cnt12 = v.cnt12; ra.cnt21 = v.cnt21;
@@ -1295,18 +1310,16 @@ constexpr int kRowTiles = 2;
 
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
-static int launch_row7(const RowArgs5 &r, int NCH, hipStream_t s) {
+static int launch_row7(const RowArgs5 &r, int S, hipStream_t s) {
     const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_match: grid too large");
-    switch (NCH) {
+    switch (S) {
 #define PCR_R7CASE(K)                                                                            \
     case K:                                                                                      \
-        hipLaunchKernelGGL((featnn_row7<K, (K <= 7 ? 8 : 4), kIdx, kRowTiles>), dim3((unsigned)nblk), \
+        hipLaunchKernelGGL((featnn_row7<K, (K <= 2 ? 8 : 4), kIdx, kRowTiles>), dim3((unsigned)nblk), \
                            dim3(512), 0, s, r);                                                  \
         break;
-        PCR_R7CASE(1) PCR_R7CASE(2) PCR_R7CASE(3) PCR_R7CASE(4) PCR_R7CASE(5) PCR_R7CASE(6)
-        PCR_R7CASE(7) PCR_R7CASE(8) PCR_R7CASE(9) PCR_R7CASE(10) PCR_R7CASE(11) PCR_R7CASE(12)
-        PCR_R7CASE(13)
+        PCR_R7CASE(1) PCR_R7CASE(2) PCR_R7CASE(3) PCR_R7CASE(4)
 #undef PCR_R7CASE
         default: set_error("feature dim too large for the f16 split screen"); return PCR_ERR_ARG;
     }
@@ -1322,7 +1335,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     V5Buf v;
     int rc = v5_prepare(F, G, P, Nmax, Mmax, D, n_src, n_tgt, s, v);
     if (rc != PCR_OK) return rc;
-    const int NCH = v.NCH, ntn = v.ntn, ntm = v.ntm;
+    const int ntn = v.ntn, ntm = v.ntm;
     // scratch: v12 [P][Nmax] f64 | e12 [P][Nmax] f32 | w1, w2 [P][Mmax] f32 | used, pos
     // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P]
     const size_t pn = (size_t)P * Nmax, pm = (size_t)P * Mmax;
@@ -1342,7 +1355,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     int *zero = ma.nj + P;
     PCR_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(int) * (size_t)P, s));
     ma.nn12 = nn12; ma.n_src = n_src; ma.n_tgt = n_tgt; ma.Nmax = Nmax; ma.Mmax = Mmax;
-    ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * NCH; ma.D = D; ma.ntm = ntm;
+    ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * v.NX; ma.D = D; ma.ntm = ntm;
     ma.v12 = v12; ma.e12 = e12; ma.w1 = w1; ma.w2 = w2; ma.gnr = v.gnr; ma.fmax = v.fmax;
     ma.list21 = v.list21; ma.cnt21 = v.cnt21; ma.nn21x = nn21x;
     ma.corres = corres; ma.n_corres = n_corres;
@@ -1355,7 +1368,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;
     prof_begin(s, kProfFeatScreen);
-    rc = launch_row7<true>(r, NCH, s);
+    rc = launch_row7<true>(r, v.S, s);
     if (rc != PCR_OK) return rc;
     prof_end(s, kProfFeatScreen);
     RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
@@ -1376,7 +1389,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
         r2.w1 = w1; r2.w2 = w2;
         prof_begin(s, kProfFeatScreen2);
-        rc = launch_row7<false>(r2, NCH, s);
+        rc = launch_row7<false>(r2, v.S, s);
         if (rc != PCR_OK) return rc;
         prof_end(s, kProfFeatScreen2);
         hipLaunchKernelGGL(featmut_resolve, dim3(cdiv(Nmax, 256), P), dim3(256), 0, s, ma);
