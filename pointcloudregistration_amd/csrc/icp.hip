@@ -8,18 +8,19 @@
 // has fewer pairs than the chip has CUs.  Each workgroup holds the pair's target
 // hash grid in LDS.
 //  * The f64 working copy (transformed in place every iteration, as Open3D's
-//    Transform does) and the correspondences (target xyz + index, one float4)
-//    are stored by source index; the sweep takes 64-query chunks of the spatial
-//    (Morton-of-cell) order from a counter.
-//  * Per iteration: every point is queried in the grid (radius-limited 1-NN),
-//    then ONE pass sums the Umeyama terms of the inliers -- s - c0, t - c0 and
-//    their 9 products, each truncated to a multiple of a per-pair quantum 2^-k
-//    small enough that every partial sum is an integer multiple of 2^-k below
-//    2^52 (oracle_icp_quantum): the f64 additions are then exact, so any split
-//    over threads, waves and workgroups gives the same bits, and the means and
-//    the cross-covariance (C = Sst - ms' St^T) come out of one pass and one
-//    reduction; Horn's quaternion solve and the T <- U*T update run
-//    redundantly in every workgroup on the same totals.
+//    Transform does) is stored by source index; the sweep takes 64-query chunks
+//    of the spatial (Morton-of-cell) order from a counter.
+//  * Per iteration ONE sweep: every point is transformed by the last update,
+//    queried in the grid (radius-limited 1-NN), and -- if it has a
+//    correspondence -- its Umeyama terms are added to the thread's sums right
+//    there: s - c0, t - c0 and their 9 products, each truncated to a multiple of
+//    a per-pair quantum 2^-k small enough that every partial sum is an integer
+//    multiple of 2^-k below 2^52 (oracle_icp_quantum).  The f64 additions are
+//    then exact, so any split over threads, waves and workgroups gives the same
+//    bits; the means and the cross-covariance (C = Sst - ms' St^T) come out of
+//    the sweep and one reduction, with no correspondence array written or
+//    re-read.  Horn's quaternion solve and the T <- U*T update run redundantly
+//    in every workgroup on the same totals.
 #include "pcr_internal.h"
 #include "coop.h"
 #include "geom.h"
@@ -51,7 +52,6 @@ struct IArgs {
     int max_iter;
     GridBatch grid;
     double *P3;          // P x Nmax x 3 working copy by source index
-    float4 *tq;          // P x Nmax correspondence per source point: target xyz, index bits
     double *T_out, *fit_out;
     int32_t *stats;
     int32_t *corr_tgt;   // optional (P, Nmax): final correspondence per source point
@@ -59,7 +59,7 @@ struct IArgs {
     int G;
     XPart *part;         // (P, 2, G) when G > 1
     unsigned *bar;       // (P, 2) when G > 1
-    int *chunk;          // (P) sweep chunk counters, when G > 1
+    int *chunk;          // (P, 2) sweep chunk counters by sweep parity, when G > 1
     unsigned long long *timing;  // debug (PCR_ICP_TIMING): per pair, phase clocks
 };
 
@@ -82,7 +82,7 @@ struct IShared {  // LDS header; the grid copy (if any) follows
     double T[16];     // the running transformation (init, then U * T per iteration)
     double U[12];     // this iteration's update
     int nred;         // reductions done (parity of the HBM partial slots)
-    int chunk;        // next 64-position chunk of the current sweep (G = 1)
+    int chunk[2];     // next 64-position chunk of the current sweep, by parity (G = 1)
 };
 
 // wave-level sums of NQ exact f64 values (integer multiples of the quantum:
@@ -167,12 +167,11 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const float *S = a.src + (size_t)p * a.Nmax * 3;
     const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
-    // working copy (f64 xyz) and correspondence (target xyz + index in one
-    // float4), both by source INDEX, AoS: one cache line per point in the sweep
+    // working copy (f64 xyz) by source INDEX, AoS
     double *P3 = a.P3 + (size_t)p * a.Nmax * 3;
-    float4 *TQ = a.tq + (size_t)p * a.Nmax;
+    int32_t *CT = a.corr_tgt ? a.corr_tgt + (size_t)p * a.Nmax : nullptr;
     if (tid < 16) sh.T[tid] = a.init[(size_t)p * 16 + tid];
-    if (tid == 0) { sh.nred = 0; sh.chunk = 0; }
+    if (tid == 0) { sh.nred = 0; sh.chunk[0] = 0; sh.chunk[1] = 0; }
     __syncthreads();
     const bool valid = a.d > 0.0 && n > 0 && m > 0;
     bool ident = true;
@@ -253,13 +252,19 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     // with_u: this iteration's update U is applied to the working copy inside
     // the sweep (each point read, transformed, written back and queried by the
     // same thread), which saves the separate transform pass and a pair barrier
+    int nsweep = 0;  // sweeps done: parity of the chunk counters
     auto evaluate = [&](bool with_u) {
         unsigned long long acc = 0;
         int cnt = 0;
+        double v[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) v[q] = 0.0;
         {  // 64-query chunks of the spatial order taken from a counter (dense and
-           // sparse regions cost different time)
-            int *ctr = G > 1 ? a.chunk + p : &sh.chunk;
+           // sparse regions cost different time); the counter of this sweep's
+           // parity was re-armed after the previous sweep's reduction
+            int *ctr = G > 1 ? a.chunk + 2 * p + (nsweep & 1) : &sh.chunk[nsweep & 1];
             const int nch = (n + 63) >> 6;
+            const double c0x = sh.c0[0], c0y = sh.c0[1], c0z = sh.c0[2];
             for (;;) {
                 int c = 0;
                 if (lane == 0) c = G > 1 ? coop_fetch_add(ctr, 1) : atomicAdd(ctr, 1);
@@ -287,48 +292,40 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                         if (q >= 0) { float w; gl.load(s, qx, qy, qz, w); }
                     } else {
                         q = grid_query<GridView, true>(gg, a.d, a.thr, x, y, z, d2, &s);
-                        if (q >= 0) { qx = gg.x[s]; qy = gg.y[s]; qz = gg.z[s]; }
+                        if (q >= 0) { float w; gg.load(s, qx, qy, qz, w); }
                     }
-                    TQ[i] = make_float4(qx, qy, qz, __int_as_float(q));
+                    if (CT) CT[i] = q;
                     if (q >= 0) {
                         ++cnt;
                         acc += (unsigned long long)(d2 * scale);
+                        // the exact Umeyama terms of this correspondence
+                        const volatile double *skv = &sh.sk;
+                        const double sk = skv[0], isk = skv[1];
+                        const double sp[3] = {x - c0x, y - c0y, z - c0z};
+                        const double tp[3] = {(double)qx - c0x, (double)qy - c0y, (double)qz - c0z};
+#pragma unroll
+                        for (int cc = 0; cc < 3; ++cc) {
+                            v[cc] = v[cc] + __builtin_trunc(sp[cc] * sk) * isk;
+                            v[3 + cc] = v[3 + cc] + __builtin_trunc(tp[cc] * sk) * isk;
+#pragma unroll
+                            for (int e = 0; e < 3; ++e)
+                                v[6 + 3 * cc + e] = v[6 + 3 * cc + e] + __builtin_trunc((sp[cc] * tp[e]) * sk) * isk;
+                        }
                     }
                 }
             }
         }
-        // every correspondence written; the counter is re-armed for the next sweep
-        // (which comes after at least two more barriers)
-        sync_pair();
-        if (tid == 0 && g == 0) {
-            if (G > 1) __hip_atomic_store(a.chunk + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else sh.chunk = 0;
-        }
         mark(0);
-        {  // the exact Umeyama sums of the inliers, any point to any thread
-            double v[kQ];
-#pragma unroll
-            for (int q = 0; q < kQ; ++q) v[q] = 0.0;
-            const double c0x = sh.c0[0], c0y = sh.c0[1], c0z = sh.c0[2];
-            const double sk = sh.sk, isk = sh.isk;
-#pragma unroll 1
-            for (int i = base; i < n; i += stride) {
-                const float4 t = TQ[i];
-                if (__float_as_int(t.w) < 0) continue;
-                const double sp[3] = {P3[3 * i] - c0x, P3[3 * i + 1] - c0y, P3[3 * i + 2] - c0z};
-                const double tp[3] = {(double)t.x - c0x, (double)t.y - c0y, (double)t.z - c0z};
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    v[c] = v[c] + __builtin_trunc(sp[c] * sk) * isk;
-                    v[3 + c] = v[3 + c] + __builtin_trunc(tp[c] * sk) * isk;
-#pragma unroll
-                    for (int e = 0; e < 3; ++e)
-                        v[6 + 3 * c + e] = v[6 + 3 * c + e] + __builtin_trunc((sp[c] * tp[e]) * sk) * isk;
-                }
-            }
-            wave_park<kQ>(sh, v);
-        }
+        wave_park<kQ>(sh, v);
         pair_reduce<kQ>(a, sh, p, g, cnt, acc);
+        // every workgroup has left this sweep (pair_reduce's barrier): re-arm its
+        // counter for the sweep after next (the next sweep uses the other one,
+        // re-armed one reduction ago)
+        if (tid == 0 && g == 0) {
+            if (G > 1) __hip_atomic_store(a.chunk + 2 * p + (nsweep & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else sh.chunk[nsweep & 1] = 0;
+        }
+        ++nsweep;
         mark(1);
         count = sh.cnt;
         if (count > 0) {
@@ -384,9 +381,8 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             if (__builtin_fabs(pf - fit) < a.rel_fit && __builtin_fabs(pr - rmse) < a.rel_rmse) break;
         }
     }
-    if (a.corr_tgt) {
-        int32_t *ct = a.corr_tgt + (size_t)p * a.Nmax;
-        for (int i = base; i < a.Nmax; i += stride) ct[i] = (valid && i < n) ? __float_as_int(TQ[i].w) : -1;
+    if (CT) {  // the last sweep wrote CT[0, n) when valid
+        for (int i = valid ? n + base : base; i < a.Nmax; i += stride) CT[i] = -1;
     }
     if (g == 0 && tid == 0) {
         for (int k = 0; k < 16; ++k) a.T_out[(size_t)p * 16 + k] = sh.T[k];
@@ -422,7 +418,6 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     a.rel_rmse = prm->relative_rmse;
     a.max_iter = prm->max_iteration;
     a.P3 = nullptr;
-    a.tq = nullptr;
     if (a.d > 0.0) {
         int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
         if (rc != PCR_OK) return rc;
@@ -451,19 +446,18 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     // workgroups their cost outgrows the split sweep (32-pair shard: G = 4
     // 0.80 ms, G = 8 0.97 ms; RANSAC, two barriers per sweep, is best at 8)
     a.G = coop_groups(P, per_cu, 4);
-    // working copy and correspondences, by position
+    // working copy, by position
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
-    char *ws = (char *)workspace(8, (sizeof(double) * 3 + sizeof(float4)) * (size_t)P * nm + 64);
+    char *ws = (char *)workspace(8, sizeof(double) * 3 * (size_t)P * nm + 64);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
     a.P3 = (double *)ws;
-    a.tq = (float4 *)(ws + sizeof(double) * 3 * (size_t)P * nm);
     if (a.G > 1) {
-        char *cw = (char *)workspace(10, (sizeof(XPart) * 2 * (size_t)a.G + sizeof(unsigned) * 3) * (size_t)P + 64);
+        char *cw = (char *)workspace(10, (sizeof(XPart) * 2 * (size_t)a.G + sizeof(unsigned) * 4) * (size_t)P + 64);
         PCR_REQUIRE(cw, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
         a.part = (XPart *)cw;
         a.bar = (unsigned *)(cw + sizeof(XPart) * 2 * (size_t)a.G * (size_t)P);
         a.chunk = (int *)(a.bar + 2 * (size_t)P);
-        PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 3 * (size_t)P, s));
+        PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 4 * (size_t)P, s));
     } else {
         a.part = nullptr;
         a.bar = nullptr;
