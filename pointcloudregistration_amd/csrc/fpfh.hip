@@ -203,8 +203,9 @@ __global__ __launch_bounds__(64) void hybrid_search_kernel(SearchArgs a) {
                 int j = 0;
                 bool pass = false;
                 if (s < s1) {
-                    d = dist2(px, py, pz, (double)g.x[s], (double)g.y[s], (double)g.z[s]);
-                    j = (int)g.idx[s];
+                    const float4 c = g.pts[s];
+                    d = dist2(px, py, pz, (double)c.x, (double)c.y, (double)c.z);
+                    j = __float_as_int(c.w);
                     pass = d < a.thr;
                 }
                 offer(pass, d, j);

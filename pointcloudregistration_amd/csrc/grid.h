@@ -2,7 +2,7 @@
 // (Open3D KDTreeFlann::SearchHybrid(r, 1) semantics: nearest target with
 // d2 < thr strictly, lowest index on exact ties).
 //
-// HBM layout per pair (SoA): x/y/z [mstride] f32 and idx [mstride] u32 sorted by
+// HBM layout per pair: pts [mstride] float4 (x, y, z, index bits) sorted by
 // slot, start [S+1] u32 slot offsets.  Cells are 2.01*r wide, so a query ball
 // touches at most 2x2x2 cells.  Hash collisions only add candidates; the exact
 // distance test decides, so results are independent of slot order and equal to
@@ -24,21 +24,20 @@ __device__ __forceinline__ unsigned cell_hash(int x, int y, int z, int S) {
            (unsigned)(S - 1);
 }
 
-// generic view: IdxT = uint32_t (HBM) or uint16_t (LDS copy)
-template <typename IdxT>
-struct GridT {
-    const float *x, *y, *z;
-    const IdxT *idx;
-    const IdxT *start;
+// view of one pair's grid in HBM: one float4 per point (x, y, z, index bits)
+struct GridView {
+    const float4 *pts;
+    const uint32_t *start;
     int S;
     double cell;
     double inv_cell;  // queries use v * inv_cell: the 1.001 r margin covers the rounding
     // candidate access shared with GridP4: coordinates of slot s, then (only for
     // candidates inside the radius) its point index
     __device__ __forceinline__ void load(int s, float &ax, float &ay, float &az, float &aw) const {
-        ax = x[s]; ay = y[s]; az = z[s]; aw = 0.0f;
+        const float4 v = pts[s];
+        ax = v.x; ay = v.y; az = v.z; aw = v.w;
     }
-    __device__ __forceinline__ int index_of(int s, float) const { return (int)idx[s]; }
+    __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
 };
 
 // LDS copy for the consumers that own a pair (RANSAC, ICP): one float4 per
@@ -57,7 +56,6 @@ struct GridP4 {
     }
     __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
 };
-using GridView = GridT<uint32_t>;
 
 // squared distance from p to cell c's box [c*cell, (c+1)*cell] along one axis,
 // the box grown by a relative 1e-12 (the build assigns cells by floor(v / cell):
@@ -211,15 +209,13 @@ __device__ __forceinline__ int grid_query(const View &g, double r, double thr, d
 
 // Grids for P target clouds (device, workspace-backed; see grid.hip).
 struct GridBatch {
-    float *x, *y, *z;   // P * mstride
-    uint32_t *idx;      // P * mstride
+    float4 *pts;        // P * mstride: x, y, z, index bits
     uint32_t *start;    // P * (S+1)
     int S;
     int mstride;
     double cell;
     __device__ GridView view(int p) const {
-        const size_t o = (size_t)p * mstride;
-        return GridView{x + o, y + o, z + o, idx + o, start + (size_t)p * (S + 1), S, cell, 1.0 / cell};
+        return GridView{pts + (size_t)p * mstride, start + (size_t)p * (S + 1), S, cell, 1.0 / cell};
     }
 };
 
@@ -237,8 +233,7 @@ __device__ inline GridP4 grid_to_lds4(const GridBatch &gb, int p, int m, char *l
     const size_t o = (size_t)p * gb.mstride;
     float4 *lp = (float4 *)lds;
     uint16_t *ls = (uint16_t *)(lp + gb.mstride);
-    for (int i = threadIdx.x; i < m; i += blockDim.x)
-        lp[i] = make_float4(gb.x[o + i], gb.y[o + i], gb.z[o + i], __int_as_float((int)gb.idx[o + i]));
+    for (int i = threadIdx.x; i < m; i += blockDim.x) lp[i] = gb.pts[o + i];
     const uint32_t *st = gb.start + (size_t)p * (gb.S + 1);
     for (int i = threadIdx.x; i <= gb.S; i += blockDim.x) ls[i] = (uint16_t)st[i];
     __syncthreads();

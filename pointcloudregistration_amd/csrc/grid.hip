@@ -14,8 +14,7 @@ struct BuildArgs {
     double cell;
     int *cnt;      // P*S
     int *start;    // P*(S+1)
-    float *x, *y, *z;
-    uint32_t *idx; // P*Mmax each
+    float4 *pts;   // P*Mmax: x, y, z, index bits (one 16-B store per point)
 };
 
 __device__ __forceinline__ int count_of(const int32_t *n, int p, int Mmax) {
@@ -45,11 +44,7 @@ __global__ void grid_scatter(BuildArgs a) {
     const unsigned h = cell_hash(cell_coord((double)q[0], a.cell), cell_coord((double)q[1], a.cell),
                                  cell_coord((double)q[2], a.cell), a.S);
     const int pos = a.start[(size_t)p * (a.S + 1) + h] + atomicAdd(a.cnt + (size_t)p * a.S + h, 1);
-    const size_t o = (size_t)p * a.Mmax + pos;
-    a.x[o] = q[0];
-    a.y[o] = q[1];
-    a.z[o] = q[2];
-    a.idx[o] = (uint32_t)j;
+    a.pts[(size_t)p * a.Mmax + pos] = make_float4(q[0], q[1], q[2], __int_as_float(j));
 }
 
 // count, scan and scatter of one pair's grid in one workgroup, the slot
@@ -79,11 +74,7 @@ __global__ __launch_bounds__(1024) void grid_build_lds(BuildArgs a) {
         const float x = q[3 * j], y = q[3 * j + 1], z = q[3 * j + 2];
         const unsigned h = cell_hash(cell_coord((double)x, a.cell), cell_coord((double)y, a.cell),
                                      cell_coord((double)z, a.cell), S);
-        const size_t o = (size_t)p * a.Mmax + atomicAdd(&cnt[h], 1);
-        a.x[o] = x;
-        a.y[o] = y;
-        a.z[o] = z;
-        a.idx[o] = (uint32_t)j;
+        a.pts[(size_t)p * a.Mmax + atomicAdd(&cnt[h], 1)] = make_float4(x, y, z, __int_as_float(j));
     }
 }
 
@@ -216,11 +207,7 @@ int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double 
     a.cnt = (int *)ws;
     a.start = (int *)(ws + cnt_b);
     size_t off = (cnt_b + start_b + 15) & ~size_t(15);
-    const size_t pm = (size_t)P * (Mmax > 0 ? Mmax : 1);
-    a.x = (float *)(ws + off);
-    a.y = a.x + pm;
-    a.z = a.y + pm;
-    a.idx = (uint32_t *)(a.z + pm);
+    a.pts = (float4 *)(ws + off);
     if (S <= kLdsSlots) {
         PCR_HIP_CHECK(hipFuncSetAttribute((const void *)grid_build_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)(sizeof(int) * (kLdsSlots + 1))));
@@ -236,10 +223,7 @@ int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double 
         hipLaunchKernelGGL(grid_scatter, g, dim3(256), 0, s, a);
         PCR_LAUNCH_CHECK();
     }
-    out.x = a.x;
-    out.y = a.y;
-    out.z = a.z;
-    out.idx = a.idx;
+    out.pts = a.pts;
     out.start = (uint32_t *)a.start;
     out.S = S;
     out.mstride = Mmax;
