@@ -468,6 +468,10 @@ typedef struct pcr_ndp_train {
     const int32_t *inv;
     float *xs;
     const float *gsub;
+    /* optional (null = off): the subset gradient as pcr_ndp_chamfer_step leaves
+     * it -- gacc[0] nonzero = a non-finite term, gacc[1 + 3k + c] = dL/dxs[k][c]
+     * in 2^-44 fixed point; read instead of gsub */
+    const long long *gacc;
 } pcr_ndp_train;
 int pcr_ndp_train_forward(const pcr_ndp_train *t, pcr_stream_t stream);
 int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32_t chunk,
@@ -477,12 +481,39 @@ int64_t pcr_ndp_train_partial_floats(int32_t N, int32_t width, int32_t depth, in
  *   pass, on the device, in a fixed reduction order:
  *   loss = sum(d1')/K + sum(d2')/M (+ w_reg * mean(-max(log(1 - s), -100)) when s
  *   is given), d' = d where d < trunc else 0; gd1 = 1/K and gd2 = 1/M where not
- *   truncated, else 0 (the dist gradients for pcr_nnd_backward);
+ *   truncated, else 0 (the dist gradients for pcr_nnd_backward; gd1 / gd2 may be
+ *   null);
  *   log[min(*ctr, log_last)] = loss; ++*ctr (device int64). */
 int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
                          const float *s, int32_t N, double w_reg, double trunc,
                          float *gd1, float *gd2, float *loss, float *log, int64_t *ctr,
                          int32_t log_last, pcr_stream_t stream);
+
+/* pcr_ndp_chamfer_*: the level's Chamfer pass with its gradient, specialised
+ *   for the loop (csrc/ndp_chamfer.hip).  xs (K,3) = x_out[inds] (written by
+ *   pcr_ndp_train_forward through inv), tgt (M,3) fixed for the level.
+ *   d1/i1 (K), d2/i2 (M): pcr_nnd_forward's outputs bit for bit.  gacc (1 + 3K
+ *   int64): the gradient of sum(d1')/K + sum(d2')/M w.r.t. xs (d' = d where
+ *   d < trunc, else 0) in 2^-44 fixed point, gacc[0] != 0 when a term was not
+ *   finite -- consumed by pcr_ndp_train_backward (pcr_ndp_train.gacc).
+ *   scratch: pcr_ndp_chamfer_scratch_bytes(K, M) bytes, 256-byte aligned,
+ *   owned by the caller for the level.
+ * pcr_ndp_chamfer_prepare: the target grid and the subset cell (from xs0, the
+ *   level's input subset); once per level, outside the captured graph.
+ * pcr_ndp_chamfer_step: one iteration (gated like the other f4 launches). */
+typedef struct pcr_ndp_chamfer {
+    const float *xs;
+    const float *tgt;
+    int32_t K, M;
+    double trunc;
+    float *d1, *d2;
+    int32_t *i1, *i2;
+    long long *gacc;
+    void *scratch;
+} pcr_ndp_chamfer;
+int64_t pcr_ndp_chamfer_scratch_bytes(int32_t K, int32_t M);
+int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs0, pcr_stream_t stream);
+int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,7 @@ struct TrainArgs {
     const int32_t *inv;
     float *xs;
     const float *gsub;
+    const long long *gacc;          // or: the subset gradient in 2^-44 fixed point (ndp_chamfer.hip)
     const double *gate;             // f4 early stop (pcr_internal.h), or null
 };
 
@@ -191,7 +192,13 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
     if (valid) {
         const float x[3] = {a.x[3 * pt], a.x[3 * pt + 1], a.x[3 * pt + 2]};
         float g[3];
-        if (a.inv) {
+        if (a.inv && a.gacc) {
+            const int k = a.inv[pt];
+            const float bad = a.gacc[0] ? __builtin_nanf("") : 0.0f;
+            constexpr double kInv = 1.0 / 17592186044416.0;  // 2^-44
+#pragma unroll
+            for (int c = 0; c < 3; ++c) g[c] = k >= 0 ? (float)((double)a.gacc[1 + 3 * k + c] * kInv) + bad : 0.0f;
+        } else if (a.inv) {
             const int k = a.inv[pt];
             g[0] = k >= 0 ? a.gsub[3 * k] : 0.0f;
             g[1] = k >= 0 ? a.gsub[3 * k + 1] : 0.0f;
@@ -410,13 +417,13 @@ __global__ __launch_bounds__(1024) void ndp_chamfer_glue(GlueArgs a) {
         const float d = a.d1[i];
         const bool in = !(d >= a.trunc);  // torch.where(d >= trunc, 0, d): NaN stays
         s1 += in ? d : 0.0f;
-        a.gd1[i] = in ? a.g1 : 0.0f;
+        if (a.gd1) a.gd1[i] = in ? a.g1 : 0.0f;
     }
     for (int i = t; i < a.M; i += 1024) {
         const float d = a.d2[i];
         const bool in = !(d >= a.trunc);
         s2 += in ? d : 0.0f;
-        a.gd2[i] = in ? a.g2 : 0.0f;
+        if (a.gd2) a.gd2[i] = in ? a.g2 : 0.0f;
     }
     if (a.s)
         for (int i = t; i < a.N; i += 1024) {
@@ -467,7 +474,7 @@ static int fill_train(const pcr_ndp_train *t, pcr::TrainArgs &a) {
     a.w_nr = L.w_nr; a.b_nr = L.b_nr;
     a.pe = t->pe; a.H = t->H; a.aux = t->aux; a.x_out = t->x_out;
     a.g = t->g; a.bce_scale = t->bce_scale; a.dO = t->dO; a.D = t->D;
-    a.inv = t->inv; a.xs = t->xs; a.gsub = t->gsub;
+    a.inv = t->inv; a.xs = t->xs; a.gsub = t->gsub; a.gacc = t->gacc;
     a.gate = pcr::current_gate();
     return PCR_OK;
 }
@@ -493,7 +500,7 @@ extern "C" int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32
     int rc = fill_train(t, a);
     if (rc != PCR_OK) return rc;
     if (a.N == 0) return PCR_OK;
-    PCR_REQUIRE((a.inv ? a.gsub != nullptr : a.g != nullptr) && a.dO && a.D && part && grads, PCR_ERR_ARG,
+    PCR_REQUIRE((a.inv ? (a.gsub != nullptr || a.gacc != nullptr) : a.g != nullptr) && a.dO && a.D && part && grads, PCR_ERR_ARG,
                 "ndp_train_backward: null buffer");
     PCR_REQUIRE(chunk >= 64 && chunk % 64 == 0, PCR_ERR_ARG, "ndp_train_backward: chunk %d", chunk);
     hipStream_t s = pcr::as_stream(stream);
@@ -539,7 +546,7 @@ extern "C" int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2,
                                     int32_t log_last, pcr_stream_t stream) {
     pcr::clear_error();
     PCR_REQUIRE(K >= 0 && M >= 0 && N >= 0 && log_last >= 0, PCR_ERR_ARG, "ndp_chamfer_glue: negative size");
-    PCR_REQUIRE((K == 0 || (d1 && gd1)) && (M == 0 || (d2 && gd2)) && loss && log && ctr, PCR_ERR_ARG,
+    PCR_REQUIRE((K == 0 || d1) && (M == 0 || d2) && loss && log && ctr, PCR_ERR_ARG,
                 "ndp_chamfer_glue: null buffer");
     pcr::GlueArgs g{d1, d2, s, K, M, N, log_last, (float)trunc, (float)w_reg,
                     (float)(1.0 / (double)K), (float)(1.0 / (double)M), gd1, gd2, loss, log,

@@ -22,6 +22,7 @@
 // served from one XCD's L2.
 #include "pcr_internal.h"
 #include "scan.h"
+#include "nng.h"
 #include <cstdlib>
 
 namespace pcr {
@@ -43,12 +44,9 @@ struct NgArgs {
     const double *gate;   // f4 early stop (pcr_internal.h), or null
 };
 
-__device__ __forceinline__ unsigned nhash(int x, int y, int z, int S) {
-    return (((unsigned)x * 73856093u) ^ ((unsigned)y * 19349663u) ^ ((unsigned)z * 83492791u)) &
-           (unsigned)(S - 1);
-}
-
-__device__ __forceinline__ int ccoord(float v, double ic) { return (int)__builtin_floor((double)v * ic); }
+using nng::ccoord;
+using nng::d2f;
+using nng::nhash;
 
 __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
     if (gated_off(a.gate)) return;
@@ -161,11 +159,6 @@ __global__ __launch_bounds__(1024) void nng_build(NgArgs a) {
     }
 }
 
-__device__ __forceinline__ float d2f(float cx, float cy, float cz, float qx, float qy, float qz) {
-    const float dx = cx - qx, dy = cy - qy, dz = cz - qz;
-    return (dx * dx + dy * dy) + dz * dz;
-}
-
 // XCD-aware block order: the hardware deals linear block ids round-robin over
 // the 8 XCDs; the k-th block an XCD receives takes the k-th slot of that XCD's
 // contiguous range of (direction, pair, chunk) work, so every grid is read by
@@ -233,42 +226,9 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
     }
     if (!done) {
         const size_t g = (size_t)gs * a.B + b;
-        const float cellf = a.cell[g];
-        const double cell = (double)cellf, ic = 1.0 / cell;
-        const int cx = ccoord(qx, ic), cy = ccoord(qy, ic), cz = ccoord(qz, ic);
-        const int *st = a.start + g * (a.S + 1);
-        const float4 *pts = a.pts + g * a.nmax;
-        const double margin = 1e-6 * (fabs((double)qx) + fabs((double)qy) + fabs((double)qz) + cell);
-        auto scan_cell = [&](int x, int y, int z) {
-            const unsigned h = nhash(x, y, z, a.S);
-            const int s1 = st[h + 1];
-            for (int s = st[h]; s < s1; ++s) {
-                const float4 p = pts[s];
-                const float d = d2f(p.x, p.y, p.z, qx, qy, qz);
-                const int j = __float_as_int(p.w);
-                if (d < best || (d == best && j < bj)) { best = d; bj = j; }
-            }
-        };
-        for (int k = 0; k <= kMaxRing && !done; ++k) {
-            // column c = (dx, dy) of ring k; lane sub takes columns sub, sub + LPQ, ...
-            const int side = 2 * k + 1;
-            for (int c = sub; c < side * side; c += LPQ) {
-                const int cq = c / side, dx = cq - k, dy = c - cq * side - k;
-                if (dx == -k || dx == k || dy == -k || dy == k) {
-                    for (int dz = -k; dz <= k; ++dz) scan_cell(cx + dx, cy + dy, cz + dz);
-                } else {
-                    scan_cell(cx + dx, cy + dy, cz - k);
-                    scan_cell(cx + dx, cy + dy, cz + k);
-                }
-            }
-            merge();
-            // distance from q to the faces of the visited (2k+1)^3 block
-            const double gx = fmin((double)qx - (double)(cx - k) * cell, (double)(cx + k + 1) * cell - (double)qx);
-            const double gy = fmin((double)qy - (double)(cy - k) * cell, (double)(cy + k + 1) * cell - (double)qy);
-            const double gz = fmin((double)qz - (double)(cz - k) * cell, (double)(cz + k + 1) * cell - (double)qz);
-            const double gmin = fmin(gx, fmin(gy, gz)) - margin;
-            if (gmin > 0.0 && gmin * gmin * (1.0 - 8.0 * 5.9604644775390625e-08) > (double)best) done = true;
-        }
+        const nng::View v{a.cell[g], a.S, a.start + g * (a.S + 1), a.pts + g * a.nmax};
+        const float4 *pts = v.pts;
+        done = nng::ring_walk<LPQ>(v, qx, qy, qz, sub, kMaxRing, best, bj);
         if (!done) {  // not certified within kMaxRing rings: every candidate, read
                       // as the grid's float4 (x, y, z, index) copy (one 16-B load each)
 #pragma unroll 4

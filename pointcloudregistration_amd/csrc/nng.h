@@ -1,0 +1,92 @@
+// Device helpers of the certified grid 1-NN (a1), shared by the nnd drop-in
+// (nnd_grid.hip) and the NDP level Chamfer (ndp_chamfer.hip).
+//
+// Contract (my_lib.cpp:3-25): the candidate minimising d = (dx*dx + dy*dy) +
+// dz*dz in f32 (dx = c - q, no FMA), lowest index on ties: for finite inputs
+// the lexicographic minimum of (d, j), which any search over a superset of the
+// winners returns unchanged.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace pcr {
+namespace nng {
+
+__device__ __forceinline__ unsigned nhash(int x, int y, int z, int S) {
+    return (((unsigned)x * 73856093u) ^ ((unsigned)y * 19349663u) ^ ((unsigned)z * 83492791u)) &
+           (unsigned)(S - 1);
+}
+
+__device__ __forceinline__ int ccoord(float v, double ic) { return (int)__builtin_floor((double)v * ic); }
+
+__device__ __forceinline__ float d2f(float cx, float cy, float cz, float qx, float qy, float qz) {
+    const float dx = cx - qx, dy = cy - qy, dz = cz - qz;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+// (d, j) lexicographic update
+__device__ __forceinline__ void take(float d, int j, float &best, int &bj) {
+    if (d < best || (d == best && j < bj)) { best = d; bj = j; }
+}
+
+// a grid view: cell edge, S hash slots, slot starts (S + 1), float4 (x, y, z,
+// index bits) points sorted by slot
+struct View {
+    float cell;
+    int S;
+    const int *start;
+    const float4 *pts;
+};
+
+// Chebyshev rings k = 0..kmax around q's cell; the LPQ lanes of a query split
+// each ring's (dx, dy) columns and merge their minima before every
+// certification test.  After ring k every unvisited point is at least g (the
+// distance from q to the faces of the (2k+1)^3 block, minus a 1e-6 relative
+// margin) away, and its computed f32 distance at least g^2 (1 - 8 * 2^-24)
+// (five relative f32 roundings); strictly above the best: final.  Returns
+// whether the answer was certified.
+template <int LPQ>
+__device__ __forceinline__ bool ring_walk(const View &v, float qx, float qy, float qz, int sub, int kmax,
+                                          float &best, int &bj) {
+    auto merge = [&]() {
+#pragma unroll
+        for (int o = 1; o < LPQ; o <<= 1) {
+            const float ob = __shfl_xor(best, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            take(ob, oj, best, bj);
+        }
+    };
+    const double cell = (double)v.cell, ic = 1.0 / cell;
+    const int cx = ccoord(qx, ic), cy = ccoord(qy, ic), cz = ccoord(qz, ic);
+    const double margin = 1e-6 * (fabs((double)qx) + fabs((double)qy) + fabs((double)qz) + cell);
+    auto scan_cell = [&](int x, int y, int z) {
+        const unsigned h = nhash(x, y, z, v.S);
+        const int s1 = v.start[h + 1];
+        for (int s = v.start[h]; s < s1; ++s) {
+            const float4 p = v.pts[s];
+            take(d2f(p.x, p.y, p.z, qx, qy, qz), __float_as_int(p.w), best, bj);
+        }
+    };
+    for (int k = 0; k <= kmax; ++k) {
+        // column c = (dx, dy) of ring k; lane sub takes columns sub, sub + LPQ, ...
+        const int side = 2 * k + 1;
+        for (int c = sub; c < side * side; c += LPQ) {
+            const int cq = c / side, dx = cq - k, dy = c - cq * side - k;
+            if (dx == -k || dx == k || dy == -k || dy == k) {
+                for (int dz = -k; dz <= k; ++dz) scan_cell(cx + dx, cy + dy, cz + dz);
+            } else {
+                scan_cell(cx + dx, cy + dy, cz - k);
+                scan_cell(cx + dx, cy + dy, cz + k);
+            }
+        }
+        merge();
+        const double gx = fmin((double)qx - (double)(cx - k) * cell, (double)(cx + k + 1) * cell - (double)qx);
+        const double gy = fmin((double)qy - (double)(cy - k) * cell, (double)(cy + k + 1) * cell - (double)qy);
+        const double gz = fmin((double)qz - (double)(cz - k) * cell, (double)(cz + k + 1) * cell - (double)qz);
+        const double gmin = fmin(gx, fmin(gy, gz)) - margin;
+        if (gmin > 0.0 && gmin * gmin * (1.0 - 8.0 * 5.9604644775390625e-08) > (double)best) return true;
+    }
+    return false;
+}
+
+}  // namespace nng
+}  // namespace pcr

@@ -25,6 +25,7 @@ configuration, config/NDP.yaml).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -267,7 +268,16 @@ class _TrainC(ctypes.Structure):
                 ("pe", ctypes.c_void_p), ("H", ctypes.c_void_p), ("aux", ctypes.c_void_p),
                 ("x_out", ctypes.c_void_p), ("g", ctypes.c_void_p), ("bce_scale", ctypes.c_double),
                 ("dO", ctypes.c_void_p), ("D", ctypes.c_void_p),
-                ("inv", ctypes.c_void_p), ("xs", ctypes.c_void_p), ("gsub", ctypes.c_void_p)]
+                ("inv", ctypes.c_void_p), ("xs", ctypes.c_void_p), ("gsub", ctypes.c_void_p),
+                ("gacc", ctypes.c_void_p)]
+
+
+class _ChamferC(ctypes.Structure):
+    """pcr_ndp_chamfer (include/pcr_api.h)."""
+    _fields_ = [("xs", ctypes.c_void_p), ("tgt", ctypes.c_void_p), ("K", ctypes.c_int32),
+                ("M", ctypes.c_int32), ("trunc", ctypes.c_double), ("d1", ctypes.c_void_p),
+                ("d2", ctypes.c_void_p), ("i1", ctypes.c_void_p), ("i2", ctypes.c_void_p),
+                ("gacc", ctypes.c_void_p), ("scratch", ctypes.c_void_p)]
 
 
 class _LevelFused(_Level):
@@ -352,6 +362,25 @@ class _LevelFused(_Level):
             self.inv[inds] = torch.arange(K, dtype=torch.int32, device=dev)
             self.xs = torch.zeros(1, K, 3, **f32)
             t.inv, t.xs, t.gsub = self.inv.data_ptr(), self.xs.data_ptr(), self.gsub.data_ptr()
+        # the level's Chamfer with its gradient in one pass (csrc/ndp_chamfer.hip):
+        # the target grid built once here, the subset grid rebuilt per iteration
+        self.use_nc = self.use_inv and K >= 1 and M >= 1 and os.environ.get("PCR_NDP_CHAMFER", "1") != "0"
+        if self.use_nc:
+            lib = _lib.load()
+            nbytes = int(lib.pcr_ndp_chamfer_scratch_bytes(K, M))
+            self.nc_raw = torch.empty(nbytes + 256, dtype=torch.uint8, device=dev)
+            off = (-self.nc_raw.data_ptr()) % 256
+            self.gacc = torch.zeros(1 + 3 * K, dtype=torch.int64, device=dev)
+            c = _ChamferC()
+            c.xs, c.tgt, c.K, c.M, c.trunc = self.xs.data_ptr(), self.t3.data_ptr(), K, M, 1e9
+            c.d1, c.d2, c.i1, c.i2 = (self.d1.data_ptr(), self.d2.data_ptr(), self.i1.data_ptr(),
+                                      self.i2.data_ptr())
+            c.gacc, c.scratch = self.gacc.data_ptr(), self.nc_raw.data_ptr() + off
+            self.nc = c
+            t.gacc = self.gacc.data_ptr()
+            self.xs0 = s_sample.index_select(0, inds).contiguous()
+            _lib.call("pcr_ndp_chamfer_prepare", ctypes.byref(c), _lib.ptr(self.xs0),
+                      _lib.stream_handle(dev))
         self.desc = t
 
     def _rebuild_table(self):
@@ -372,11 +401,30 @@ class _LevelFused(_Level):
             _lib.call("pcr_set_gate", None)
 
     def _step(self):
-        from .nndistance import nnd_backward_cuda, nnd_forward_cuda
         cfg = self.cfg
         st = _lib.stream_handle(self.s.device)
         desc = ctypes.byref(self.desc)
         _lib.call("pcr_ndp_train_forward", desc, st)
+        if self.use_nc:
+            _lib.call("pcr_ndp_chamfer_step", ctypes.byref(self.nc), st)
+            _lib.call("pcr_ndp_chamfer_glue", _lib.ptr(self.d1), self.K, _lib.ptr(self.d2), self.M,
+                      _lib.ptr(self.aux[6] if self.bce_on else None), self.N, float(cfg.w_reg), 1e9,
+                      None, None, _lib.ptr(self.loss), _lib.ptr(self.log), _lib.ptr(self.ctr),
+                      int(cfg.iters), st)
+        else:
+            self._chamfer_nnd(st)
+        _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
+                  ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
+        _lib.call("pcr_ndp_control", _lib.ptr(self.loss), _lib.ptr(self.state),
+                  float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4, st)
+        _lib.call("pcr_adam_masked", _lib.ptr(self.table), len(self.params), self.max_numel,
+                  _lib.ptr(self.state), float(cfg.lr), 0.9, 0.999, 1e-8, st)
+
+    def _chamfer_nnd(self, st):
+        """The Chamfer pass on the nnd drop-in kernels (a1 forward, the glue, a2
+        backward): subsets with repeated indices (no inverse map)."""
+        from .nndistance import nnd_backward_cuda, nnd_forward_cuda
+        cfg = self.cfg
         xs = self.xs if self.use_inv else self.xo.index_select(0, self.inds)[None].contiguous()
         nnd_forward_cuda(xs, self.t3, self.d1, self.d2, self.i1, self.i2)
         # loss (truncated Chamfer means + BCE), dL/dd1, dL/dd2, the log entry, the counter
@@ -388,12 +436,6 @@ class _LevelFused(_Level):
         if not self.use_inv:
             self.gx.zero_()
             self.gx.index_add_(0, self.inds, self.gsub[0])
-        _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
-                  ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
-        _lib.call("pcr_ndp_control", _lib.ptr(self.loss), _lib.ptr(self.state),
-                  float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4, st)
-        _lib.call("pcr_adam_masked", _lib.ptr(self.table), len(self.params), self.max_numel,
-                  _lib.ptr(self.state), float(cfg.lr), 0.9, 0.999, 1e-8, st)
 
 
 def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, use_graph=True,

@@ -1,0 +1,160 @@
+"""GPU: the NDP level Chamfer pass (csrc/ndp_chamfer.hip) against the nnd drop-in
+kernels it specialises (a1 / a2, themselves bit-exact vs the reference's
+my_lib.cpp: test_nnd_gpu.py).
+
+* distances and indices: bit-exact vs pcr_nnd_forward, for every ring cap
+  (PCR_NDP_CHAMFER_RINGS 0..3: more or fewer queries go to the tiled exact
+  scan), on a partially overlapping pair (a third of the target far from the
+  subset), quantised ties, and with a NaN (the reference loop);
+* the gradient (2^-44 fixed-point sums): vs pcr_nnd_backward with
+  gd1 = 1/K, gd2 = 1/M (0 where d >= trunc), 2e-6 of the largest entry + 1e-12
+  (f32 terms summed exactly vs summed in f32 in index order);
+* repeated steps (the per-iteration resets) give the same bits; a closed gate
+  skips the step.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from pointcloudregistration_amd import _lib
+from pointcloudregistration_amd.ndp_opt import _ChamferC
+from pointcloudregistration_amd.nndistance import nnd_backward_cuda, nnd_forward_cuda
+
+pytestmark = pytest.mark.gpu
+
+
+class _Nc:
+    def __init__(self, xs, tgt, trunc=1e9, xs0=None):
+        self.xs, self.tgt = xs.contiguous(), tgt.contiguous()
+        K, M = xs.shape[0], tgt.shape[0]
+        self.K, self.M, self.trunc = K, M, trunc
+        f = dict(device="cuda")
+        self.d1, self.d2 = torch.zeros(K, **f), torch.zeros(M, **f)
+        self.i1 = torch.zeros(K, dtype=torch.int32, **f)
+        self.i2 = torch.zeros(M, dtype=torch.int32, **f)
+        self.gacc = torch.zeros(1 + 3 * K, dtype=torch.int64, **f)
+        nb = int(_lib.load().pcr_ndp_chamfer_scratch_bytes(K, M))
+        self.raw = torch.empty(nb + 256, dtype=torch.uint8, **f)
+        c = _ChamferC()
+        c.xs, c.tgt, c.K, c.M, c.trunc = self.xs.data_ptr(), self.tgt.data_ptr(), K, M, trunc
+        c.d1, c.d2, c.i1, c.i2 = (self.d1.data_ptr(), self.d2.data_ptr(), self.i1.data_ptr(),
+                                  self.i2.data_ptr())
+        c.gacc = self.gacc.data_ptr()
+        c.scratch = self.raw.data_ptr() + (-self.raw.data_ptr()) % 256
+        self.c = c
+        x0 = self.xs if xs0 is None else xs0.contiguous()
+        _lib.call("pcr_ndp_chamfer_prepare", ctypes.byref(c), _lib.ptr(x0), _lib.stream_handle())
+
+    def step(self):
+        _lib.call("pcr_ndp_chamfer_step", ctypes.byref(self.c), _lib.stream_handle())
+        torch.cuda.synchronize()
+
+    def grad(self):
+        g = self.gacc[1:].double().reshape(-1, 3) * 2.0 ** -44
+        return g.float(), int(self.gacc[0])
+
+
+def _reference(xs, tgt, trunc):
+    K, M = xs.shape[0], tgt.shape[0]
+    d1, d2 = torch.zeros(1, K, device="cuda"), torch.zeros(1, M, device="cuda")
+    i1 = torch.zeros(1, K, dtype=torch.int32, device="cuda")
+    i2 = torch.zeros(1, M, dtype=torch.int32, device="cuda")
+    nnd_forward_cuda(xs[None].contiguous(), tgt[None].contiguous(), d1, d2, i1, i2)
+    gd1 = torch.where(d1 >= trunc, 0.0, torch.full_like(d1, np.float32(1.0 / K)))
+    gd2 = torch.where(d2 >= trunc, 0.0, torch.full_like(d2, np.float32(1.0 / M)))
+    g1, g2 = torch.zeros(1, K, 3, device="cuda"), torch.zeros(1, M, 3, device="cuda")
+    nnd_backward_cuda(xs[None].contiguous(), tgt[None].contiguous(), g1, g2, gd1, gd2, i1, i2)
+    torch.cuda.synchronize()
+    return d1[0], d2[0], i1[0], i2[0], g1[0]
+
+
+def _partial_pair(seed, K=6000, M=12000):
+    """A warped subset of a surface against a target of which a third lies far
+    from it (the C5 regime that sends queries past the ring cap)."""
+    rng = np.random.default_rng(seed)
+    u = rng.uniform(0, 1, (M, 2))
+    t = np.stack([u[:, 0], u[:, 1], 0.1 * np.sin(6 * u[:, 0]) * np.cos(4 * u[:, 1])], 1)
+    s = t[u[:, 0] < 0.66][:K] + rng.normal(0, 0.004, (min(K, int((u[:, 0] < 0.66).sum())), 3))
+    return (torch.from_numpy(s.astype(np.float32)).cuda(), torch.from_numpy(t.astype(np.float32)).cuda())
+
+
+def _check(xs, tgt, trunc=1e9, rings=None):
+    old = os.environ.get("PCR_NDP_CHAMFER_RINGS")
+    try:
+        if rings is not None:
+            os.environ["PCR_NDP_CHAMFER_RINGS"] = str(rings)
+        nc = _Nc(xs, tgt, trunc)
+        nc.step()
+    finally:
+        if old is None:
+            os.environ.pop("PCR_NDP_CHAMFER_RINGS", None)
+        else:
+            os.environ["PCR_NDP_CHAMFER_RINGS"] = old
+    d1, d2, i1, i2, g1 = _reference(xs, tgt, trunc)
+    assert torch.equal(nc.d1, d1) and torch.equal(nc.i1, i1)
+    assert torch.equal(nc.d2, d2) and torch.equal(nc.i2, i2)
+    g, bad = nc.grad()
+    assert bad == 0
+    tol = 2e-6 * float(g1.abs().max()) + 1e-12
+    assert torch.allclose(g, g1, atol=tol, rtol=0), float((g - g1).abs().max())
+    return nc
+
+
+@pytest.mark.parametrize("rings", [0, 1, 2, 3])
+def test_partial_overlap_bitexact_every_ring_cap(rings):
+    xs, tgt = _partial_pair(1)
+    _check(xs, tgt, rings=rings)
+
+
+def test_quantised_ties_and_truncation():
+    rng = np.random.default_rng(2)
+    xs = torch.from_numpy((rng.integers(0, 20, (3000, 3)) * 0.05).astype(np.float32)).cuda()
+    tgt = torch.from_numpy((rng.integers(0, 20, (5000, 3)) * 0.05).astype(np.float32)).cuda()
+    _check(xs, tgt)
+    _check(xs, tgt, trunc=0.0025)  # d >= trunc: no gradient, as the glue's mask
+
+
+def test_nan_switches_to_reference_loop():
+    xs, tgt = _partial_pair(3, K=2000, M=3000)
+    xs[17, 1] = float("nan")
+    nc = _Nc(xs, tgt)
+    nc.step()
+    d1, d2, i1, i2, _ = _reference(xs, tgt, 1e9)
+    assert torch.equal(nc.i1, i1) and torch.equal(nc.i2, i2)
+    assert torch.equal(torch.nan_to_num(nc.d1, nan=-1.0), torch.nan_to_num(d1, nan=-1.0))
+    assert torch.equal(torch.nan_to_num(nc.d2, nan=-1.0), torch.nan_to_num(d2, nan=-1.0))
+    assert nc.grad()[1] != 0  # the NaN term is flagged (the backward returns NaN)
+
+
+def test_repeated_steps_and_moving_subset():
+    """Per-iteration resets: a second step on the same input gives the same bits,
+    then a moved subset (the cell fixed at prepare) is still exact."""
+    xs, tgt = _partial_pair(4)
+    nc = _Nc(xs, tgt)
+    nc.step()
+    first = [t.clone() for t in (nc.d1, nc.d2, nc.i1, nc.i2, nc.gacc)]
+    nc.step()
+    for a, b in zip(first, (nc.d1, nc.d2, nc.i1, nc.i2, nc.gacc)):
+        assert torch.equal(a, b)
+    nc.xs.mul_(1.3).add_(0.05)  # the level's warp moves the subset
+    nc.step()
+    d1, d2, i1, i2, g1 = _reference(nc.xs, tgt, 1e9)
+    assert torch.equal(nc.d1, d1) and torch.equal(nc.i1, i1)
+    assert torch.equal(nc.d2, d2) and torch.equal(nc.i2, i2)
+    g, _ = nc.grad()
+    assert torch.allclose(g, g1, atol=2e-6 * float(g1.abs().max()) + 1e-12, rtol=0)
+
+
+def test_gate_closed_skips_step():
+    xs, tgt = _partial_pair(5, K=1500, M=2500)
+    nc = _Nc(xs, tgt)
+    gate = torch.zeros(8, dtype=torch.float64, device="cuda")
+    _lib.call("pcr_set_gate", _lib.ptr(gate))
+    try:
+        nc.step()
+    finally:
+        _lib.call("pcr_set_gate", None)
+    assert int(nc.i1.abs().sum()) == 0 and int(nc.gacc.abs().sum()) == 0
