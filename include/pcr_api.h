@@ -469,9 +469,11 @@ typedef struct pcr_ndp_train {
     float *xs;
     const float *gsub;
     /* optional (null = off): the subset gradient as pcr_ndp_chamfer_step leaves
-     * it -- gacc[0] nonzero = a non-finite term, gacc[1 + 3k + c] = dL/dxs[k][c]
-     * in 2^-44 fixed point; read instead of gsub */
+     * it -- gacc[0] nonzero = a non-finite term, the sum over r of
+     * gacc[1 + 3 (r K + k) + c] = dL/dxs[k][c] in 2^-44 fixed point; read
+     * instead of gsub; K = gacc_k */
     const long long *gacc;
+    int32_t gacc_k, reserved;
 } pcr_ndp_train;
 int pcr_ndp_train_forward(const pcr_ndp_train *t, pcr_stream_t stream);
 int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32_t chunk,
@@ -492,15 +494,18 @@ int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
 /* pcr_ndp_chamfer_*: the level's Chamfer pass with its gradient, specialised
  *   for the loop (csrc/ndp_chamfer.hip).  xs (K,3) = x_out[inds] (written by
  *   pcr_ndp_train_forward through inv), tgt (M,3) fixed for the level.
- *   d1/i1 (K), d2/i2 (M): pcr_nnd_forward's outputs bit for bit.  gacc (1 + 3K
- *   int64): the gradient of sum(d1')/K + sum(d2')/M w.r.t. xs (d' = d where
- *   d < trunc, else 0) in 2^-44 fixed point, gacc[0] != 0 when a term was not
- *   finite -- consumed by pcr_ndp_train_backward (pcr_ndp_train.gacc).
+ *   d1/i1 (K), d2/i2 (M): pcr_nnd_forward's outputs bit for bit.  gacc
+ *   (1 + 3 K PCR_NDP_GACC_REPLICAS int64): the gradient of sum(d1')/K +
+ *   sum(d2')/M w.r.t. xs (d' = d where d < trunc, else 0) in 2^-44 fixed point,
+ *   as PCR_NDP_GACC_REPLICAS partial sums gacc[1 + 3 (r K + k) + c] (the
+ *   gradient is their sum), gacc[0] != 0 when a term was not finite -- consumed
+ *   by pcr_ndp_train_backward (pcr_ndp_train.gacc).  K, M <= 32768.
  *   scratch: pcr_ndp_chamfer_scratch_bytes(K, M) bytes, 256-byte aligned,
  *   owned by the caller for the level.
  * pcr_ndp_chamfer_prepare: the target grid and the subset cell (from xs0, the
  *   level's input subset); once per level, outside the captured graph.
  * pcr_ndp_chamfer_step: one iteration (gated like the other f4 launches). */
+#define PCR_NDP_GACC_REPLICAS 16
 typedef struct pcr_ndp_chamfer {
     const float *xs;
     const float *tgt;

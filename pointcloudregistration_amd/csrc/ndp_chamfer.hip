@@ -10,8 +10,10 @@
 //     scan, scatter; a single-pair cloud in one workgroup took 35-63 us);
 //   * queries of both directions in one launch, LPQ lanes per query, the ring
 //     walk of nng.h; a query not certified within kmax rings is listed and
-//     answered by nc_fallback, a tiled exact scan (one wave per 4 listed
-//     queries, 1,024 candidates per LDS tile) -- the far target points of a
+//     answered by nc_fallback: every cloud also has a coarse grid (cell 4x,
+//     ~n/32 hash slots, an AABB per slot), and one wave per listed query visits
+//     the coarse slots in increasing box distance until the next box's
+//     certified lower bound exceeds the best -- the far target points of a
 //     partially overlapping pair (36 % of the C5 target) had made every wave
 //     of the general kernel run a whole-cloud scan;
 //   * the gradient dL/dxs is accumulated in the same epilogue: query i of the
@@ -31,6 +33,8 @@
 #include "pcr_internal.h"
 #include "nng.h"
 #include "scan.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace pcr {
 namespace {
@@ -41,8 +45,10 @@ using nng::nhash;
 using nng::take;
 
 constexpr double kFixScale = 17592186044416.0;  // 2^44
-constexpr int kTile = 1024;                     // candidates per LDS tile of nc_fallback
-constexpr int kFbWaves = 8, kFbQ = 4;           // nc_fallback: waves per block, queries per wave
+constexpr int kRep = PCR_NDP_GACC_REPLICAS;     // gradient sum replicas (query index mod kRep)
+constexpr int kScMax = 1024;                    // coarse slots per cloud (at most)
+constexpr int kCoarse = 4;                      // coarse cell = kCoarse x the fine cell
+constexpr int kFbBlocks = 1024;                 // nc_fallback: persistent 256-thread blocks
 
 struct NcHdr {
     float cell_t, cell_s;
@@ -53,17 +59,26 @@ struct NcHdr {
     int pad;
 };
 
+// one cloud's grids: the fine hashed grid of nng.h and a coarse one whose slots
+// carry the AABB of their points
+struct NcCloud {
+    int S, Sc;
+    int *start, *cstart;  // S + 1, Sc + 1
+    float4 *pts, *cpts;   // n: (x, y, z, index bits) sorted by fine / coarse slot
+    float4 *cbox;         // Sc x (lo, hi)
+};
+
 struct NcArgs {
     const float *xs, *tgt;  // (K, 3), (M, 3)
     int K, M, St, Ss, kmax;
+    NcCloud ct, cs;         // target, subset
     float trunc, g1, g2;    // g1 = 1/K, g2 = 1/M (as the glue)
     float *d1, *d2;
     int32_t *i1, *i2;
-    long long *gacc;        // [0]: non-finite contribution flag; [1 + 3k + c]: dL/dxs fixed point
+    long long *gacc;        // [0]: non-finite contribution flag; [1 + 3 (r K + k) + c]: replica r of
+                            // dL/dxs[k][c] in fixed point (pcr_ndp_train_backward sums the replicas)
     NcHdr *hdr;
-    int *cnt;               // max(Ss, St): counting-sort counts, zero between builds
-    int *start_t, *start_s; // St + 1, Ss + 1
-    float4 *pts_t, *pts_s;  // M, K: (x, y, z, index bits) sorted by slot
+    int *cnt, *ccnt;        // counting-sort counts (fine, coarse), zero between builds
     int *fb;                // K + M: listed queries (dir 0 at 0, dir 1 at K)
     const double *gate;
 };
@@ -123,26 +138,47 @@ __global__ __launch_bounds__(1024) void nc_bbox(const float *P, int n, float *ce
 // counting sort of one cloud by hash slot: count (optionally zeroing the
 // gradient sums of the subset), scan, scatter.  cnt is all-zero before count
 // and after scatter (scatter counts down).
-__global__ void nc_count(const float *P, int n, const float *cellp, int S, int *cnt, int *flag,
+__device__ __forceinline__ unsigned chash(float x, float y, float z, double ic, int Sc) {
+    const double icc = ic * (1.0 / kCoarse);
+    return nhash(ccoord(x, icc), ccoord(y, icc), ccoord(z, icc), Sc);
+}
+
+__global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, int *cnt, int *ccnt, int *flag,
                          long long *gacc, const double *gate) {
     if (gated_off(gate)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (gacc) {
-        gacc[1 + 3 * i] = 0; gacc[2 + 3 * i] = 0; gacc[3 + 3 * i] = 0;
-    }
+    if (gacc)
+#pragma unroll
+        for (int r = 0; r < kRep; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) gacc[1 + 3 * ((size_t)r * n + i) + c] = 0;
     const float x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
     const double ic = 1.0 / (double)*cellp;
     if (!cell_ok(x, y, z, ic)) { atomicOr(flag, 1); return; }
-    atomicAdd(cnt + nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), S), 1);
+    atomicAdd(cnt + nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), g.S), 1);
+    atomicAdd(ccnt + chash(x, y, z, ic, g.Sc), 1);
 }
 
 // one workgroup: starts of the subset (or target) grid; the per-iteration
 // resets (mode, listed counts, the gradient's non-finite flag) ride along
-__global__ __launch_bounds__(1024) void nc_scan(int *cnt, int *start, int S, NcHdr *h, long long *gacc,
-                                                const double *gate) {
+// (the counts are staged through LDS with coalesced loads: the span scan's
+// strided global reads took ~19 us for 16K slots)
+constexpr int kScanLds = 32768;
+
+__global__ __launch_bounds__(1024) void nc_scan(const int *cnt, const int *ccnt, NcCloud g, NcHdr *h,
+                                                long long *gacc, const double *gate) {
     if (gated_off(gate)) return;
-    block_exclusive_scan_1024(cnt, start, S, false);
+    extern __shared__ int lds[];  // S + 1
+    for (int i = threadIdx.x; i < g.S; i += 1024) lds[i] = cnt[i];
+    __syncthreads();
+    block_exclusive_scan_1024(lds, lds, g.S, false);
+    for (int i = threadIdx.x; i <= g.S; i += 1024) g.start[i] = lds[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < g.Sc; i += 1024) lds[i] = ccnt[i];
+    __syncthreads();
+    block_exclusive_scan_1024(lds, lds, g.Sc, false);
+    for (int i = threadIdx.x; i <= g.Sc; i += 1024) g.cstart[i] = lds[i];
     if (threadIdx.x == 0 && gacc) {
         h->mode = h->sflag | h->tflag;
         h->sflag = 0;
@@ -152,17 +188,44 @@ __global__ __launch_bounds__(1024) void nc_scan(int *cnt, int *start, int S, NcH
     }
 }
 
-__global__ void nc_scatter(const float *P, int n, const float *cellp, int S, int *cnt, const int *start,
-                           float4 *pts, const double *gate) {
+__global__ void nc_scatter(const float *P, int n, const float *cellp, NcCloud g, int *cnt, int *ccnt,
+                           const double *gate) {
     if (gated_off(gate)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
     const double ic = 1.0 / (double)*cellp;
     if (!cell_ok(x, y, z, ic)) return;
-    const unsigned hs = nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), S);
-    const int pos = start[hs] + atomicSub(cnt + hs, 1) - 1;
-    pts[pos] = make_float4(x, y, z, __int_as_float(i));
+    const float4 v = make_float4(x, y, z, __int_as_float(i));
+    const unsigned hs = nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), g.S);
+    g.pts[g.start[hs] + atomicSub(cnt + hs, 1) - 1] = v;
+    const unsigned hc = chash(x, y, z, ic, g.Sc);
+    g.cpts[g.cstart[hc] + atomicSub(ccnt + hc, 1) - 1] = v;
+}
+
+// the AABB of every coarse slot (one wave per slot; empty: lo = +inf, hi = -inf)
+__global__ __launch_bounds__(256) void nc_cbox(NcCloud g, const double *gate) {
+    if (gated_off(gate)) return;
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (s >= g.Sc) return;
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    for (int i = g.cstart[s] + lane; i < g.cstart[s + 1]; i += 64) {
+        const float4 p = g.cpts[i];
+        lo[0] = fminf(lo[0], p.x); lo[1] = fminf(lo[1], p.y); lo[2] = fminf(lo[2], p.z);
+        hi[0] = fmaxf(hi[0], p.x); hi[1] = fmaxf(hi[1], p.y); hi[2] = fmaxf(hi[2], p.z);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            lo[c] = fminf(lo[c], __shfl_xor(lo[c], o, 64));
+            hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o, 64));
+        }
+    if (lane == 0) {
+        g.cbox[2 * s] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+        g.cbox[2 * s + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+    }
 }
 
 __device__ __forceinline__ void fix_add(long long *dst, float v, long long *flag) {
@@ -175,22 +238,26 @@ __device__ __forceinline__ void fix_add(long long *dst, float v, long long *flag
 }
 
 // the answer (best, bj) of query q in direction dir: outputs and gradient
-// (pcr_nnd_backward's terms: g = gd * 2, grad1 += g (x - y), grad1[i] -= g (y - x))
+// (pcr_nnd_backward's terms: g = gd * 2, grad1 += g (x - y), grad1[i] -= g (y - x)).
+// The far target points of a partial overlap share a few boundary answers (up to
+// ~350 terms on one subset point in C5): the terms go to replica q mod kRep, so
+// same-address atomics stay short (integer sums: the replica split changes no bit)
 __device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best, int bj) {
+    long long *rep = a.gacc + 1 + (size_t)(q & (kRep - 1)) * 3 * a.K;
     if (dir == 0) {
         a.d1[q] = best;
         a.i1[q] = bj;
         const float g = (!(best >= a.trunc) ? a.g1 : 0.0f) * 2;
         if (bj < 0 || bj >= a.M) return;
         for (int c = 0; c < 3; ++c)
-            fix_add(a.gacc + 1 + 3 * q + c, g * (a.xs[3 * q + c] - a.tgt[3 * bj + c]), a.gacc);
+            fix_add(rep + 3 * q + c, g * (a.xs[3 * q + c] - a.tgt[3 * bj + c]), a.gacc);
     } else {
         a.d2[q] = best;
         a.i2[q] = bj;
         const float g = (!(best >= a.trunc) ? a.g2 : 0.0f) * 2;
         if (bj < 0 || bj >= a.K) return;
         for (int c = 0; c < 3; ++c)
-            fix_add(a.gacc + 1 + 3 * bj + c, -(g * (a.tgt[3 * q + c] - a.xs[3 * bj + c])), a.gacc);
+            fix_add(rep + 3 * bj + c, -(g * (a.tgt[3 * q + c] - a.xs[3 * bj + c])), a.gacc);
     }
 }
 
@@ -214,7 +281,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
     if (brute) {
         qx = Q[3 * qi]; qy = Q[3 * qi + 1]; qz = Q[3 * qi + 2];
     } else {
-        const float4 qp = (dir ? a.pts_t : a.pts_s)[qslot];
+        const float4 qp = (dir ? a.ct.pts : a.cs.pts)[qslot];
         qx = qp.x; qy = qp.y; qz = qp.z;
         qi = __float_as_int(qp.w);
     }
@@ -232,76 +299,107 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
         emit(a, dir, qi, best, bj);
         return;
     }
-    const nng::View v = dir ? nng::View{a.hdr->cell_s, a.Ss, a.start_s, a.pts_s}
-                            : nng::View{a.hdr->cell_t, a.St, a.start_t, a.pts_t};
+    const nng::View v = dir ? nng::View{a.hdr->cell_s, a.cs.S, a.cs.start, a.cs.pts}
+                            : nng::View{a.hdr->cell_t, a.ct.S, a.ct.start, a.ct.pts};
     const bool done = nng::ring_walk<LPQ>(v, qx, qy, qz, sub, a.kmax, best, bj);
-    if (sub != 0) return;
-    if (done) {
-        emit(a, dir, qi, best, bj);
-    } else {
-        const int pos = atomicAdd(&a.hdr->fb_cnt[dir], 1);
-        a.fb[(dir ? a.K : 0) + pos] = qi;
+    // listed queries appended with one atomic per wave (thousands of far
+    // queries on one counter serialised at the L2); a wave holds one direction
+    const bool list = !done && sub == 0;
+    const unsigned long long bal = __ballot(list);
+    if (bal) {
+        const int lane = threadIdx.x & 63;
+        int base = 0;
+        if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(&a.hdr->fb_cnt[dir], __popcll(bal));
+        base = __shfl(base, __ffsll((long long)bal) - 1, 64);
+        if (list) a.fb[(dir ? a.K : 0) + base + __popcll(bal & ((1ULL << lane) - 1))] = qi;
+    }
+    if (sub == 0 && done) emit(a, dir, qi, best, bj);
+}
+
+// the listed queries, one wave each (persistent blocks): the coarse slots of
+// the candidate cloud in increasing (box distance, slot) order, every point of
+// a visited slot examined, until the next slot's box distance -- a lower bound
+// of all slots left, as keys only grow -- exceeds the best with the margin of
+// the f32 roundings (box distance and point distance, 2^-20 relative covers
+// both); then no unvisited point can reach (or tie) the best.  Exact for any
+// coarse cell and any hash collisions.
+__global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
+    if (gated_off(a.gate)) return;
+    const int c0 = a.hdr->fb_cnt[0], c1 = a.hdr->fb_cnt[1];
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * 4;
+    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < c0 + c1; w += nw) {
+        const int dir = w < c0 ? 0 : 1;
+        const int qi = a.fb[dir ? a.K + (w - c0) : w];
+        const float *Q = dir ? a.tgt : a.xs;
+        const NcCloud &g = dir ? a.cs : a.ct;
+        const float qx = Q[3 * qi], qy = Q[3 * qi + 1], qz = Q[3 * qi + 2];
+        // this lane's slots s = lane + 64 u: keys (f32 box distance bits, slot)
+        constexpr int kPer = kScMax / 64;
+        unsigned long long key[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int sl = lane + 64 * u;
+            key[u] = ~0ULL;
+            if (sl < g.Sc) {
+                const float4 lo = g.cbox[2 * sl], hi = g.cbox[2 * sl + 1];
+                const float dx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
+                const float dy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
+                const float dz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
+                const float lb = (dx * dx + dy * dy) + dz * dz;  // empty slot: +inf
+                key[u] = ((unsigned long long)__float_as_uint(lb) << 32) | (unsigned)sl;
+            }
+        }
+        float best = __builtin_inff();
+        int bj = 0x7fffffff;
+        unsigned long long thr = 0;
+        for (;;) {
+            unsigned long long m = ~0ULL;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u)
+                if (key[u] >= thr && key[u] < m) m = key[u];
+#pragma unroll
+            for (int o = 32; o; o >>= 1) {
+                const unsigned long long om = __shfl_xor(m, o, 64);
+                m = om < m ? om : m;
+            }
+            if (m == ~0ULL) break;
+            const float lbf = __uint_as_float((unsigned)(m >> 32));
+            if ((double)lbf * (1.0 - 9.5367431640625e-07) > (double)best) break;
+            const int sl = (int)(m & 0xffffffffu);
+            const int e1 = g.cstart[sl + 1];
+            for (int i = g.cstart[sl] + lane; i < e1; i += 64) {
+                const float4 p = g.cpts[i];
+                take(d2f(p.x, p.y, p.z, qx, qy, qz), __float_as_int(p.w), best, bj);
+            }
+#pragma unroll
+            for (int o = 32; o; o >>= 1) {
+                const float ob = __shfl_xor(best, o, 64);
+                const int oj = __shfl_xor(bj, o, 64);
+                take(ob, oj, best, bj);
+            }
+            thr = m + 1;
+        }
+        if (lane == 0) emit(a, dir, qi, best, bj);
     }
 }
 
-// the listed queries: exact scan of every candidate, kTile at a time through
-// LDS; wave w holds queries 4w..4w+3 of the block's 32 in registers, lane l
-// takes candidates l, l + 64, ... of each tile
-__global__ __launch_bounds__(64 * kFbWaves) void nc_fallback(NcArgs a) {
-    if (gated_off(a.gate)) return;
-    const int dir = blockIdx.y;
-    const int cnt = a.hdr->fb_cnt[dir];
-    const int base = blockIdx.x * (kFbWaves * kFbQ);
-    if (base >= cnt) return;  // uniform over the block
-    __shared__ float4 tile[kTile];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const float *Q = dir ? a.tgt : a.xs;
-    const float4 *cand = dir ? a.pts_s : a.pts_t;
-    const int nc = dir ? a.K : a.M;
-    const int *list = a.fb + (dir ? a.K : 0);
-    float qx[kFbQ], qy[kFbQ], qz[kFbQ], best[kFbQ];
-    int qi[kFbQ], bj[kFbQ];
-#pragma unroll
-    for (int u = 0; u < kFbQ; ++u) {
-        const int e = base + wv * kFbQ + u;
-        qi[u] = e < cnt ? list[e] : -1;
-        const int q = qi[u] >= 0 ? qi[u] : 0;
-        qx[u] = Q[3 * q]; qy[u] = Q[3 * q + 1]; qz[u] = Q[3 * q + 2];
-        best[u] = __builtin_inff();
-        bj[u] = 0x7fffffff;
-    }
-    for (int t0 = 0; t0 < nc; t0 += kTile) {
-        const int tn = min(kTile, nc - t0);
-        __syncthreads();
-        for (int c = threadIdx.x; c < tn; c += 64 * kFbWaves) tile[c] = cand[t0 + c];
-        __syncthreads();
-        for (int c = lane; c < tn; c += 64) {
-            const float4 p = tile[c];
-            const int j = __float_as_int(p.w);
-#pragma unroll
-            for (int u = 0; u < kFbQ; ++u) take(d2f(p.x, p.y, p.z, qx[u], qy[u], qz[u]), j, best[u], bj[u]);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < kFbQ; ++u)
-#pragma unroll
-        for (int o = 32; o; o >>= 1) {
-            const float ob = __shfl_xor(best[u], o, 64);
-            const int oj = __shfl_xor(bj[u], o, 64);
-            take(ob, oj, best[u], bj[u]);
-        }
-#pragma unroll
-    for (int u = 0; u < kFbQ; ++u)
-        if (lane == u && qi[u] >= 0) emit(a, dir, qi[u], best[u], bj[u]);
+// the scan's dynamic LDS limit, set once outside any stream capture (prepare
+// runs eagerly before a level graph is captured)
+hipError_t nc_scan_attr() {
+    static const hipError_t e = hipFuncSetAttribute((const void *)nc_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)(sizeof(int) * (kScanLds + 1)));
+    return e;
 }
 
 struct NcLayout {
-    size_t hdr, cnt, start_t, start_s, pts_t, pts_s, fb, total;
-    int St, Ss;
+    size_t hdr, cnt, ccnt, fb, total;
+    size_t start[2], cstart[2], pts[2], cpts[2], cbox[2];  // [0] target, [1] subset
+    int S[2], Sc[2];
 };
 
-inline int pow2_at_least(int n) {
-    int S = 256;
+inline int pow2_at_least(int n, int lo) {
+    int S = lo;
     while (S < n) S <<= 1;
     return S;
 }
@@ -310,15 +408,20 @@ inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 NcLayout nc_layout(int K, int M) {
     NcLayout L;
-    L.St = pow2_at_least(M);
-    L.Ss = pow2_at_least(K);
+    const int n[2] = {M, K};
     size_t o = 0;
     L.hdr = o; o = up256(o + sizeof(NcHdr));
-    L.cnt = o; o = up256(o + sizeof(int) * (size_t)(L.St > L.Ss ? L.St : L.Ss));
-    L.start_t = o; o = up256(o + sizeof(int) * ((size_t)L.St + 1));
-    L.start_s = o; o = up256(o + sizeof(int) * ((size_t)L.Ss + 1));
-    L.pts_t = o; o = up256(o + sizeof(float4) * (size_t)M);
-    L.pts_s = o; o = up256(o + sizeof(float4) * (size_t)K);
+    for (int c = 0; c < 2; ++c) {
+        L.S[c] = pow2_at_least(n[c], 256);
+        L.Sc[c] = std::min(kScMax, pow2_at_least((n[c] + 31) / 32, 64));
+        L.start[c] = o; o = up256(o + sizeof(int) * ((size_t)L.S[c] + 1));
+        L.cstart[c] = o; o = up256(o + sizeof(int) * ((size_t)L.Sc[c] + 1));
+        L.pts[c] = o; o = up256(o + sizeof(float4) * (size_t)n[c]);
+        L.cpts[c] = o; o = up256(o + sizeof(float4) * (size_t)n[c]);
+        L.cbox[c] = o; o = up256(o + 2 * sizeof(float4) * (size_t)L.Sc[c]);
+    }
+    L.cnt = o; o = up256(o + sizeof(int) * (size_t)std::max(L.S[0], L.S[1]));
+    L.ccnt = o; o = up256(o + sizeof(int) * (size_t)kScMax);
     L.fb = o; o = up256(o + sizeof(int) * ((size_t)K + M));
     L.total = o;
     return L;
@@ -327,13 +430,24 @@ NcLayout nc_layout(int K, int M) {
 int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     PCR_REQUIRE(c, PCR_ERR_ARG, "ndp_chamfer: null descriptor");
     PCR_REQUIRE(c->K >= 1 && c->M >= 1, PCR_ERR_ARG, "ndp_chamfer: K=%d, M=%d (both >= 1)", c->K, c->M);
+    PCR_REQUIRE(c->K <= kScanLds && c->M <= kScanLds, PCR_ERR_ARG,
+                "ndp_chamfer: K=%d, M=%d (at most %d each)", c->K, c->M, kScanLds);
     PCR_REQUIRE(c->xs && c->tgt && c->d1 && c->d2 && c->i1 && c->i2 && c->gacc && c->scratch, PCR_ERR_ARG,
                 "ndp_chamfer: null buffer");
     PCR_REQUIRE(((uintptr_t)c->scratch & 255) == 0, PCR_ERR_ARG, "ndp_chamfer: scratch not 256-byte aligned");
     const NcLayout L = nc_layout(c->K, c->M);
     char *s = (char *)c->scratch;
-    a.xs = c->xs; a.tgt = c->tgt; a.K = c->K; a.M = c->M; a.St = L.St; a.Ss = L.Ss;
-    a.kmax = 2;
+    a.xs = c->xs; a.tgt = c->tgt; a.K = c->K; a.M = c->M; a.St = L.S[0]; a.Ss = L.S[1];
+    for (int k = 0; k < 2; ++k) {
+        NcCloud &g = k ? a.cs : a.ct;
+        g.S = L.S[k]; g.Sc = L.Sc[k];
+        g.start = (int *)(s + L.start[k]);
+        g.cstart = (int *)(s + L.cstart[k]);
+        g.pts = (float4 *)(s + L.pts[k]);
+        g.cpts = (float4 *)(s + L.cpts[k]);
+        g.cbox = (float4 *)(s + L.cbox[k]);
+    }
+    a.kmax = 1;
     if (const char *e = getenv("PCR_NDP_CHAMFER_RINGS")) {  // test / tuning hook: 0..3
         const int v = atoi(e);
         if (v >= 0 && v <= 3) a.kmax = v;
@@ -345,10 +459,7 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     a.gacc = (long long *)c->gacc;
     a.hdr = (NcHdr *)(s + L.hdr);
     a.cnt = (int *)(s + L.cnt);
-    a.start_t = (int *)(s + L.start_t);
-    a.start_s = (int *)(s + L.start_s);
-    a.pts_t = (float4 *)(s + L.pts_t);
-    a.pts_s = (float4 *)(s + L.pts_s);
+    a.ccnt = (int *)(s + L.ccnt);
     a.fb = (int *)(s + L.fb);
     a.gate = current_gate();
     return PCR_OK;
@@ -362,6 +473,26 @@ extern "C" int64_t pcr_ndp_chamfer_scratch_bytes(int32_t K, int32_t M) {
     return (int64_t)pcr::nc_layout(K, M).total;
 }
 
+namespace pcr {
+namespace {
+// count, scan, scatter and the coarse boxes of one cloud (cell from the header)
+int nc_build(const NcArgs &a, const float *P, int n, const float *cellp, const NcCloud &g, int *flag,
+             long long *gacc, const double *gate, hipStream_t s) {
+    const int nb = (n + 255) / 256;
+    hipLaunchKernelGGL(nc_count, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, a.ccnt, flag, gacc, gate);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1), s, (const int *)a.cnt,
+                       (const int *)a.ccnt, g, a.hdr, gacc, gate);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(nc_scatter, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, a.ccnt, gate);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(nc_cbox, dim3((g.Sc + 3) / 4), dim3(256), 0, s, g, gate);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+}  // namespace
+}  // namespace pcr
+
 extern "C" int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs0, pcr_stream_t stream) {
     pcr::clear_error();
     pcr::NcArgs a;
@@ -369,24 +500,16 @@ extern "C" int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs
     if (rc != PCR_OK) return rc;
     PCR_REQUIRE(xs0, PCR_ERR_ARG, "ndp_chamfer_prepare: null xs0");
     hipStream_t s = pcr::as_stream(stream);
+    PCR_HIP_CHECK(pcr::nc_scan_attr());
     PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, sizeof(pcr::NcHdr), s));
     PCR_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * (size_t)(a.St > a.Ss ? a.St : a.Ss), s));
+    PCR_HIP_CHECK(hipMemsetAsync(a.ccnt, 0, sizeof(int) * (size_t)pcr::kScMax, s));
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, a.tgt, a.M, &a.hdr->cell_t, &a.hdr->tflag);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, xs0, a.K, &a.hdr->cell_s, (int *)nullptr);
     PCR_LAUNCH_CHECK();
-    // the target grid, once (ungated: prepare runs outside the level graph)
-    const int nb = (a.M + 255) / 256;
-    hipLaunchKernelGGL(pcr::nc_count, dim3(nb), dim3(256), 0, s, a.tgt, a.M, &a.hdr->cell_t, a.St, a.cnt,
-                       &a.hdr->tflag, (long long *)nullptr, (const double *)nullptr);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(pcr::nc_scan, dim3(1), dim3(1024), 0, s, a.cnt, a.start_t, a.St, a.hdr,
-                       (long long *)nullptr, (const double *)nullptr);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(pcr::nc_scatter, dim3(nb), dim3(256), 0, s, a.tgt, a.M, &a.hdr->cell_t, a.St, a.cnt,
-                       (const int *)a.start_t, a.pts_t, (const double *)nullptr);
-    PCR_LAUNCH_CHECK();
-    return PCR_OK;
+    // the target grids, once (ungated: prepare runs outside the level graph)
+    return pcr::nc_build(a, a.tgt, a.M, &a.hdr->cell_t, a.ct, &a.hdr->tflag, nullptr, nullptr, s);
 }
 
 extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t stream) {
@@ -395,15 +518,8 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
     int rc = pcr::nc_args(c, a);
     if (rc != PCR_OK) return rc;
     hipStream_t s = pcr::as_stream(stream);
-    const int nbk = (a.K + 255) / 256;
-    hipLaunchKernelGGL(pcr::nc_count, dim3(nbk), dim3(256), 0, s, a.xs, a.K, &a.hdr->cell_s, a.Ss, a.cnt,
-                       &a.hdr->sflag, a.gacc, a.gate);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(pcr::nc_scan, dim3(1), dim3(1024), 0, s, a.cnt, a.start_s, a.Ss, a.hdr, a.gacc, a.gate);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(pcr::nc_scatter, dim3(nbk), dim3(256), 0, s, a.xs, a.K, &a.hdr->cell_s, a.Ss, a.cnt,
-                       (const int *)a.start_s, a.pts_s, a.gate);
-    PCR_LAUNCH_CHECK();
+    rc = pcr::nc_build(a, a.xs, a.K, &a.hdr->cell_s, a.cs, &a.hdr->sflag, a.gacc, a.gate, s);
+    if (rc != PCR_OK) return rc;
     // lanes per query as pcr_nnd_forward's grid search (8 below 64K queries)
     const long long nq = (long long)a.K + a.M;
     int lpq = nq >= (1LL << 18) ? 1 : nq >= (1LL << 16) ? 4 : 8;
@@ -422,9 +538,7 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
     }
     PCR_LAUNCH_CHECK();
     prof_end(s, pcr::kProfNndGrid);
-    const int per = pcr::kFbWaves * pcr::kFbQ;
-    const int nmax = a.K > a.M ? a.K : a.M;
-    hipLaunchKernelGGL(pcr::nc_fallback, dim3((nmax + per - 1) / per, 2), dim3(64 * pcr::kFbWaves), 0, s, a);
+    hipLaunchKernelGGL(pcr::nc_fallback, dim3(pcr::kFbBlocks), dim3(256), 0, s, a);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }

@@ -64,6 +64,7 @@ struct TrainArgs {
     float *xs;
     const float *gsub;
     const long long *gacc;          // or: the subset gradient in 2^-44 fixed point (ndp_chamfer.hip)
+    int gacc_k;                     // its K (replica stride)
     const double *gate;             // f4 early stop (pcr_internal.h), or null
 };
 
@@ -197,7 +198,13 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
             const float bad = a.gacc[0] ? __builtin_nanf("") : 0.0f;
             constexpr double kInv = 1.0 / 17592186044416.0;  // 2^-44
 #pragma unroll
-            for (int c = 0; c < 3; ++c) g[c] = k >= 0 ? (float)((double)a.gacc[1 + 3 * k + c] * kInv) + bad : 0.0f;
+            for (int c = 0; c < 3; ++c) {
+                long long v = 0;
+                if (k >= 0)
+#pragma unroll
+                    for (int r = 0; r < PCR_NDP_GACC_REPLICAS; ++r) v += a.gacc[1 + 3 * ((size_t)r * a.gacc_k + k) + c];
+                g[c] = k >= 0 ? (float)((double)v * kInv) + bad : 0.0f;
+            }
         } else if (a.inv) {
             const int k = a.inv[pt];
             g[0] = k >= 0 ? a.gsub[3 * k] : 0.0f;
@@ -474,7 +481,7 @@ static int fill_train(const pcr_ndp_train *t, pcr::TrainArgs &a) {
     a.w_nr = L.w_nr; a.b_nr = L.b_nr;
     a.pe = t->pe; a.H = t->H; a.aux = t->aux; a.x_out = t->x_out;
     a.g = t->g; a.bce_scale = t->bce_scale; a.dO = t->dO; a.D = t->D;
-    a.inv = t->inv; a.xs = t->xs; a.gsub = t->gsub; a.gacc = t->gacc;
+    a.inv = t->inv; a.xs = t->xs; a.gsub = t->gsub; a.gacc = t->gacc; a.gacc_k = t->gacc_k;
     a.gate = pcr::current_gate();
     return PCR_OK;
 }

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -241,6 +242,7 @@ class _Level:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.step()
+        self.capture_done = time.perf_counter()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         for k in range(iters):
@@ -269,7 +271,9 @@ class _TrainC(ctypes.Structure):
                 ("x_out", ctypes.c_void_p), ("g", ctypes.c_void_p), ("bce_scale", ctypes.c_double),
                 ("dO", ctypes.c_void_p), ("D", ctypes.c_void_p),
                 ("inv", ctypes.c_void_p), ("xs", ctypes.c_void_p), ("gsub", ctypes.c_void_p),
-                ("gacc", ctypes.c_void_p)]
+                ("gacc", ctypes.c_void_p), ("gacc_k", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+GACC_REPLICAS = 16  # PCR_NDP_GACC_REPLICAS (include/pcr_api.h)
 
 
 class _ChamferC(ctypes.Structure):
@@ -370,14 +374,14 @@ class _LevelFused(_Level):
             nbytes = int(lib.pcr_ndp_chamfer_scratch_bytes(K, M))
             self.nc_raw = torch.empty(nbytes + 256, dtype=torch.uint8, device=dev)
             off = (-self.nc_raw.data_ptr()) % 256
-            self.gacc = torch.zeros(1 + 3 * K, dtype=torch.int64, device=dev)
+            self.gacc = torch.zeros(1 + 3 * K * GACC_REPLICAS, dtype=torch.int64, device=dev)
             c = _ChamferC()
             c.xs, c.tgt, c.K, c.M, c.trunc = self.xs.data_ptr(), self.t3.data_ptr(), K, M, 1e9
             c.d1, c.d2, c.i1, c.i2 = (self.d1.data_ptr(), self.d2.data_ptr(), self.i1.data_ptr(),
                                       self.i2.data_ptr())
             c.gacc, c.scratch = self.gacc.data_ptr(), self.nc_raw.data_ptr() + off
             self.nc = c
-            t.gacc = self.gacc.data_ptr()
+            t.gacc, t.gacc_k = self.gacc.data_ptr(), K
             self.xs0 = s_sample.index_select(0, inds).contiguous()
             _lib.call("pcr_ndp_chamfer_prepare", ctypes.byref(c), _lib.ptr(self.xs0),
                       _lib.stream_handle(dev))
@@ -463,14 +467,20 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
         NDP.gradient_setup(optimized_level=level)
         layer = NDP.pyramid[level]
         use_fused = fused and layer.input[0].weight.shape[0] == 128
+        t0 = time.perf_counter()
         lv = (_LevelFused if use_fused else _Level)(layer, s_sample, t_sample, ind, level, cfg)
+        t1 = time.perf_counter()
         lv.run(use_graph)
         st = lv.state.cpu().numpy()
+        t2 = time.perf_counter()
         info.append({"steps": int(st[3]), "evaluated": int(st[6]), "last_loss": float(st[4]),
                      "losses": lv.log[:int(st[6])].cpu().numpy()})
         ev = getattr(lv, "replay_events", None)
         if ev is not None:
             info[-1]["replay_ms"] = ev[0].elapsed_time(ev[1])
+            info[-1]["capture_ms"] = (lv.capture_done - t1) * 1e3
+        info[-1]["setup_ms"] = (t1 - t0) * 1e3
+        info[-1]["level_ms"] = (t2 - t0) * 1e3
         hist.append((lv.warped + tgt_mean).cpu().numpy())
         s_sample = lv.warped.clone()
     NDP.gradient_setup(optimized_level=-1)

@@ -20,7 +20,7 @@ import pytest
 import torch
 
 from pointcloudregistration_amd import _lib
-from pointcloudregistration_amd.ndp_opt import _ChamferC
+from pointcloudregistration_amd.ndp_opt import GACC_REPLICAS, _ChamferC
 from pointcloudregistration_amd.nndistance import nnd_backward_cuda, nnd_forward_cuda
 
 pytestmark = pytest.mark.gpu
@@ -35,7 +35,7 @@ class _Nc:
         self.d1, self.d2 = torch.zeros(K, **f), torch.zeros(M, **f)
         self.i1 = torch.zeros(K, dtype=torch.int32, **f)
         self.i2 = torch.zeros(M, dtype=torch.int32, **f)
-        self.gacc = torch.zeros(1 + 3 * K, dtype=torch.int64, **f)
+        self.gacc = torch.zeros(1 + 3 * K * GACC_REPLICAS, dtype=torch.int64, **f)
         nb = int(_lib.load().pcr_ndp_chamfer_scratch_bytes(K, M))
         self.raw = torch.empty(nb + 256, dtype=torch.uint8, **f)
         c = _ChamferC()
@@ -53,7 +53,7 @@ class _Nc:
         torch.cuda.synchronize()
 
     def grad(self):
-        g = self.gacc[1:].double().reshape(-1, 3) * 2.0 ** -44
+        g = self.gacc[1:].reshape(GACC_REPLICAS, self.K, 3).sum(0).double() * 2.0 ** -44
         return g.float(), int(self.gacc[0])
 
 
@@ -115,6 +115,19 @@ def test_quantised_ties_and_truncation():
     tgt = torch.from_numpy((rng.integers(0, 20, (5000, 3)) * 0.05).astype(np.float32)).cuda()
     _check(xs, tgt)
     _check(xs, tgt, trunc=0.0025)  # d >= trunc: no gradient, as the glue's mask
+
+
+@pytest.mark.parametrize("rings", [0, 1])
+def test_far_clusters_and_duplicates(rings):
+    """Two target clusters far apart (one 50 cells from every subset point: the
+    coarse-box search walks many empty and colliding slots), duplicated points
+    (index ties), a subset straddling both."""
+    rng = np.random.default_rng(11)
+    a = rng.normal(0, 0.05, (4000, 3))
+    b = rng.normal(0, 0.05, (3000, 3)) + np.array([3.0, -2.0, 1.0])
+    tgt = np.concatenate([a, b, a[:500]]).astype(np.float32)
+    xs = np.concatenate([a[::3] + rng.normal(0, 0.01, (1334, 3)), b[:40]]).astype(np.float32)
+    _check(torch.from_numpy(xs).cuda(), torch.from_numpy(tgt).cuda(), rings=rings)
 
 
 def test_nan_switches_to_reference_loop():

@@ -43,4 +43,7 @@ for rep in range(int(os.environ.get("REPS", "2"))):
     t2 = time.perf_counter()
     print(f"rep {rep}: rigid {1e3 * (t1 - t0):.1f} ms, ndp {1e3 * (t2 - t1):.1f} ms, inds {len(corrs)}, "
           f"evaluated {[i['evaluated'] for i in info]}, replay_ms "
-          f"{[round(i.get('replay_ms', 0), 1) for i in info]}", flush=True)
+          f"{[round(i.get('replay_ms', 0), 1) for i in info]}, setup_ms "
+          f"{[round(i.get('setup_ms', 0), 1) for i in info]}, capture_ms "
+          f"{[round(i.get('capture_ms', 0), 1) for i in info]}, level_ms "
+          f"{[round(i.get('level_ms', 0), 1) for i in info]}", flush=True)
