@@ -10,12 +10,13 @@
 //     scan, scatter; a single-pair cloud in one workgroup took 35-63 us);
 //   * queries of both directions in one launch, LPQ lanes per query, the ring
 //     walk of nng.h; a query not certified within kmax rings is listed and
-//     answered by nc_fallback: every cloud also has a coarse grid (cell 4x,
-//     ~n/32 hash slots, an AABB per slot), and one wave per listed query visits
-//     the coarse slots in increasing box distance until the next box's
-//     certified lower bound exceeds the best -- the far target points of a
-//     partially overlapping pair (36 % of the C5 target) had made every wave
-//     of the general kernel run a whole-cloud scan;
+//     answered by nc_fallback, an exact scan of the other cloud spread over
+//     the whole chip (blocks of 32 listed queries x 1,024-candidate slices,
+//     8 queries per wave against each LDS-staged candidate, the slices' (d, j)
+//     minima combined by 64-bit atomicMin on (d bits, j): d >= 0, so that is
+//     the lexicographic minimum) -- the far target points of a partially
+//     overlapping pair (36 % of the C5 target) had made every wave of the
+//     general kernel run a whole-cloud scan (428 us per C5 iteration);
 //   * the gradient dL/dxs is accumulated in the same epilogue: query i of the
 //     subset adds 2 gd1 (x_i - y_j), query k of the target subtracts
 //     2 gd2 (y_k - x_i) at its answer i, each rounded to 2^-44 fixed point and
@@ -46,9 +47,8 @@ using nng::take;
 
 constexpr double kFixScale = 17592186044416.0;  // 2^44
 constexpr int kRep = PCR_NDP_GACC_REPLICAS;     // gradient sum replicas (query index mod kRep)
-constexpr int kScMax = 1024;                    // coarse slots per cloud (at most)
-constexpr int kCoarse = 4;                      // coarse cell = kCoarse x the fine cell
-constexpr int kFbBlocks = 1024;                 // nc_fallback: persistent 256-thread blocks
+constexpr int kFbQ = 32, kFbSlice = 1024;       // nc_fallback work item: listed queries x candidates
+constexpr int kFbBlocks = 2048;                 // nc_fallback: persistent 256-thread blocks
 
 struct NcHdr {
     float cell_t, cell_s;
@@ -59,13 +59,11 @@ struct NcHdr {
     int pad;
 };
 
-// one cloud's grids: the fine hashed grid of nng.h and a coarse one whose slots
-// carry the AABB of their points
+// one cloud's hashed grid (nng.h)
 struct NcCloud {
-    int S, Sc;
-    int *start, *cstart;  // S + 1, Sc + 1
-    float4 *pts, *cpts;   // n: (x, y, z, index bits) sorted by fine / coarse slot
-    float4 *cbox;         // Sc x (lo, hi)
+    int S;
+    int *start;   // S + 1
+    float4 *pts;  // n: (x, y, z, index bits) sorted by slot
 };
 
 struct NcArgs {
@@ -78,8 +76,9 @@ struct NcArgs {
     long long *gacc;        // [0]: non-finite contribution flag; [1 + 3 (r K + k) + c]: replica r of
                             // dL/dxs[k][c] in fixed point (pcr_ndp_train_backward sums the replicas)
     NcHdr *hdr;
-    int *cnt, *ccnt;        // counting-sort counts (fine, coarse), zero between builds
+    int *cnt;               // counting-sort counts, zero between builds
     int *fb;                // K + M: listed queries (dir 0 at 0, dir 1 at K)
+    unsigned long long *fbkey;  // K + M: their (d bits, j) minima
     const double *gate;
 };
 
@@ -138,12 +137,7 @@ __global__ __launch_bounds__(1024) void nc_bbox(const float *P, int n, float *ce
 // counting sort of one cloud by hash slot: count (optionally zeroing the
 // gradient sums of the subset), scan, scatter.  cnt is all-zero before count
 // and after scatter (scatter counts down).
-__device__ __forceinline__ unsigned chash(float x, float y, float z, double ic, int Sc) {
-    const double icc = ic * (1.0 / kCoarse);
-    return nhash(ccoord(x, icc), ccoord(y, icc), ccoord(z, icc), Sc);
-}
-
-__global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, int *cnt, int *ccnt, int *flag,
+__global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, int *cnt, int *flag,
                          long long *gacc, const double *gate) {
     if (gated_off(gate)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -157,7 +151,6 @@ __global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, i
     const double ic = 1.0 / (double)*cellp;
     if (!cell_ok(x, y, z, ic)) { atomicOr(flag, 1); return; }
     atomicAdd(cnt + nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), g.S), 1);
-    atomicAdd(ccnt + chash(x, y, z, ic, g.Sc), 1);
 }
 
 // one workgroup: starts of the subset (or target) grid; the per-iteration
@@ -166,19 +159,14 @@ __global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, i
 // strided global reads took ~19 us for 16K slots)
 constexpr int kScanLds = 32768;
 
-__global__ __launch_bounds__(1024) void nc_scan(const int *cnt, const int *ccnt, NcCloud g, NcHdr *h,
-                                                long long *gacc, const double *gate) {
+__global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr *h, long long *gacc,
+                                                const double *gate) {
     if (gated_off(gate)) return;
     extern __shared__ int lds[];  // S + 1
     for (int i = threadIdx.x; i < g.S; i += 1024) lds[i] = cnt[i];
     __syncthreads();
     block_exclusive_scan_1024(lds, lds, g.S, false);
     for (int i = threadIdx.x; i <= g.S; i += 1024) g.start[i] = lds[i];
-    __syncthreads();
-    for (int i = threadIdx.x; i < g.Sc; i += 1024) lds[i] = ccnt[i];
-    __syncthreads();
-    block_exclusive_scan_1024(lds, lds, g.Sc, false);
-    for (int i = threadIdx.x; i <= g.Sc; i += 1024) g.cstart[i] = lds[i];
     if (threadIdx.x == 0 && gacc) {
         h->mode = h->sflag | h->tflag;
         h->sflag = 0;
@@ -188,44 +176,15 @@ __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, const int *ccnt,
     }
 }
 
-__global__ void nc_scatter(const float *P, int n, const float *cellp, NcCloud g, int *cnt, int *ccnt,
-                           const double *gate) {
+__global__ void nc_scatter(const float *P, int n, const float *cellp, NcCloud g, int *cnt, const double *gate) {
     if (gated_off(gate)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
     const double ic = 1.0 / (double)*cellp;
     if (!cell_ok(x, y, z, ic)) return;
-    const float4 v = make_float4(x, y, z, __int_as_float(i));
     const unsigned hs = nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), g.S);
-    g.pts[g.start[hs] + atomicSub(cnt + hs, 1) - 1] = v;
-    const unsigned hc = chash(x, y, z, ic, g.Sc);
-    g.cpts[g.cstart[hc] + atomicSub(ccnt + hc, 1) - 1] = v;
-}
-
-// the AABB of every coarse slot (one wave per slot; empty: lo = +inf, hi = -inf)
-__global__ __launch_bounds__(256) void nc_cbox(NcCloud g, const double *gate) {
-    if (gated_off(gate)) return;
-    const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (s >= g.Sc) return;
-    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    for (int i = g.cstart[s] + lane; i < g.cstart[s + 1]; i += 64) {
-        const float4 p = g.cpts[i];
-        lo[0] = fminf(lo[0], p.x); lo[1] = fminf(lo[1], p.y); lo[2] = fminf(lo[2], p.z);
-        hi[0] = fmaxf(hi[0], p.x); hi[1] = fmaxf(hi[1], p.y); hi[2] = fmaxf(hi[2], p.z);
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int o = 32; o; o >>= 1) {
-            lo[c] = fminf(lo[c], __shfl_xor(lo[c], o, 64));
-            hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o, 64));
-        }
-    if (lane == 0) {
-        g.cbox[2 * s] = make_float4(lo[0], lo[1], lo[2], 0.0f);
-        g.cbox[2 * s + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
-    }
+    g.pts[g.start[hs] + atomicSub(cnt + hs, 1) - 1] = make_float4(x, y, z, __int_as_float(i));
 }
 
 __device__ __forceinline__ void fix_add(long long *dst, float v, long long *flag) {
@@ -311,77 +270,99 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
         int base = 0;
         if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(&a.hdr->fb_cnt[dir], __popcll(bal));
         base = __shfl(base, __ffsll((long long)bal) - 1, 64);
-        if (list) a.fb[(dir ? a.K : 0) + base + __popcll(bal & ((1ULL << lane) - 1))] = qi;
+        if (list) {
+            const int e = (dir ? a.K : 0) + base + __popcll(bal & ((1ULL << lane) - 1));
+            a.fb[e] = qi;
+            a.fbkey[e] = ~0ULL;
+        }
     }
     if (sub == 0 && done) emit(a, dir, qi, best, bj);
 }
 
-// the listed queries, one wave each (persistent blocks): the coarse slots of
-// the candidate cloud in increasing (box distance, slot) order, every point of
-// a visited slot examined, until the next slot's box distance -- a lower bound
-// of all slots left, as keys only grow -- exceeds the best with the margin of
-// the f32 roundings (box distance and point distance, 2^-20 relative covers
-// both); then no unvisited point can reach (or tie) the best.  Exact for any
-// coarse cell and any hash collisions.
+// the listed queries: work item = (32 listed queries of one direction, a
+// 1,024-candidate slice of the other cloud), persistent blocks over all items.
+// The slice is staged in LDS (float4 of the grid copy); wave w holds queries
+// 8w..8w+7 as four packed pairs, lane l takes candidates l, l + 64, ...; each
+// query's (d, j) minimum over the slice goes to its key by atomicMin.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
     if (gated_off(a.gate)) return;
+    __shared__ float4 tile[kFbSlice];
     const int c0 = a.hdr->fb_cnt[0], c1 = a.hdr->fb_cnt[1];
-    const int lane = threadIdx.x & 63;
-    const int nw = gridDim.x * 4;
-    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < c0 + c1; w += nw) {
-        const int dir = w < c0 ? 0 : 1;
-        const int qi = a.fb[dir ? a.K + (w - c0) : w];
+    const int g0 = (c0 + kFbQ - 1) / kFbQ, g1 = (c1 + kFbQ - 1) / kFbQ;
+    const int s0 = (a.M + kFbSlice - 1) / kFbSlice, s1 = (a.K + kFbSlice - 1) / kFbSlice;
+    const int n0 = g0 * s0, total = n0 + g1 * s1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int it = blockIdx.x; it < total; it += gridDim.x) {
+        const int dir = it < n0 ? 0 : 1;
+        const int r = dir ? it - n0 : it, ns = dir ? s1 : s0;
+        const int grp = r / ns, sl = r - grp * ns;
+        const int cnt = dir ? c1 : c0, nc = dir ? a.K : a.M;
         const float *Q = dir ? a.tgt : a.xs;
-        const NcCloud &g = dir ? a.cs : a.ct;
-        const float qx = Q[3 * qi], qy = Q[3 * qi + 1], qz = Q[3 * qi + 2];
-        // this lane's slots s = lane + 64 u: keys (f32 box distance bits, slot)
-        constexpr int kPer = kScMax / 64;
-        unsigned long long key[kPer];
+        const float4 *cand = (dir ? a.cs : a.ct).pts;
+        const int lbase = (dir ? a.K : 0) + grp * kFbQ;
+        const int qn = min(kFbQ, cnt - grp * kFbQ);
+        const int t0 = sl * kFbSlice, tn = min(kFbSlice, nc - t0);
+        __syncthreads();  // the previous item's tile is consumed
+        for (int c = threadIdx.x; c < tn; c += 256) tile[c] = cand[t0 + c];
+        __syncthreads();
+        f2v qx[4], qy[4], qz[4], best[4];
+        int bj[8];
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int sl = lane + 64 * u;
-            key[u] = ~0ULL;
-            if (sl < g.Sc) {
-                const float4 lo = g.cbox[2 * sl], hi = g.cbox[2 * sl + 1];
-                const float dx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
-                const float dy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
-                const float dz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
-                const float lb = (dx * dx + dy * dy) + dz * dz;  // empty slot: +inf
-                key[u] = ((unsigned long long)__float_as_uint(lb) << 32) | (unsigned)sl;
+        for (int u = 0; u < 8; ++u) {
+            const int e = wv * 8 + u;
+            const int q = e < qn ? a.fb[lbase + e] : a.fb[lbase];
+            qx[u >> 1][u & 1] = Q[3 * q];
+            qy[u >> 1][u & 1] = Q[3 * q + 1];
+            qz[u >> 1][u & 1] = Q[3 * q + 2];
+            best[u >> 1][u & 1] = __builtin_inff();
+            bj[u] = 0x7fffffff;
+        }
+        for (int c = lane; c < tn; c += 64) {
+            const float4 p = tile[c];
+            const int j = __float_as_int(p.w);
+            const f2v px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const f2v dx = px - qx[h], dy = py - qy[h], dz = pz - qz[h];
+                const f2v d = (dx * dx + dy * dy) + dz * dz;  // d2f's roundings, two queries at once
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int u = 2 * h + b;
+                    float bb = best[h][b];
+                    nng::take_sel(d[b], j, bb, bj[u]);
+                    best[h][b] = bb;
+                }
             }
         }
-        float best = __builtin_inff();
-        int bj = 0x7fffffff;
-        unsigned long long thr = 0;
-        for (;;) {
-            unsigned long long m = ~0ULL;
 #pragma unroll
-            for (int u = 0; u < kPer; ++u)
-                if (key[u] >= thr && key[u] < m) m = key[u];
+        for (int u = 0; u < 8; ++u) {
+            float bb = best[u >> 1][u & 1];
+            int jj = bj[u];
 #pragma unroll
             for (int o = 32; o; o >>= 1) {
-                const unsigned long long om = __shfl_xor(m, o, 64);
-                m = om < m ? om : m;
+                const float ob = __shfl_xor(bb, o, 64);
+                const int oj = __shfl_xor(jj, o, 64);
+                take(ob, oj, bb, jj);
             }
-            if (m == ~0ULL) break;
-            const float lbf = __uint_as_float((unsigned)(m >> 32));
-            if ((double)lbf * (1.0 - 9.5367431640625e-07) > (double)best) break;
-            const int sl = (int)(m & 0xffffffffu);
-            const int e1 = g.cstart[sl + 1];
-            for (int i = g.cstart[sl] + lane; i < e1; i += 64) {
-                const float4 p = g.cpts[i];
-                take(d2f(p.x, p.y, p.z, qx, qy, qz), __float_as_int(p.w), best, bj);
-            }
-#pragma unroll
-            for (int o = 32; o; o >>= 1) {
-                const float ob = __shfl_xor(best, o, 64);
-                const int oj = __shfl_xor(bj, o, 64);
-                take(ob, oj, best, bj);
-            }
-            thr = m + 1;
+            const int e = wv * 8 + u;
+            if (lane == u && e < qn && jj != 0x7fffffff)
+                atomicMin(a.fbkey + lbase + e, ((unsigned long long)__float_as_uint(bb) << 32) | (unsigned)jj);
         }
-        if (lane == 0) emit(a, dir, qi, best, bj);
     }
+}
+
+// the listed queries' answers from their keys
+__global__ __launch_bounds__(256) void nc_fallback_emit(NcArgs a) {
+    if (gated_off(a.gate)) return;
+    const int c0 = a.hdr->fb_cnt[0], c1 = a.hdr->fb_cnt[1];
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= c0 + c1) return;
+    const int dir = w < c0 ? 0 : 1;
+    const int e = dir ? a.K + (w - c0) : w;
+    const unsigned long long k = a.fbkey[e];
+    emit(a, dir, a.fb[e], __uint_as_float((unsigned)(k >> 32)), (int)(unsigned)(k & 0xffffffffu));
 }
 
 // the scan's dynamic LDS limit, set once outside any stream capture (prepare
@@ -393,9 +374,9 @@ hipError_t nc_scan_attr() {
 }
 
 struct NcLayout {
-    size_t hdr, cnt, ccnt, fb, total;
-    size_t start[2], cstart[2], pts[2], cpts[2], cbox[2];  // [0] target, [1] subset
-    int S[2], Sc[2];
+    size_t hdr, cnt, fb, fbkey, total;
+    size_t start[2], pts[2];  // [0] target, [1] subset
+    int S[2];
 };
 
 inline int pow2_at_least(int n, int lo) {
@@ -413,16 +394,12 @@ NcLayout nc_layout(int K, int M) {
     L.hdr = o; o = up256(o + sizeof(NcHdr));
     for (int c = 0; c < 2; ++c) {
         L.S[c] = pow2_at_least(n[c], 256);
-        L.Sc[c] = std::min(kScMax, pow2_at_least((n[c] + 31) / 32, 64));
         L.start[c] = o; o = up256(o + sizeof(int) * ((size_t)L.S[c] + 1));
-        L.cstart[c] = o; o = up256(o + sizeof(int) * ((size_t)L.Sc[c] + 1));
         L.pts[c] = o; o = up256(o + sizeof(float4) * (size_t)n[c]);
-        L.cpts[c] = o; o = up256(o + sizeof(float4) * (size_t)n[c]);
-        L.cbox[c] = o; o = up256(o + 2 * sizeof(float4) * (size_t)L.Sc[c]);
     }
     L.cnt = o; o = up256(o + sizeof(int) * (size_t)std::max(L.S[0], L.S[1]));
-    L.ccnt = o; o = up256(o + sizeof(int) * (size_t)kScMax);
     L.fb = o; o = up256(o + sizeof(int) * ((size_t)K + M));
+    L.fbkey = o; o = up256(o + sizeof(unsigned long long) * ((size_t)K + M));
     L.total = o;
     return L;
 }
@@ -440,14 +417,11 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     a.xs = c->xs; a.tgt = c->tgt; a.K = c->K; a.M = c->M; a.St = L.S[0]; a.Ss = L.S[1];
     for (int k = 0; k < 2; ++k) {
         NcCloud &g = k ? a.cs : a.ct;
-        g.S = L.S[k]; g.Sc = L.Sc[k];
+        g.S = L.S[k];
         g.start = (int *)(s + L.start[k]);
-        g.cstart = (int *)(s + L.cstart[k]);
         g.pts = (float4 *)(s + L.pts[k]);
-        g.cpts = (float4 *)(s + L.cpts[k]);
-        g.cbox = (float4 *)(s + L.cbox[k]);
     }
-    a.kmax = 1;
+    a.kmax = 2;
     if (const char *e = getenv("PCR_NDP_CHAMFER_RINGS")) {  // test / tuning hook: 0..3
         const int v = atoi(e);
         if (v >= 0 && v <= 3) a.kmax = v;
@@ -459,8 +433,8 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     a.gacc = (long long *)c->gacc;
     a.hdr = (NcHdr *)(s + L.hdr);
     a.cnt = (int *)(s + L.cnt);
-    a.ccnt = (int *)(s + L.ccnt);
     a.fb = (int *)(s + L.fb);
+    a.fbkey = (unsigned long long *)(s + L.fbkey);
     a.gate = current_gate();
     return PCR_OK;
 }
@@ -479,14 +453,12 @@ namespace {
 int nc_build(const NcArgs &a, const float *P, int n, const float *cellp, const NcCloud &g, int *flag,
              long long *gacc, const double *gate, hipStream_t s) {
     const int nb = (n + 255) / 256;
-    hipLaunchKernelGGL(nc_count, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, a.ccnt, flag, gacc, gate);
+    hipLaunchKernelGGL(nc_count, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, flag, gacc, gate);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1), s, (const int *)a.cnt,
-                       (const int *)a.ccnt, g, a.hdr, gacc, gate);
+    hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1), s, (const int *)a.cnt, g,
+                       a.hdr, gacc, gate);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(nc_scatter, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, a.ccnt, gate);
-    PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(nc_cbox, dim3((g.Sc + 3) / 4), dim3(256), 0, s, g, gate);
+    hipLaunchKernelGGL(nc_scatter, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, gate);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
@@ -503,7 +475,6 @@ extern "C" int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs
     PCR_HIP_CHECK(pcr::nc_scan_attr());
     PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, sizeof(pcr::NcHdr), s));
     PCR_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * (size_t)(a.St > a.Ss ? a.St : a.Ss), s));
-    PCR_HIP_CHECK(hipMemsetAsync(a.ccnt, 0, sizeof(int) * (size_t)pcr::kScMax, s));
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, a.tgt, a.M, &a.hdr->cell_t, &a.hdr->tflag);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, xs0, a.K, &a.hdr->cell_s, (int *)nullptr);
@@ -539,6 +510,8 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
     PCR_LAUNCH_CHECK();
     prof_end(s, pcr::kProfNndGrid);
     hipLaunchKernelGGL(pcr::nc_fallback, dim3(pcr::kFbBlocks), dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(pcr::nc_fallback_emit, dim3((a.K + a.M + 255) / 256), dim3(256), 0, s, a);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }

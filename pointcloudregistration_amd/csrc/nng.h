@@ -28,6 +28,13 @@ __device__ __forceinline__ void take(float d, int j, float &best, int &bj) {
     if (d < best || (d == best && j < bj)) { best = d; bj = j; }
 }
 
+// the same update as selects (no branch: for many independent minima per lane)
+__device__ __forceinline__ void take_sel(float d, int j, float &best, int &bj) {
+    const bool lt = (d < best) | ((d == best) & (j < bj));
+    best = lt ? d : best;
+    bj = lt ? j : bj;
+}
+
 // a grid view: cell edge, S hash slots, slot starts (S + 1), float4 (x, y, z,
 // index bits) points sorted by slot
 struct View {
