@@ -505,6 +505,16 @@ int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
  * pcr_ndp_chamfer_prepare: the target grid and the subset cell (from xs0, the
  *   level's input subset); once per level, outside the captured graph.
  * pcr_ndp_chamfer_step: one iteration (gated like the other f4 launches). */
+/* pcr_ndp_chamfer_loss: pcr_ndp_chamfer_glue's loss (no dist gradients: the
+ *   Chamfer step made them) over 32 workgroups (fixed ranges, partials summed in
+ *   block order), then -- when state is given -- pcr_ndp_control's rule on it,
+ *   in one launch.  scratch: pcr_ndp_loss_scratch_bytes() bytes, zeroed once
+ *   by the caller (the launch leaves it zeroed). */
+int64_t pcr_ndp_loss_scratch_bytes(void);
+int pcr_ndp_chamfer_loss(const float *d1, int32_t K, const float *d2, int32_t M, const float *s,
+                         int32_t N, double w_reg, double trunc, float *loss, float *log, int64_t *ctr,
+                         int32_t log_last, double *state, double break_threshold_ratio,
+                         int32_t max_break_count, double stop_loss, void *scratch, pcr_stream_t stream);
 #define PCR_NDP_GACC_REPLICAS 16
 typedef struct pcr_ndp_chamfer {
     const float *xs;

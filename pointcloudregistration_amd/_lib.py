@@ -85,6 +85,8 @@ SIGNATURES = {
     "pcr_ndp_chamfer_glue": [_p, _i32, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _p, _p, _i32, _p],
     "pcr_ndp_chamfer_prepare": [_p, _p, _p],
     "pcr_ndp_chamfer_step": [_p, _p],
+    "pcr_ndp_chamfer_loss": [_p, _i32, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _i32, _p, _f64, _i32,
+                             _f64, _p, _p],
     "pcr_hybrid_search": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
     "pcr_estimate_normals": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p],
     "pcr_compute_fpfh": [_p, _p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
@@ -123,6 +125,8 @@ def load():
         lib.pcr_ndp_train_partial_floats.argtypes = [_i32, _i32, _i32, _i32]
         lib.pcr_ndp_chamfer_scratch_bytes.restype = _i64
         lib.pcr_ndp_chamfer_scratch_bytes.argtypes = [_i32, _i32]
+        lib.pcr_ndp_loss_scratch_bytes.restype = _i64
+        lib.pcr_ndp_loss_scratch_bytes.argtypes = []
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
@@ -133,7 +137,8 @@ def load():
 
 def exported_symbols():
     return ["pcr_last_error", "pcr_version", "pcr_workspace_release", "pcr_profile_enable", "pcr_profile_read",
-            "pcr_featnn_rescan_rows", "pcr_ndp_train_partial_floats", "pcr_ndp_chamfer_scratch_bytes"] + \
+            "pcr_featnn_rescan_rows", "pcr_ndp_train_partial_floats", "pcr_ndp_chamfer_scratch_bytes",
+            "pcr_ndp_loss_scratch_bytes"] + \
         list(SIGNATURES)
 
 

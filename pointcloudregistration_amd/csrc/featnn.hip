@@ -637,6 +637,8 @@ __device__ __forceinline__ void rescan_out(const RescanArgs5 &a, int dir, int p,
     }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 template <int DV, bool V4>
 __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
     // thread (row r = tid>>3, slice sl = tid&7): row r of the current batch of
@@ -704,41 +706,59 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
             }
         };
         auto scan = [&](const float *cs, int c0, int ncand) {
-            for (int i = sl; i < ncand; i += 8) {
-                const float *cp = cs + i * kSt;
-                // f32 fma screen: all terms are >= 0, so |d32 - d| <= (D+2) u d;
-                // only candidates within kRel of this thread's running f32 minimum
-                // (>= the global one) can be the exact winner -> f64 for those
-                float a32 = 0.0f;
+            // f32 screen of the thread's kChunk / 8 candidates (packed: two
+            // dims per v_pk_fma): all terms are >= 0, so |d32 - d| <= (D+3) u d
+            // whatever the order; only candidates within kRel of the thread's
+            // running f32 minimum after the chunk (>= the global one) can be
+            // the exact winner.  Those are re-ranked in f64 AFTER the chunk's
+            // screen, in candidate order (first index on ties): a wave runs
+            // one or two f64 ranks per chunk instead of one wherever any lane
+            // had a running-minimum candidate (~a quarter of the steps).
+            constexpr int kPer8 = kChunk / 8;
+            float a32v[kPer8];
 #pragma unroll
-                for (int k = 0; k < DV; k += 4) {
-                    const float4 v = *reinterpret_cast<const float4 *>(cp + k);
-                    float df = v.x - qf[k];
-                    a32 = fmaf(df, df, a32);
-                    df = v.y - qf[k + 1];
-                    a32 = fmaf(df, df, a32);
-                    df = v.z - qf[k + 2];
-                    a32 = fmaf(df, df, a32);
-                    df = v.w - qf[k + 3];
-                    a32 = fmaf(df, df, a32);
-                }
-                if (a32 <= m32 * kRel + 1e-30f) {
-                    double acc = 0.0;
+            for (int t = 0; t < kPer8; ++t) {
+                const int i = sl + 8 * t;
+                float a32 = __builtin_inff();
+                if (i < ncand) {
+                    const float *cp = cs + i * kSt;
+                    f2v acc = {0.0f, 0.0f};
 #pragma unroll
                     for (int k = 0; k < DV; k += 4) {
                         const float4 v = *reinterpret_cast<const float4 *>(cp + k);
-                        double df = qd[k] - (double)v.x;
-                        acc = acc + df * df;
-                        df = qd[k + 1] - (double)v.y;
-                        acc = acc + df * df;
-                        df = qd[k + 2] - (double)v.z;
-                        acc = acc + df * df;
-                        df = qd[k + 3] - (double)v.w;
-                        acc = acc + df * df;
+                        const f2v d0 = f2v{v.x, v.y} - f2v{qf[k], qf[k + 1]};
+                        const f2v d1 = f2v{v.z, v.w} - f2v{qf[k + 2], qf[k + 3]};
+                        acc = __builtin_elementwise_fma(d0, d0, acc);
+                        acc = __builtin_elementwise_fma(d1, d1, acc);
                     }
-                    if (acc < best) { best = acc; bj = c0 + i; }
+                    a32 = acc.x + acc.y;
                 }
+                a32v[t] = a32;
                 m32 = fminf(m32, a32);
+            }
+            const float lim = m32 * kRel + 1e-30f;
+            unsigned pend = 0;
+#pragma unroll
+            for (int t = 0; t < kPer8; ++t) pend |= (a32v[t] <= lim ? 1u : 0u) << t;
+            while (pend) {
+                const int t = __builtin_ctz(pend);
+                pend &= pend - 1;
+                const int i = sl + 8 * t;
+                const float *cp = cs + i * kSt;
+                double acc = 0.0;
+#pragma unroll
+                for (int k = 0; k < DV; k += 4) {
+                    const float4 v = *reinterpret_cast<const float4 *>(cp + k);
+                    double df = qd[k] - (double)v.x;
+                    acc = acc + df * df;
+                    df = qd[k + 1] - (double)v.y;
+                    acc = acc + df * df;
+                    df = qd[k + 2] - (double)v.z;
+                    acc = acc + df * df;
+                    df = qd[k + 3] - (double)v.w;
+                    acc = acc + df * df;
+                }
+                if (acc < best) { best = acc; bj = c0 + i; }
             }
         };
         if (V4) {

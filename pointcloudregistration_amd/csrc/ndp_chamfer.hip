@@ -11,8 +11,8 @@
 //   * queries of both directions in one launch, LPQ lanes per query, the ring
 //     walk of nng.h; a query not certified within kmax rings is listed and
 //     answered by nc_fallback, an exact scan of the other cloud spread over
-//     the whole chip (blocks of 32 listed queries x 1,024-candidate slices,
-//     8 queries per wave against each LDS-staged candidate, the slices' (d, j)
+//     the whole chip (blocks of 64 listed queries x 2,048-candidate slices,
+//     16 queries per wave against each LDS-staged candidate, the slices' (d, j)
 //     minima combined by 64-bit atomicMin on (d bits, j): d >= 0, so that is
 //     the lexicographic minimum) -- the far target points of a partially
 //     overlapping pair (36 % of the C5 target) had made every wave of the
@@ -47,7 +47,8 @@ using nng::take;
 
 constexpr double kFixScale = 17592186044416.0;  // 2^44
 constexpr int kRep = PCR_NDP_GACC_REPLICAS;     // gradient sum replicas (query index mod kRep)
-constexpr int kFbQ = 32, kFbSlice = 1024;       // nc_fallback work item: listed queries x candidates
+constexpr int kFbQW = 16;                       // nc_fallback: listed queries per wave (8 packed pairs)
+constexpr int kFbQ = 4 * kFbQW, kFbSlice = 2048;  // work item: listed queries x candidates
 constexpr int kFbBlocks = 2048;                 // nc_fallback: persistent 256-thread blocks
 
 struct NcHdr {
@@ -162,11 +163,36 @@ constexpr int kScanLds = 32768;
 __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr *h, long long *gacc,
                                                 const double *gate) {
     if (gated_off(gate)) return;
-    extern __shared__ int lds[];  // S + 1
-    for (int i = threadIdx.x; i < g.S; i += 1024) lds[i] = cnt[i];
+    // LDS index i + i / 16: thread t's span [t per, (t+1) per) starts 17 t words
+    // apart at per = 16 (no bank conflicts; the plain layout was 16-way)
+    extern __shared__ int lds[];  // (S + 1) * 17 / 16
+    __shared__ int wtot[16];
+    auto P = [](int i) { return i + (i >> 4); };
+    const int S = g.S, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int i = t; i < S; i += 1024) lds[P(i)] = cnt[i];
     __syncthreads();
-    block_exclusive_scan_1024(lds, lds, g.S, false);
-    for (int i = threadIdx.x; i <= g.S; i += 1024) g.start[i] = lds[i];
+    const int per = (S + 1023) >> 10;
+    const int b0 = min(S, t * per), b1 = min(S, b0 + per);
+    int v = 0;
+    for (int i = b0; i < b1; ++i) v += lds[P(i)];
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int k = 0; k < 16; ++k) { const int c = wtot[k]; wtot[k] = acc; acc += c; }
+        lds[P(S)] = acc;
+    }
+    __syncthreads();
+    int run = wtot[w] + x - v;
+    for (int i = b0; i < b1; ++i) { const int c = lds[P(i)]; lds[P(i)] = run; run += c; }
+    __syncthreads();
+    for (int i = t; i <= S; i += 1024) g.start[i] = lds[P(i)];
     if (threadIdx.x == 0 && gacc) {
         h->mode = h->sflag | h->tflag;
         h->sflag = 0;
@@ -279,11 +305,11 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
     if (sub == 0 && done) emit(a, dir, qi, best, bj);
 }
 
-// the listed queries: work item = (32 listed queries of one direction, a
-// 1,024-candidate slice of the other cloud), persistent blocks over all items.
+// the listed queries: work item = (64 listed queries of one direction, a
+// 2,048-candidate slice of the other cloud), persistent blocks over all items.
 // The slice is staged in LDS (float4 of the grid copy); wave w holds queries
-// 8w..8w+7 as four packed pairs, lane l takes candidates l, l + 64, ...; each
-// query's (d, j) minimum over the slice goes to its key by atomicMin.
+// 16w..16w+15 as eight packed pairs, lane l takes candidates l, l + 64, ...;
+// each query's (d, j) minimum over the slice goes to its key by atomicMin.
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
@@ -294,6 +320,7 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
     const int s0 = (a.M + kFbSlice - 1) / kFbSlice, s1 = (a.K + kFbSlice - 1) / kFbSlice;
     const int n0 = g0 * s0, total = n0 + g1 * s1;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int H = kFbQW / 2;
     for (int it = blockIdx.x; it < total; it += gridDim.x) {
         const int dir = it < n0 ? 0 : 1;
         const int r = dir ? it - n0 : it, ns = dir ? s1 : s0;
@@ -307,11 +334,12 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
         __syncthreads();  // the previous item's tile is consumed
         for (int c = threadIdx.x; c < tn; c += 256) tile[c] = cand[t0 + c];
         __syncthreads();
-        f2v qx[4], qy[4], qz[4], best[4];
-        int bj[8];
+        if (wv * kFbQW >= qn) continue;  // no listed query for this wave (barriers are above)
+        f2v qx[H], qy[H], qz[H], best[H];
+        int bj[kFbQW];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = wv * 8 + u;
+        for (int u = 0; u < kFbQW; ++u) {
+            const int e = wv * kFbQW + u;
             const int q = e < qn ? a.fb[lbase + e] : a.fb[lbase];
             qx[u >> 1][u & 1] = Q[3 * q];
             qy[u >> 1][u & 1] = Q[3 * q + 1];
@@ -324,29 +352,28 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
             const int j = __float_as_int(p.w);
             const f2v px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
+            for (int h = 0; h < H; ++h) {
                 const f2v dx = px - qx[h], dy = py - qy[h], dz = pz - qz[h];
                 const f2v d = (dx * dx + dy * dy) + dz * dz;  // d2f's roundings, two queries at once
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
-                    const int u = 2 * h + b;
                     float bb = best[h][b];
-                    nng::take_sel(d[b], j, bb, bj[u]);
+                    nng::take_sel(d[b], j, bb, bj[2 * h + b]);
                     best[h][b] = bb;
                 }
             }
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < kFbQW; ++u) {
             float bb = best[u >> 1][u & 1];
             int jj = bj[u];
 #pragma unroll
             for (int o = 32; o; o >>= 1) {
                 const float ob = __shfl_xor(bb, o, 64);
                 const int oj = __shfl_xor(jj, o, 64);
-                take(ob, oj, bb, jj);
+                nng::take_sel(ob, oj, bb, jj);
             }
-            const int e = wv * 8 + u;
+            const int e = wv * kFbQW + u;
             if (lane == u && e < qn && jj != 0x7fffffff)
                 atomicMin(a.fbkey + lbase + e, ((unsigned long long)__float_as_uint(bb) << 32) | (unsigned)jj);
         }
@@ -369,7 +396,7 @@ __global__ __launch_bounds__(256) void nc_fallback_emit(NcArgs a) {
 // runs eagerly before a level graph is captured)
 hipError_t nc_scan_attr() {
     static const hipError_t e = hipFuncSetAttribute((const void *)nc_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    (int)(sizeof(int) * (kScanLds + 1)));
+                                                    (int)(sizeof(int) * (kScanLds + 2 + kScanLds / 16)));
     return e;
 }
 
@@ -421,7 +448,7 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
         g.start = (int *)(s + L.start[k]);
         g.pts = (float4 *)(s + L.pts[k]);
     }
-    a.kmax = 2;
+    a.kmax = 1;
     if (const char *e = getenv("PCR_NDP_CHAMFER_RINGS")) {  // test / tuning hook: 0..3
         const int v = atoi(e);
         if (v >= 0 && v <= 3) a.kmax = v;
@@ -455,7 +482,7 @@ int nc_build(const NcArgs &a, const float *P, int n, const float *cellp, const N
     const int nb = (n + 255) / 256;
     hipLaunchKernelGGL(nc_count, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, flag, gacc, gate);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1), s, (const int *)a.cnt, g,
+    hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1 + (g.S >> 4) + 1), s, (const int *)a.cnt, g,
                        a.hdr, gacc, gate);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(nc_scatter, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, gate);
@@ -491,9 +518,10 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
     hipStream_t s = pcr::as_stream(stream);
     rc = pcr::nc_build(a, a.xs, a.K, &a.hdr->cell_s, a.cs, &a.hdr->sflag, a.gacc, a.gate, s);
     if (rc != PCR_OK) return rc;
-    // lanes per query as pcr_nnd_forward's grid search (8 below 64K queries)
+    // lanes per query (C5, 30K queries: 4 lanes and a ring cap of 1 measured best,
+    // tools/ndp_sweep.sh)
     const long long nq = (long long)a.K + a.M;
-    int lpq = nq >= (1LL << 18) ? 1 : nq >= (1LL << 16) ? 4 : 8;
+    int lpq = nq >= (1LL << 18) ? 1 : nq >= (1LL << 14) ? 4 : 8;
     if (const char *e = getenv("PCR_NND_LPQ")) {
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 4 || v == 8) lpq = v;

@@ -18,6 +18,7 @@
 // State (device f64[8]): 0 active, 1 break count, 2 loss_prev, 3 steps taken,
 // 4 last loss, 5 step flag of this iteration, 6 iterations evaluated.
 #include "pcr_internal.h"
+#include "ndp_ctl.h"
 
 namespace pcr {
 namespace {
@@ -25,27 +26,7 @@ namespace {
 __global__ void ndp_control_kernel(const float *loss, double *st, double ratio, int max_break,
                                    double stop_loss) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    if (st[0] == 0.0) {
-        st[5] = 0.0;
-        return;
-    }
-    const double L = (double)*loss;
-    st[6] += 1.0;
-    st[4] = L;
-    if (L < stop_loss) {
-        st[0] = 0.0;
-        st[5] = 0.0;
-        return;
-    }
-    if (fabs(st[2] - L) < st[2] * ratio) st[1] += 1.0;
-    if (st[1] >= (double)max_break) {
-        st[0] = 0.0;
-        st[5] = 0.0;
-        return;
-    }
-    st[2] = L;
-    st[3] += 1.0;
-    st[5] = 1.0;
+    ndp_control_rule(*loss, st, ratio, max_break, stop_loss);
 }
 
 __global__ __launch_bounds__(256) void adam_masked_kernel(const pcr_adam_tensor *tab,

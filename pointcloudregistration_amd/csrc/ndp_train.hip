@@ -29,6 +29,7 @@
 // (deterministic).
 #include "pcr_internal.h"
 #include "ndp_tile.h"
+#include "ndp_ctl.h"
 
 namespace pcr {
 namespace {
@@ -456,6 +457,84 @@ __global__ __launch_bounds__(1024) void ndp_chamfer_glue(GlueArgs a) {
     *a.ctr = c + 1;
 }
 
+// ---- the same loss over kLossBlocks workgroups (fixed index ranges, partials
+// summed in block order by the last block to finish), with the early-stop rule
+// applied by that block: one launch for the glue and pcr_ndp_control ----------
+constexpr int kLossBlocks = 32;
+
+struct LossArgs {
+    GlueArgs g;
+    double *state;  // or null (no rule)
+    double ratio, stop_loss;
+    int max_break;
+    float *part;    // [3][kLossBlocks]
+    unsigned *done; // zero between launches (the last block resets it)
+};
+
+__global__ __launch_bounds__(256) void ndp_loss_kernel(LossArgs a) {
+    const GlueArgs &g = a.g;
+    if (gated_off(g.gate)) return;
+    __shared__ float red[3][4];
+    __shared__ bool last;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, b = blockIdx.x;
+    auto range = [&](int n, int &lo, int &hi) {
+        const int per = (n + kLossBlocks - 1) / kLossBlocks;
+        lo = min(n, b * per);
+        hi = min(n, lo + per);
+    };
+    float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    int lo, hi;
+    range(g.K, lo, hi);
+    for (int i = lo + t; i < hi; i += 256) {
+        const float d = g.d1[i];
+        s1 += !(d >= g.trunc) ? d : 0.0f;  // torch.where(d >= trunc, 0, d): NaN stays
+    }
+    range(g.M, lo, hi);
+    for (int i = lo + t; i < hi; i += 256) {
+        const float d = g.d2[i];
+        s2 += !(d >= g.trunc) ? d : 0.0f;
+    }
+    if (g.s) {
+        range(g.N, lo, hi);
+        for (int i = lo + t; i < hi; i += 256) {
+            const float v = logf(1.0f - g.s[i]);
+            s3 += v < -100.0f ? -100.0f : v;  // clamp(min=-100), NaN stays
+        }
+    }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+        s3 += __shfl_xor(s3, o, 64);
+    }
+    if (lane == 0) { red[0][wv] = s1; red[1][wv] = s2; red[2][wv] = s3; }
+    __syncthreads();
+    if (t == 0) {
+        a.part[b] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        a.part[kLossBlocks + b] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+        a.part[2 * kLossBlocks + b] = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
+        __threadfence();
+        last = atomicAdd(a.done, 1u) == kLossBlocks - 1;
+    }
+    __syncthreads();
+    if (!last || t != 0) return;
+    __threadfence();
+    float S1 = 0.0f, S2 = 0.0f, S3 = 0.0f;
+    for (int k = 0; k < kLossBlocks; ++k) {
+        S1 += __hip_atomic_load(a.part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S2 += __hip_atomic_load(a.part + kLossBlocks + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S3 += __hip_atomic_load(a.part + 2 * kLossBlocks + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    float L = S1 / (float)g.K + S2 / (float)g.M;
+    if (g.s) L = L + g.w_reg * (-S3 / (float)g.N);
+    *g.loss = L;
+    const long long c = *g.ctr;
+    g.log[c < g.log_last ? c : g.log_last] = L;
+    *g.ctr = c + 1;
+    *a.done = 0;
+    if (a.state) ndp_control_rule(L, a.state, a.ratio, a.max_break, a.stop_loss);
+}
+
 }  // namespace
 }  // namespace pcr
 
@@ -560,6 +639,34 @@ extern "C" int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2,
                     (long long *)ctr};
     g.gate = pcr::current_gate();
     hipLaunchKernelGGL(pcr::ndp_chamfer_glue, dim3(1), dim3(1024), 0, pcr::as_stream(stream), g);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+extern "C" int64_t pcr_ndp_loss_scratch_bytes(void) {
+    return (int64_t)(sizeof(float) * 3 * pcr::kLossBlocks + 64);
+}
+
+extern "C" int pcr_ndp_chamfer_loss(const float *d1, int32_t K, const float *d2, int32_t M, const float *s,
+                                    int32_t N, double w_reg, double trunc, float *loss, float *log,
+                                    int64_t *ctr, int32_t log_last, double *state, double break_threshold_ratio,
+                                    int32_t max_break_count, double stop_loss, void *scratch,
+                                    pcr_stream_t stream) {
+    pcr::clear_error();
+    PCR_REQUIRE(K >= 1 && M >= 1 && N >= 0 && log_last >= 0, PCR_ERR_ARG, "ndp_chamfer_loss: bad size");
+    PCR_REQUIRE(d1 && d2 && loss && log && ctr && scratch, PCR_ERR_ARG, "ndp_chamfer_loss: null buffer");
+    pcr::LossArgs a;
+    a.g = pcr::GlueArgs{d1, d2, s, K, M, N, log_last, (float)trunc, (float)w_reg,
+                        (float)(1.0 / (double)K), (float)(1.0 / (double)M), nullptr, nullptr, loss, log,
+                        (long long *)ctr};
+    a.g.gate = pcr::current_gate();
+    a.state = state;
+    a.ratio = break_threshold_ratio;
+    a.stop_loss = stop_loss;
+    a.max_break = max_break_count;
+    a.part = (float *)scratch;
+    a.done = (unsigned *)(a.part + 3 * pcr::kLossBlocks);
+    hipLaunchKernelGGL(pcr::ndp_loss_kernel, dim3(pcr::kLossBlocks), dim3(256), 0, pcr::as_stream(stream), a);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }

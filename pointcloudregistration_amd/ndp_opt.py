@@ -382,6 +382,7 @@ class _LevelFused(_Level):
             c.gacc, c.scratch = self.gacc.data_ptr(), self.nc_raw.data_ptr() + off
             self.nc = c
             t.gacc, t.gacc_k = self.gacc.data_ptr(), K
+            self.loss_scratch = torch.zeros(int(lib.pcr_ndp_loss_scratch_bytes()), dtype=torch.uint8, device=dev)
             self.xs0 = s_sample.index_select(0, inds).contiguous()
             _lib.call("pcr_ndp_chamfer_prepare", ctypes.byref(c), _lib.ptr(self.xs0),
                       _lib.stream_handle(dev))
@@ -410,17 +411,21 @@ class _LevelFused(_Level):
         desc = ctypes.byref(self.desc)
         _lib.call("pcr_ndp_train_forward", desc, st)
         if self.use_nc:
+            # the Chamfer with its gradient, then the loss and the early-stop rule in one launch
             _lib.call("pcr_ndp_chamfer_step", ctypes.byref(self.nc), st)
-            _lib.call("pcr_ndp_chamfer_glue", _lib.ptr(self.d1), self.K, _lib.ptr(self.d2), self.M,
+            _lib.call("pcr_ndp_chamfer_loss", _lib.ptr(self.d1), self.K, _lib.ptr(self.d2), self.M,
                       _lib.ptr(self.aux[6] if self.bce_on else None), self.N, float(cfg.w_reg), 1e9,
-                      None, None, _lib.ptr(self.loss), _lib.ptr(self.log), _lib.ptr(self.ctr),
-                      int(cfg.iters), st)
+                      _lib.ptr(self.loss), _lib.ptr(self.log), _lib.ptr(self.ctr), int(cfg.iters),
+                      _lib.ptr(self.state), float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4,
+                      _lib.ptr(self.loss_scratch), st)
+            _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
+                      ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
         else:
             self._chamfer_nnd(st)
-        _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
-                  ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
-        _lib.call("pcr_ndp_control", _lib.ptr(self.loss), _lib.ptr(self.state),
-                  float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4, st)
+            _lib.call("pcr_ndp_train_backward", desc, _lib.ptr(self.part), self.CHUNK,
+                      ctypes.cast(self.grad_ptrs, ctypes.c_void_p), st)
+            _lib.call("pcr_ndp_control", _lib.ptr(self.loss), _lib.ptr(self.state),
+                      float(cfg.break_threshold_ratio), int(cfg.max_break_count), 1e-4, st)
         _lib.call("pcr_adam_masked", _lib.ptr(self.table), len(self.params), self.max_numel,
                   _lib.ptr(self.state), float(cfg.lr), 0.9, 0.999, 1e-8, st)
 

@@ -136,3 +136,36 @@ def test_fused_optimisation_close_to_autograd_path():
     for x, y in zip(a[3], b[3]):
         np.testing.assert_allclose(x["losses"], y["losses"], rtol=1e-4)
     assert torch.allclose(a[0], b[0], atol=1e-4)
+
+
+def test_fused_loss_and_control_match_glue_then_control():
+    """pcr_ndp_chamfer_loss (32-block loss + the early-stop rule in one launch) ==
+    pcr_ndp_chamfer_glue followed by pcr_ndp_control: the loss to 1e-6 relative
+    (another f32 summation order), the log / counter, and the rule's state over
+    a sequence of losses that counts breaks and stops."""
+    rng = np.random.default_rng(9)
+    K, M, N = 5000, 20000, 20000
+    s = torch.from_numpy(rng.random(N).astype(np.float32) * 0.9).cuda()
+    st = _lib.stream_handle()
+    scratch = torch.zeros(int(_lib.load().pcr_ndp_loss_scratch_bytes()), dtype=torch.uint8, device="cuda")
+    state = [torch.tensor([1.0, 0, 1e6, 0, 0, 0, 0, 0], dtype=torch.float64, device="cuda") for _ in range(2)]
+    loss = [torch.zeros((), device="cuda") for _ in range(2)]
+    log = [torch.zeros(41, device="cuda") for _ in range(2)]
+    ctr = [torch.zeros(1, dtype=torch.long, device="cuda") for _ in range(2)]
+    base1 = rng.random(K).astype(np.float32) * 0.01
+    base2 = rng.random(M).astype(np.float32) * 0.01
+    for it in range(12):
+        f = 1.0 if it < 4 else 1.0 + 1e-5 * it  # flat losses: the break counter runs
+        d1 = torch.from_numpy(base1 * f).cuda()
+        d2 = torch.from_numpy(base2 * f).cuda()
+        _lib.call("pcr_ndp_chamfer_glue", _lib.ptr(d1), K, _lib.ptr(d2), M, _lib.ptr(s), N, 0.05, 1e9,
+                  None, None, _lib.ptr(loss[0]), _lib.ptr(log[0]), _lib.ptr(ctr[0]), 40, st)
+        _lib.call("pcr_ndp_control", _lib.ptr(loss[0]), _lib.ptr(state[0]), 0.001, 3, 1e-4, st)
+        _lib.call("pcr_ndp_chamfer_loss", _lib.ptr(d1), K, _lib.ptr(d2), M, _lib.ptr(s), N, 0.05, 1e9,
+                  _lib.ptr(loss[1]), _lib.ptr(log[1]), _lib.ptr(ctr[1]), 40, _lib.ptr(state[1]), 0.001, 3, 1e-4,
+                  _lib.ptr(scratch), st)
+        torch.cuda.synchronize()
+        assert abs(float(loss[1]) - float(loss[0])) <= 1e-6 * abs(float(loss[0]))
+        assert torch.equal(state[0][[0, 1, 3, 5, 6]], state[1][[0, 1, 3, 5, 6]]), it
+    assert int(ctr[0]) == int(ctr[1]) == 12 and float(state[1][0]) == 0.0
+    assert int(scratch.view(torch.int32)[96]) == 0  # the completion counter is left at zero

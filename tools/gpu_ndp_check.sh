@@ -12,5 +12,7 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 tail -3 gpurun_out/${T}_tests.txt
 timeout -k 10 200 python tools/c5_run.py > gpurun_out/${T}_c5.txt 2>&1 || { tail -20 gpurun_out/${T}_c5.txt; exit 12; }
 grep rep gpurun_out/${T}_c5.txt
+timeout -k 10 200 python tools/ndp_opt_bench.py > gpurun_out/${T}_f4.txt 2>&1 || { tail -20 gpurun_out/${T}_f4.txt; exit 14; }
+tail -3 gpurun_out/${T}_f4.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_c5prof -o run -- python3 tools/c5_run.py > gpurun_out/${T}_c5prof.log 2>&1 || exit 13
 echo done
