@@ -739,7 +739,7 @@ __global__ __launch_bounds__(256) void featnn_rescan3(RescanArgs5 a) {
             const float lim = m32 * kRel + 1e-30f;
             unsigned pend = 0;
 #pragma unroll
-            for (int t = 0; t < kPer8; ++t) pend |= (a32v[t] <= lim ? 1u : 0u) << t;
+            for (int t = 0; t < kPer8; ++t) pend |= (sl + 8 * t < ncand && a32v[t] <= lim ? 1u : 0u) << t;
             while (pend) {
                 const int t = __builtin_ctz(pend);
                 pend &= pend - 1;
