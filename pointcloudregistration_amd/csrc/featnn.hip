@@ -1179,7 +1179,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.W = 8;                                          // waves (32-row tiles) per workgroup
     v.nrb = cdiv(cdiv(Nmax, 32), v.W);                // dual screen row blocks
     // row tiles, padded to whole blocks of the dual screen (8 tiles) and of the
-    // row screens (8 waves x kRowTiles tiles; the sentinel rows are valid encodings)
+    // row screens (8 waves x row_tiles(S) tiles; the sentinel rows are valid encodings)
     v.ntn = cdiv(cdiv(Nmax, 32), 16) * 16;
     v.ntm = cdiv(cdiv(Mmax, 32), 8) * 8;              // column tiles, padded to whole groups (G | 8)
     v.ctbits = 1;
@@ -1326,7 +1326,9 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
 }
 
 // row tiles per wave of the row screens (featnn_row7)
-constexpr int kRowTiles = 2;
+// (two up to D = 32; one above, where two tiles' accumulators and fragments
+// spilled at S = 4: 256 VGPRs + 179 spilled)
+constexpr int row_tiles(int S) { return S <= 2 ? 2 : 1; }
 
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
@@ -1336,7 +1338,7 @@ static int launch_row7(const RowArgs5 &r, int S, hipStream_t s) {
     switch (S) {
 #define PCR_R7CASE(K)                                                                            \
     case K:                                                                                      \
-        hipLaunchKernelGGL((featnn_row7<K, (K <= 2 ? 8 : 4), kIdx, kRowTiles>), dim3((unsigned)nblk), \
+        hipLaunchKernelGGL((featnn_row7<K, (K <= 2 ? 8 : 4), kIdx, row_tiles(K)>), dim3((unsigned)nblk), \
                            dim3(512), 0, s, r);                                                  \
         break;
         PCR_R7CASE(1) PCR_R7CASE(2) PCR_R7CASE(3) PCR_R7CASE(4)
@@ -1383,7 +1385,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     RowArgs5 r;
     r.Ap = v.Ap; r.Bp = v.Bp; r.rnr = v.fnr; r.cmax = v.gmax; r.n_rows = n_src; r.n_cols = n_tgt;
     r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
-    r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * kRowTiles); r.D = D; r.ctbits = 1;
+    r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * row_tiles(v.S)); r.D = D; r.ctbits = 1;
     while ((1 << r.ctbits) < ntm) ++r.ctbits;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;
@@ -1405,7 +1407,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         RowArgs5 r2 = r;
         r2.Ap = v.Bp; r2.Bp = v.Ap; r2.rnr = v.gnr; r2.cmax = v.fmax; r2.n_rows = n_tgt;
         r2.n_cols = n_src; r2.rlist = ma.jlist; r2.rcount = ma.nj; r2.Rmax = Mmax; r2.Cmax = Nmax;
-        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * kRowTiles);
+        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * row_tiles(v.S));
         r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
         r2.w1 = w1; r2.w2 = w2;
         prof_begin(s, kProfFeatScreen2);
