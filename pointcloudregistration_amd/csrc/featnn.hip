@@ -221,11 +221,15 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
         }
         dst[(size_t)c * 64] = o;
     }
-    if (h == 0) {
-        const float r = valid ? (float)__builtin_sqrt(acc) : 0.0f;
-        nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
-        if (valid) atomicMax(nmax + p, __float_as_uint(r));
-    }
+    // the pair's max norm: one atomic per wave (a per-lane atomicMax on the
+    // pair's one word serialised 8K same-address atomics per cloud)
+    // (max of the bit patterns: the same word the per-lane atomics left, NaN included)
+    const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
+    if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+    unsigned rb = __float_as_uint(r);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
+    if (l == 0 && rb != 0u) atomicMax(nmax + p, rb);
 }
 
 // Register-resident pack for a compile-time D (the hot D = 32): one lane per
@@ -316,11 +320,15 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
         const f16x8 a = frag(2 * c), b = frag(2 * c + 1);
         dst[(size_t)c * 64] = h ? b : a;
     }
-    if (h == 0) {
-        const float r = valid ? (float)__builtin_sqrt(acc) : 0.0f;
-        nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
-        if (valid) atomicMax(nmax + p, __float_as_uint(r));
-    }
+    // the pair's max norm: one atomic per wave (a per-lane atomicMax on the
+    // pair's one word serialised 8K same-address atomics per cloud)
+    // (max of the bit patterns: the same word the per-lane atomics left, NaN included)
+    const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
+    if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+    unsigned rb = __float_as_uint(r);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
+    if (l == 0 && rb != 0u) atomicMax(nmax + p, rb);
 }
 
 // certification threshold for a top-2 gap in scaled units (see header)
