@@ -149,14 +149,18 @@ typedef struct pcr_ransac_params {
  * stats (P,5) = {iterations, validated, best_itr, status(1 ok/0 none/-1 bad
  * input), n_correspondences}, corr_tgt (P,Nmax) target index per source point
  * or -1 (optional), inlier_mask (P, ceil(Nmax/32)) bitset (optional).
- * Blocks the host between rounds of hypotheses (one 32-byte readback per
- * round: [0,1024), then 4096 at a time while a pair's bound est_k lies beyond).
+ * Asynchronous on the stream (no host round trip): hypotheses run in two
+ * rounds, [0,1024) and [1024, max_iteration), the second launched behind the
+ * first and returning at once when no pair's bound est_k lies beyond 1024.
  * Verification runs speculatively on persistent workgroups, the sequential rule
- * is replayed afterwards: results do not depend on the scheduling.  Workspace
- * per pair: ~135 B per hypothesis of the largest round (4096 when
- * max_iteration > 1024, else max_iteration rounded up to 256: ~540 KB / ~135 KB
- * per pair), 2 x Nmax x 4 B of target buffers, plus up to 256 MB per device of
- * per-hypothesis target slots (fewer slots only add one sweep per pair).
+ * is replayed afterwards: results do not depend on the scheduling or the round
+ * split.  Workspace per pair: ~135 B per hypothesis slot of the larger round
+ * (max_iteration - 1024 rounded up to 256, at least 1024: ~13 MB per pair at
+ * max_iteration 100000), 2 x Nmax x 4 B of target buffers, plus up to 256 MB
+ * per device of per-hypothesis target slots (fewer slots only add one sweep per
+ * pair).  Past 2^26 slots in all (P x max_iteration), or with
+ * PCR_RANSAC_SYNC=1, the host instead runs rounds of 4096 while a pair is
+ * still active (one 32-byte readback per round, ~540 KB per pair).
  * ------------------------------------------------------------------------- */
 int pcr_ransac_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t Nmax,
                      int32_t Mmax, const int32_t *n_src, const int32_t *n_tgt,

@@ -122,7 +122,13 @@ struct RArgs {
     RHeader *hdr;
     int split;              // workgroups per task (1, 2, 4 or 8: more when the pairs are few)
     TaskPart *parts;        // (P, hcap, split) when split > 1
+    const int *prev_active; // later rounds launched without a host decision: the previous
+                            // round's active_count (0: every kernel of this round returns)
 };
+
+__device__ __forceinline__ bool round_off(const RArgs &a) {
+    return a.prev_active != nullptr && *a.prev_active == 0;
+}
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
     return n ? min(max(n[p], 0), mx) : mx;
@@ -196,34 +202,37 @@ __device__ bool make_hypothesis(const RArgs &a, int p, int K, uint32_t pid, int 
     return true;
 }
 
-// grid (ceil(span / 256), P): thread = iteration b0 + x*256 + tid of pair y
+// grid (x, P): block x takes the 256-iteration chunks x, x + gridDim.x, ... of
+// the round (a later round can span up to max_iter, but stops at the pair's
+// bound); thread = iteration b0 + chunk*256 + tid of pair y
 template <int RN>
 __global__ __launch_bounds__(kHypThreads) void ransac_hyp_kernel(RArgs a) {
+    if (round_off(a)) return;
     const int p = blockIdx.y;
-    const int off = blockIdx.x * kHypThreads + threadIdx.x;
-    const int itr = a.b0 + off;
-    bool live = off < a.hcap && itr < a.b1 && pair_ok(a, p, RN);
-    int lim = a.max_iter;
-    if (live && a.b0 > 0) {   // later rounds: only pairs still running, below their bound
+    int lim = min(a.b1, a.max_iter);
+    if (a.b0 > 0) {   // later rounds: only pairs still running, below their bound
         const RState &st = a.state[p];
-        live = st.active != 0;
+        if (!st.active) return;
         lim = min(lim, st.est_k);
     }
-    live = live && itr < lim;
-    double T[12];
-    bool pass = false;
-    if (live) {
-        const int K = a.n_corres ? min(max(a.n_corres[p], 0), a.Kmax) : a.Kmax;
-        const uint32_t pid = a.pair_ids ? a.pair_ids[p] : (uint32_t)p;
-        pass = make_hypothesis<RN>(a, p, K, pid, itr, T);
-    }
-    const unsigned long long bal = __ballot(pass);
-    if (off < a.hcap && (threadIdx.x & 63) == 0)
-        a.hypbits[(size_t)p * (a.hcap / 64) + (off >> 6)] = bal;
-    if (pass) {
-        double *o = a.hypT + ((size_t)p * a.hcap + off) * 12;
+    const bool okp = pair_ok(a, p, RN);
+    const int K = a.n_corres ? min(max(a.n_corres[p], 0), a.Kmax) : a.Kmax;
+    const uint32_t pid = a.pair_ids ? a.pair_ids[p] : (uint32_t)p;
+    for (int cx = blockIdx.x; a.b0 + cx * kHypThreads < lim; cx += gridDim.x) {
+        const int off = cx * kHypThreads + threadIdx.x;
+        const int itr = a.b0 + off;
+        const bool live = okp && off < a.hcap && itr < lim;
+        double T[12];
+        bool pass = false;
+        if (live) pass = make_hypothesis<RN>(a, p, K, pid, itr, T);
+        const unsigned long long bal = __ballot(pass);
+        if (off < a.hcap && (threadIdx.x & 63) == 0)
+            a.hypbits[(size_t)p * (a.hcap / 64) + (off >> 6)] = bal;
+        if (pass) {
+            double *o = a.hypT + ((size_t)p * a.hcap + off) * 12;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) o[k] = T[k];
+            for (int k = 0; k < 12; ++k) o[k] = T[k];
+        }
     }
 }
 
@@ -359,6 +368,7 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
 // Round setup, one wave per pair: the round-0 state, then the round's tasks =
 // the passing hypotheses below min(b1, max_iter, est_k), in iteration order.
 __global__ __launch_bounds__(64) void ransac_task_kernel(RArgs a, int RN) {
+    if (round_off(a)) return;
     const int p = blockIdx.x, lane = threadIdx.x;
     RState *sp = a.state + p;
     if (a.b0 == 0 && lane == 0) {
@@ -468,6 +478,7 @@ __device__ inline void finish_task(const RArgs &a, TaskRes *rt, int p, int r, in
 //    that can only fall further; a task at or beyond it is never validated.
 template <bool kLds, int RN>
 __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
+    if (round_off(a)) return;
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     Shared &sh = *reinterpret_cast<Shared *>(dsm);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -563,6 +574,7 @@ __global__ __launch_bounds__(kThreads) void ransac_sweep_kernel(RArgs a) {
 // kept, and -- once the pair is finished -- its outputs.
 template <bool kLds, int RN>
 __global__ __launch_bounds__(kThreads) void ransac_replay_kernel(RArgs a) {
+    if (round_off(a)) return;
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     Shared &sh = *reinterpret_cast<Shared *>(dsm);
     const int p = blockIdx.x, tid = threadIdx.x;
@@ -698,9 +710,23 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.words = (Nmax + 31) / 32;
     a.order = nullptr;
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
+    // Rounds.  Device-gated (default): [0, kRound0) and, when max_iteration is
+    // larger, ONE more round [kRound0, max_iteration) launched right behind it,
+    // whose kernels return at once when no pair is still running (the previous
+    // round's active_count) and otherwise stop at each pair's bound -- no host
+    // round trip, so the host keeps queueing the next stages (and the call can
+    // be captured).  Its slots hold max_iteration - kRound0 hypotheses per pair;
+    // past kAsyncSlots slots in all (huge batches) or with PCR_RANSAC_SYNC=1 the
+    // host loop of kRoundN-hypothesis rounds runs instead (same results: a
+    // round boundary cannot change the sequential decisions).
+    constexpr long long kAsyncSlots = 1LL << 26;
+    const int span1 = a.max_iter > kRound0 ? (a.max_iter - kRound0 + 255) / 256 * 256 : 0;
+    const bool gated = env_int("PCR_RANSAC_SYNC", 0) == 0 &&
+                       (long long)P * std::max(span1, kRound0) <= kAsyncSlots;
     // hypotheses per round slot: the largest round that can run (kRound0 when
     // max_iteration fits the first round), a multiple of 256
-    a.hcap = a.max_iter > kRound0 ? kRoundN : std::max(256, (std::max(a.max_iter, 1) + 255) / 256 * 256);
+    a.hcap = a.max_iter > kRound0 ? (gated ? std::max(span1, kRound0) : kRoundN)
+                                  : std::max(256, (std::max(a.max_iter, 1) + 255) / 256 * 256);
     // target slots of the first tasks of every pair (the best's are kept from
     // there; a best without one is swept again at the end): up to 32 per pair
     // within 256 MB
@@ -711,13 +737,14 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.state = (RState *)workspace(22, sizeof(RState) * (size_t)P);
     a.hypT = (double *)workspace(23, sizeof(double) * 12 * (size_t)P * a.hcap);
     a.hypbits = (unsigned long long *)workspace(24, sizeof(unsigned long long) * (size_t)P * (a.hcap / 64));
-    a.hdr = (RHeader *)workspace(25, sizeof(RHeader) + sizeof(int) * (size_t)P);
+    a.hdr = (RHeader *)workspace(25, 2 * sizeof(RHeader) + sizeof(int) * (size_t)P);
     a.tasks = (int *)workspace(29, sizeof(int) * (size_t)P * a.hcap);
     a.res = (TaskRes *)workspace(30, sizeof(TaskRes) * (size_t)P * a.hcap);
     a.slots = (int32_t *)workspace(31, a.nslots > 0 ? per * a.nslots : 16);
     PCR_REQUIRE(a.bestbuf && a.state && a.hypT && a.hypbits && a.hdr && a.tasks && a.res && a.slots,
                 PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
-    a.ntask = (int *)(a.hdr + 1);
+    a.ntask = (int *)(a.hdr + 2);
+    a.prev_active = nullptr;
     a.grid = GridBatch{};
     a.grid.S = 1;
     a.grid.cell = 1.0;
@@ -774,9 +801,46 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     const int rnarg = a.rn;
     const bool stats_env = env_int("PCR_RANSAC_STATS", 0) != 0;
     prof_begin(s, kProfRansacValidate);
-    // rounds: [0, kRound0), then kRoundN at a time while a pair is still running
     a.b0 = 0;
     a.b1 = std::min(a.max_iter, kRound0);
+    if (gated) {
+        PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, 2 * sizeof(RHeader), s));
+        RHeader *h0 = a.hdr;
+        for (int round = 0; round < (a.max_iter > kRound0 ? 2 : 1); ++round) {
+            if (round == 1) {
+                a.b0 = kRound0;
+                a.b1 = a.max_iter;
+                a.hdr = h0 + 1;
+                a.prev_active = &h0->active_count;
+            }
+            void *args[] = {&a};
+            const int nx = (a.b1 - a.b0 + kHypThreads - 1) / kHypThreads;
+            if (nx > 0) {
+                PCR_HIP_CHECK(hipLaunchKernel(hfn, dim3(round == 0 ? nx : std::min(nx, 16), P),
+                                              dim3(kHypThreads), args, 0, s));
+                PCR_LAUNCH_CHECK();
+            }
+            void *targs[] = {&a, (void *)&rnarg};
+            PCR_HIP_CHECK(hipLaunchKernel((const void *)ransac_task_kernel, dim3(P), dim3(64), targs, 0, s));
+            PCR_LAUNCH_CHECK();
+            PCR_HIP_CHECK(hipLaunchKernel(sfn, dim3(nwg), dim3(kThreads), args, sm, s));
+            PCR_LAUNCH_CHECK();
+            PCR_HIP_CHECK(hipLaunchKernel(rfn, dim3(P), dim3(kThreads), args, sm, s));
+            PCR_LAUNCH_CHECK();
+        }
+        prof_end(s, kProfRansacValidate);
+        if (stats_env) {  // diagnostics only: one host read of both headers
+            RHeader h[2];
+            PCR_HIP_CHECK(hipMemcpyAsync(h, h0, sizeof(h), hipMemcpyDeviceToHost, s));
+            PCR_HIP_CHECK(hipStreamSynchronize(s));
+            for (int r = 0; r < 2; ++r)
+                fprintf(stderr, "ransac gated round %d: tasks done %d cut %d skipped %d, chunks %d, active after %d, "
+                        "bad %d\n", r, h[r].n_done, h[r].n_cut, h[r].n_skip, h[r].n_chunks, h[r].active_count,
+                        h[r].bad);
+        }
+        return PCR_OK;
+    }
+    // host loop: [0, kRound0), then kRoundN at a time while a pair is still running
     for (;;) {
         PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, sizeof(RHeader), s));
         const int span = a.b1 - a.b0;

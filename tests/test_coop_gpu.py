@@ -50,11 +50,11 @@ def coop_g():
 
 @pytest.fixture()
 def ransac_sched():
-    keys = ("PCR_RANSAC_WGS", "PCR_RANSAC_SLOTS", "PCR_RANSAC_SPLIT")
+    keys = ("PCR_RANSAC_WGS", "PCR_RANSAC_SLOTS", "PCR_RANSAC_SPLIT", "PCR_RANSAC_SYNC")
     old = {k: os.environ.get(k) for k in keys}
 
-    def set_sched(wgs, slots, split=None):
-        for k, v in zip(keys, (wgs, slots, split)):
+    def set_sched(wgs, slots, split=None, sync=None):
+        for k, v in zip(keys, (wgs, slots, split, sync)):
             if v is None:
                 os.environ.pop(k, None)
             else:
@@ -93,11 +93,14 @@ def test_ransac_speculative_bitexact_vs_oracle(oracle, ransac_sched, wgs, slots,
 
 def test_ransac_multi_round_low_inlier_ratio(oracle, ransac_sched):
     """Noisy descriptors -> a low inlier ratio -> est_k beyond the first round of
-    1024 hypotheses: the later rounds continue the same sequential loop."""
+    1024 hypotheses: the later rounds continue the same sequential loop -- the
+    device-gated second round [1024, max_iteration) and the host loop of
+    4096-hypothesis rounds (PCR_RANSAC_SYNC=1) alike."""
     P, n = 2, 2048
     B = synth.make_batch(P, n=n, m=n, d=32, base_seed=3100, feat_noise=2.2)
-    for wgs, slots, split in ((None, None, None), (1, 0, 2), (5, 3, 1), (3, 1, 2)):
-        ransac_sched(wgs, slots, split)
+    for wgs, slots, split, sync in ((None, None, None, None), (1, 0, 2, None), (5, 3, 1, None),
+                                    (3, 1, 2, None), (None, None, None, 1), (3, 1, 2, 1)):
+        ransac_sched(wgs, slots, split, sync)
         prm = reg.RansacParams(max_correspondence_distance=0.04, seed=3, max_iteration=6000)
         res = reg.register_feature_ransac_batch(B.src, B.tgt, B.src_feat, B.tgt_feat, prm)
         st = _np(res.stats)
