@@ -204,6 +204,39 @@ int pcr_icp_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t
                   int32_t *corr_tgt, pcr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * The C4 pipeline step (DataPreparation/RANSAC.py:109-122 per pair, with the
+ * QualityCheck.py:25-31 Chamfer) for P resident pairs, no host round trip:
+ * mutual feature correspondences (a5) -> RANSAC (a6/a7) -> ICP from the RANSAC
+ * T (a8) -> aligned source (f64 T, f32 out) -> nnd both ways (a1) -> records.
+ * Every buffer is device memory owned by the caller (inlier_mask optional).
+ * records (P, 40) f64: [0,16) T_ransac, [16,32) T_icp, 32/33 RANSAC fitness /
+ * rmse, 34/35 ICP fitness / rmse, 36 Chamfer = mean(d1) + mean(d2) (f64 sums
+ * of the f32 distances in index order), 37 RANSAC iterations, 38 RANSAC
+ * status, 39 correspondences after the mutual filter.
+ * pcr_pipeline_records: the records alone, from buffers the stage calls filled.
+ * ------------------------------------------------------------------------- */
+typedef struct pcr_pipeline_io {
+    const float *src_xyz, *tgt_xyz;    /* (P,N,3), (P,M,3) */
+    const float *src_feat, *tgt_feat;  /* (P,N,D), (P,M,D) */
+    int32_t P, N, M, D;
+    const uint32_t *pair_ids;          /* (P) or null */
+    int32_t *nn12;                     /* (P,N) */
+    int32_t *corres, *n_corres;        /* (P,N,2), (P) */
+    double *T_ransac, *fit_ransac;     /* (P,16), (P,2) */
+    int32_t *stats_ransac;             /* (P,5) */
+    uint32_t *inlier_mask;             /* (P, ceil(N/32)) or null */
+    double *T_icp, *fit_icp;           /* (P,16), (P,2) */
+    int32_t *stats_icp;                /* (P,2) */
+    float *aligned;                    /* (P,N,3) */
+    float *d1, *d2;                    /* (P,N), (P,M) */
+    int32_t *i1, *i2;                  /* (P,N), (P,M) */
+    double *records;                   /* (P,40) */
+} pcr_pipeline_io;
+int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_params *ransac,
+                      const pcr_icp_params *icp, pcr_stream_t stream);
+int pcr_pipeline_records(const pcr_pipeline_io *io, pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * radius-limited 1-NN (Open3D KDTreeFlann::SearchHybrid(r, max_nn=1), used by
  * RANSAC verification / ICP): for each f64 query (P,Qmax,3) the nearest target
  * point with d^2 < float(r*r), lowest index on ties; idx -1 if none, d2 optional.

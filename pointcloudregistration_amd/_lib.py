@@ -87,6 +87,8 @@ SIGNATURES = {
     "pcr_ndp_chamfer_step": [_p, _p],
     "pcr_ndp_chamfer_loss": [_p, _i32, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _i32, _p, _f64, _i32,
                              _f64, _p, _p],
+    "pcr_pipeline_step": [_p, _p, _p, _p],
+    "pcr_pipeline_records": [_p, _p],
     "pcr_hybrid_search": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],
     "pcr_estimate_normals": [_p, _i32, _i32, _p, _f64, _i32, _p, _p, _p],
     "pcr_compute_fpfh": [_p, _p, _i32, _i32, _p, _f64, _i32, _p, _p, _p, _p],

@@ -1,4 +1,8 @@
-// Composite entry: feature matching -> correspondences -> RANSAC for P pairs.
+// Composite entries: feature matching -> correspondences -> RANSAC for P pairs
+// (pcr_register_feature_ransac), and the whole C4 pipeline step
+// (pcr_pipeline_step) as one host call with no round trip -- the Python stage
+// calls cost ~0.3 ms of host time per step, which a 32-pair shard (2.3 ms of
+// kernels) could not hide.
 #include "pcr_internal.h"
 
 namespace pcr {
@@ -16,6 +20,10 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
                 const int32_t *n_corres, int Kmax, const uint32_t *pair_ids,
                 const pcr_ransac_params *prm, double *T_out, double *fit_out, int32_t *stats,
                 int32_t *corr_tgt, uint32_t *mask, hipStream_t s);
+int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, const int32_t *n_src,
+             const int32_t *n_tgt, const double *init, const pcr_icp_params *prm, double *T_out,
+             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s);
+int pipeline_records(const pcr_pipeline_io *io, hipStream_t s);
 }  // namespace pcr
 
 extern "C" int pcr_register_feature_ransac(const float *src_xyz, const float *tgt_xyz,
@@ -53,4 +61,51 @@ extern "C" int pcr_register_feature_ransac(const float *src_xyz, const float *tg
     if (rc != PCR_OK) return rc;
     return pcr::ransac_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, corres, n_corres, Nmax,
                             pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask, s);
+}
+
+static int io_check(const pcr_pipeline_io *io) {
+    PCR_REQUIRE(io, PCR_ERR_ARG, "pipeline: null io");
+    PCR_REQUIRE(io->P >= 0 && io->N >= 0 && io->M >= 0 && io->D >= 1, PCR_ERR_ARG, "pipeline: bad size");
+    PCR_REQUIRE(io->P <= 65535, PCR_ERR_ARG, "pipeline: P=%d > 65535", io->P);
+    PCR_REQUIRE(io->T_ransac && io->fit_ransac && io->stats_ransac && io->T_icp && io->fit_icp &&
+                    io->stats_icp && io->n_corres && io->d1 && io->d2 && io->records,
+                PCR_ERR_ARG, "pipeline: null buffer");
+    return PCR_OK;
+}
+
+extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_params *rp,
+                                 const pcr_icp_params *ip, pcr_stream_t stream) {
+    pcr::clear_error();
+    int rc = io_check(io);
+    if (rc != PCR_OK) return rc;
+    PCR_REQUIRE(rp && ip && io->src_xyz && io->tgt_xyz && io->src_feat && io->tgt_feat && io->nn12 &&
+                    io->corres && io->aligned && io->i1 && io->i2,
+                PCR_ERR_ARG, "pipeline: null pointer");
+    PCR_REQUIRE(io->N >= 1 && io->M >= 1, PCR_ERR_ARG, "pipeline: empty clouds");
+    if (io->P == 0) return PCR_OK;
+    hipStream_t s = pcr::as_stream(stream);
+    const int P = io->P, N = io->N, M = io->M;
+    rc = pcr::feature_corres_impl(io->src_feat, io->tgt_feat, P, N, M, io->D, nullptr, nullptr,
+                                  rp->mutual_filter, rp->ransac_n, io->nn12, io->corres, io->n_corres, s);
+    if (rc != PCR_OK) return rc;
+    rc = pcr::ransac_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->corres, io->n_corres, N,
+                          io->pair_ids, rp, io->T_ransac, io->fit_ransac, io->stats_ransac, nullptr,
+                          io->inlier_mask, s);
+    if (rc != PCR_OK) return rc;
+    rc = pcr::icp_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->T_ransac, ip, io->T_icp,
+                       io->fit_icp, io->stats_icp, nullptr, s);
+    if (rc != PCR_OK) return rc;
+    rc = pcr_transform_batch(io->src_xyz, P, N, io->T_icp, io->aligned, stream);
+    if (rc != PCR_OK) return rc;
+    rc = pcr_nnd_forward(io->aligned, io->tgt_xyz, P, N, M, io->d1, io->d2, io->i1, io->i2, stream);
+    if (rc != PCR_OK) return rc;
+    return pcr::pipeline_records(io, s);
+}
+
+extern "C" int pcr_pipeline_records(const pcr_pipeline_io *io, pcr_stream_t stream) {
+    pcr::clear_error();
+    int rc = io_check(io);
+    if (rc != PCR_OK) return rc;
+    if (io->P == 0) return PCR_OK;
+    return pcr::pipeline_records(io, pcr::as_stream(stream));
 }

@@ -125,3 +125,49 @@ extern "C" int pcr_transform_batch(const float *xyz, int32_t B, int32_t N, const
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
+
+// ---------------------------------------------------------------------------
+// C4 pipeline records (pcr_pipeline_step): one 256-thread block per pair; the
+// Chamfer means as f64 sums of the f32 distances in index order (a fixed
+// 256-lane split and tree), then / N and / M.
+// ---------------------------------------------------------------------------
+namespace pcr {
+namespace {
+__global__ __launch_bounds__(256) void pipeline_records_kernel(pcr_pipeline_io io) {
+    const int p = blockIdx.x, t = threadIdx.x;
+    __shared__ double red[2][256];
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = t; i < io.N; i += 256) s1 += (double)io.d1[(size_t)p * io.N + i];
+    for (int i = t; i < io.M; i += 256) s2 += (double)io.d2[(size_t)p * io.M + i];
+    red[0][t] = s1;
+    red[1][t] = s2;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) { red[0][t] += red[0][t + h]; red[1][t] += red[1][t + h]; }
+        __syncthreads();
+    }
+    double *r = io.records + (size_t)p * 40;
+    if (t < 16) {
+        r[t] = io.T_ransac[(size_t)p * 16 + t];
+        r[16 + t] = io.T_icp[(size_t)p * 16 + t];
+    }
+    if (t == 0) {
+        r[32] = io.fit_ransac[2 * p];
+        r[33] = io.fit_ransac[2 * p + 1];
+        r[34] = io.fit_icp[2 * p];
+        r[35] = io.fit_icp[2 * p + 1];
+        r[36] = red[0][0] / (double)io.N + red[1][0] / (double)io.M;
+        r[37] = (double)io.stats_ransac[(size_t)p * 5];
+        r[38] = (double)io.stats_ransac[(size_t)p * 5 + 3];
+        r[39] = (double)io.n_corres[p];
+    }
+}
+}  // namespace
+
+int pipeline_records(const pcr_pipeline_io *io, hipStream_t s) {
+    PCR_REQUIRE(io->N >= 1 && io->M >= 1, PCR_ERR_ARG, "pipeline_records: empty clouds");
+    hipLaunchKernelGGL(pipeline_records_kernel, dim3(io->P), dim3(256), 0, s, *io);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+}  // namespace pcr

@@ -17,13 +17,23 @@ chamfer, stats.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import torch
 
-from . import nndistance, registration as reg
+from . import _lib, nndistance, registration as reg
 
 RECORD_WIDTH = 40  # f64 per pair, see PairPipeline.records()
+
+
+class _PipelineIO(ctypes.Structure):
+    """pcr_pipeline_io (include/pcr_api.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("src_xyz", "tgt_xyz", "src_feat", "tgt_feat")] + \
+        [(n, ctypes.c_int32) for n in ("P", "N", "M", "D")] + \
+        [(n, ctypes.c_void_p) for n in ("pair_ids", "nn12", "corres", "n_corres", "T_ransac", "fit_ransac",
+                                        "stats_ransac", "inlier_mask", "T_icp", "fit_icp", "stats_icp",
+                                        "aligned", "d1", "d2", "i1", "i2", "records")]
 
 
 @dataclass
@@ -57,44 +67,84 @@ class PairPipeline:
         self.pair_ids = None if pair_ids is None else d(pair_ids, torch.int32)
         self.device = dev
         self.stage_events = None
-        # preallocated Chamfer buffers
-        self.d1 = torch.empty(self.P, self.N, device=dev)
-        self.d2 = torch.empty(self.P, self.M, device=dev)
-        self.i1 = torch.empty(self.P, self.N, dtype=torch.int32, device=dev)
-        self.i2 = torch.empty(self.P, self.M, dtype=torch.int32, device=dev)
+        # preallocated stage outputs: the one-call step (pcr_pipeline_step) writes
+        # them all; the staged path (time_stages) fills the same records
+        P, N, M = self.P, self.N, self.M
+        i32, f64 = dict(dtype=torch.int32, device=dev), dict(dtype=torch.float64, device=dev)
+        self.d1 = torch.empty(P, N, device=dev)
+        self.d2 = torch.empty(P, M, device=dev)
+        self.i1 = torch.empty(P, N, **i32)
+        self.i2 = torch.empty(P, M, **i32)
         self.aligned = torch.empty_like(self.src)
+        self.b_nn12 = torch.empty(P, N, **i32)
+        self.b_corres = torch.empty(P, N, 2, **i32)
+        self.b_ncor = torch.empty(P, **i32)
+        self.T_r, self.fr_r, self.st_r = (torch.empty(P, 4, 4, **f64), torch.empty(P, 2, **f64),
+                                          torch.empty(P, 5, **i32))
+        self.mask = torch.empty(P, (N + 31) // 32, **i32)
+        self.T_i, self.fr_i, self.st_i = (torch.empty(P, 4, 4, **f64), torch.empty(P, 2, **f64),
+                                          torch.empty(P, 2, **i32))
+        self.rec = torch.zeros(P, RECORD_WIDTH, **f64)
+        io = _PipelineIO()
+        io.src_xyz, io.tgt_xyz = self.src.data_ptr(), self.tgt.data_ptr()
+        io.src_feat, io.tgt_feat = self.src_feat.data_ptr(), self.tgt_feat.data_ptr()
+        io.P, io.N, io.M, io.D = P, N, M, self.src_feat.shape[2]
+        io.pair_ids = None if self.pair_ids is None else self.pair_ids.data_ptr()
+        for name, t in (("nn12", self.b_nn12), ("corres", self.b_corres), ("n_corres", self.b_ncor),
+                        ("T_ransac", self.T_r), ("fit_ransac", self.fr_r), ("stats_ransac", self.st_r),
+                        ("inlier_mask", self.mask), ("T_icp", self.T_i), ("fit_icp", self.fr_i),
+                        ("stats_icp", self.st_i), ("aligned", self.aligned), ("d1", self.d1),
+                        ("d2", self.d2), ("i1", self.i1), ("i2", self.i2), ("records", self.rec)):
+            setattr(io, name, t.data_ptr())
+        self.io = io
+        self.c_ransac, self.c_icp = params.ransac.to_c(), params.icp.to_c()
 
-    def run(self, time_stages=False):
-        ev = None
-        if time_stages:
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-            ev[0].record()
-        # feature NN + mutual filter (nn21 only where the filter reads it)
-        corres, ncor, nn12 = reg.feature_correspondences(
-            self.src_feat, self.tgt_feat, mutual_filter=self.params.ransac.mutual_filter,
-            ransac_n=self.params.ransac.ransac_n)
-        if ev:
-            ev[1].record()
-        rr = reg.ransac_batch(self.src, self.tgt, corres, ncor, self.params.ransac,
-                              pair_ids=self.pair_ids, want_corr=False, want_mask=True)
-        if ev:
-            ev[2].record()
-        ir = reg.icp_batch(self.src, self.tgt, rr.transformation, self.params.icp, want_corr=False)
-        if ev:
-            ev[3].record()
-        T = ir.transformation
-        aligned = reg.transform_batch(self.src, T, out=self.aligned)
-        if ev:
-            ev[4].record()
-        nndistance.nnd_forward_cuda(aligned, self.tgt, self.d1, self.d2, self.i1, self.i2)
-        chamfer = self.d1.mean(1, dtype=torch.float64) + self.d2.mean(1, dtype=torch.float64)
-        if ev:
-            ev[5].record()
-            self.stage_events = ev
+    def _publish(self, rr, ir, ncor, corres, nn12):
+        chamfer = self.rec[:, 36]
         self.last = (rr, ir, chamfer, ncor)
         self.corres = corres
         self.nn12 = nn12
         return rr, ir, chamfer
+
+    def run(self, time_stages=False):
+        if not time_stages:
+            # the whole step in one host call, no round trip (csrc/pipeline.cpp)
+            with torch.cuda.device(self.device):
+                _lib.call("pcr_pipeline_step", ctypes.byref(self.io), ctypes.byref(self.c_ransac),
+                          ctypes.byref(self.c_icp), _lib.stream_handle(self.device))
+            rr = reg.BatchResult(self.T_r, self.fr_r[:, 0], self.fr_r[:, 1], self.st_r, None, self.mask)
+            ir = reg.BatchResult(self.T_i, self.fr_i[:, 0], self.fr_i[:, 1], self.st_i, None)
+            return self._publish(rr, ir, self.b_ncor, self.b_corres, self.b_nn12)
+        # the same stages called one by one with events between them
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        ev[0].record()
+        # feature NN + mutual filter (nn21 only where the filter reads it)
+        corres, ncor, nn12 = reg.feature_correspondences(
+            self.src_feat, self.tgt_feat, mutual_filter=self.params.ransac.mutual_filter,
+            ransac_n=self.params.ransac.ransac_n)
+        ev[1].record()
+        rr = reg.ransac_batch(self.src, self.tgt, corres, ncor, self.params.ransac,
+                              pair_ids=self.pair_ids, want_corr=False, want_mask=True)
+        ev[2].record()
+        ir = reg.icp_batch(self.src, self.tgt, rr.transformation, self.params.icp, want_corr=False)
+        ev[3].record()
+        T = ir.transformation
+        aligned = reg.transform_batch(self.src, T, out=self.aligned)
+        ev[4].record()
+        nndistance.nnd_forward_cuda(aligned, self.tgt, self.d1, self.d2, self.i1, self.i2)
+        io = _PipelineIO.from_buffer_copy(self.io)
+        for name, t in (("nn12", nn12), ("corres", corres), ("n_corres", ncor),
+                        ("T_ransac", rr.transformation), ("fit_ransac", None), ("stats_ransac", rr.stats),
+                        ("T_icp", ir.transformation), ("fit_icp", None), ("stats_icp", ir.stats)):
+            if t is not None:
+                setattr(io, name, t.data_ptr())
+        # fitness / rmse come as column views of (P, 2) buffers: pass the buffers
+        io.fit_ransac = rr.fitness.data_ptr()
+        io.fit_icp = ir.fitness.data_ptr()
+        _lib.call("pcr_pipeline_records", ctypes.byref(io), _lib.stream_handle(self.device))
+        ev[5].record()
+        self.stage_events = ev
+        return self._publish(rr, ir, ncor, corres, nn12)
 
     def stage_ms(self):
         """(feature_match, corres+ransac, icp, transform, chamfer) in ms of the last run."""
@@ -102,17 +152,8 @@ class PairPipeline:
         return [ev[k].elapsed_time(ev[k + 1]) for k in range(5)]
 
     def records(self):
-        """(P, RECORD_WIDTH) f64 per-pair result records (device)."""
-        rr, ir, chamfer, ncor = self.last
-        rec = torch.zeros(self.P, RECORD_WIDTH, dtype=torch.float64, device=self.device)
-        rec[:, 0:16] = rr.transformation.reshape(self.P, 16)
-        rec[:, 16:32] = ir.transformation.reshape(self.P, 16)
-        rec[:, 32] = rr.fitness
-        rec[:, 33] = rr.inlier_rmse
-        rec[:, 34] = ir.fitness
-        rec[:, 35] = ir.inlier_rmse
-        rec[:, 36] = chamfer
-        rec[:, 37] = rr.stats[:, 0].double()     # RANSAC iterations
-        rec[:, 38] = rr.stats[:, 3].double()     # RANSAC status
-        rec[:, 39] = ncor.double()               # correspondences after mutual filter
-        return rec
+        """(P, RECORD_WIDTH) f64 per-pair result records (device), written by the
+        step (pcr_pipeline_records): T_ransac (16), T_icp (16), RANSAC fitness /
+        rmse, ICP fitness / rmse, Chamfer, RANSAC iterations, RANSAC status,
+        correspondences after the mutual filter."""
+        return self.rec

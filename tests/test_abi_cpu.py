@@ -8,7 +8,7 @@ import tempfile
 
 import pytest
 
-from pointcloudregistration_amd import _lib, ndp, ndp_opt
+from pointcloudregistration_amd import _lib, ndp, ndp_opt, pipeline
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -19,6 +19,7 @@ MIRRORS = {
     "pcr_adam_tensor": ndp_opt._AdamTensor,
     "pcr_ndp_train": ndp_opt._TrainC,
     "pcr_ndp_chamfer": ndp_opt._ChamferC,
+    "pcr_pipeline_io": pipeline._PipelineIO,
 }
 
 
