@@ -407,7 +407,7 @@ const void *icp_fn(bool lds) {
 
 int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, const int32_t *n_src,
              const int32_t *n_tgt, const double *init, const pcr_icp_params *prm, double *T_out,
-             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s) {
+             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s, const int32_t *order_in) {
     IArgs a;
     a.src = src; a.tgt = tgt; a.n_src = n_src; a.n_tgt = n_tgt; a.Nmax = Nmax; a.Mmax = Mmax;
     a.init = init;
@@ -422,8 +422,14 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
         if (rc != PCR_OK) return rc;
         if (Nmax > 0) {
-            rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 14, &a.order);
-            if (rc != PCR_OK) return rc;
+            // any spatial order serves (it only groups a wave's queries): the
+            // pipeline hands over RANSAC's, sorted by its coarser cells
+            if (order_in) {
+                a.order = order_in;
+            } else {
+                rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 14, &a.order);
+                if (rc != PCR_OK) return rc;
+            }
         }
     } else {
         a.grid = GridBatch{};
@@ -504,5 +510,5 @@ extern "C" int pcr_icp_batch(const float *src_xyz, const float *tgt_xyz, int32_t
     PCR_REQUIRE(src_xyz && tgt_xyz && init && params && T && fitness_rmse && stats, PCR_ERR_ARG,
                 "icp: null pointer");
     return pcr::icp_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, init, params, T,
-                         fitness_rmse, stats, corr_tgt, pcr::as_stream(stream));
+                         fitness_rmse, stats, corr_tgt, pcr::as_stream(stream), nullptr);
 }

@@ -19,10 +19,10 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
                 const int32_t *n_src, const int32_t *n_tgt, const int32_t *corres,
                 const int32_t *n_corres, int Kmax, const uint32_t *pair_ids,
                 const pcr_ransac_params *prm, double *T_out, double *fit_out, int32_t *stats,
-                int32_t *corr_tgt, uint32_t *mask, hipStream_t s);
+                int32_t *corr_tgt, uint32_t *mask, hipStream_t s, const int32_t **order_out);
 int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, const int32_t *n_src,
              const int32_t *n_tgt, const double *init, const pcr_icp_params *prm, double *T_out,
-             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s);
+             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s, const int32_t *order_in);
 int pipeline_records(const pcr_pipeline_io *io, hipStream_t s);
 }  // namespace pcr
 
@@ -60,7 +60,7 @@ extern "C" int pcr_register_feature_ransac(const float *src_xyz, const float *tg
     }
     if (rc != PCR_OK) return rc;
     return pcr::ransac_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, corres, n_corres, Nmax,
-                            pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask, s);
+                            pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask, s, nullptr);
 }
 
 static int io_check(const pcr_pipeline_io *io) {
@@ -88,12 +88,13 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     rc = pcr::feature_corres_impl(io->src_feat, io->tgt_feat, P, N, M, io->D, nullptr, nullptr,
                                   rp->mutual_filter, rp->ransac_n, io->nn12, io->corres, io->n_corres, s);
     if (rc != PCR_OK) return rc;
+    const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP
     rc = pcr::ransac_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->corres, io->n_corres, N,
                           io->pair_ids, rp, io->T_ransac, io->fit_ransac, io->stats_ransac, nullptr,
-                          io->inlier_mask, s);
+                          io->inlier_mask, s, &order);
     if (rc != PCR_OK) return rc;
     rc = pcr::icp_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->T_ransac, ip, io->T_icp,
-                       io->fit_icp, io->stats_icp, nullptr, s);
+                       io->fit_icp, io->stats_icp, nullptr, s, order);
     if (rc != PCR_OK) return rc;
     rc = pcr_transform_batch(io->src_xyz, P, N, io->T_icp, io->aligned, stream);
     if (rc != PCR_OK) return rc;

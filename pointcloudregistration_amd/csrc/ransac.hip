@@ -690,7 +690,8 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
                 const int32_t *n_src, const int32_t *n_tgt, const int32_t *corres,
                 const int32_t *n_corres, int Kmax, const uint32_t *pair_ids,
                 const pcr_ransac_params *prm, double *T_out, double *fit_out, int32_t *stats,
-                int32_t *corr_tgt, uint32_t *mask, hipStream_t s) {
+                int32_t *corr_tgt, uint32_t *mask, hipStream_t s, const int32_t **order_out) {
+    if (order_out) *order_out = nullptr;
     PCR_REQUIRE(prm->ransac_n >= 3 && prm->ransac_n <= kMaxRansacN, PCR_ERR_ARG,
                 "ransac: ransac_n=%d unsupported (3..%d)", prm->ransac_n, kMaxRansacN);
     PCR_REQUIRE(prm->max_iteration >= 0, PCR_ERR_ARG, "ransac: negative max_iteration");
@@ -754,6 +755,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
         if (Nmax > 0) {
             rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 13, &a.order);
             if (rc != PCR_OK) return rc;
+            if (order_out) *order_out = a.order;
         }
     }
     const size_t hdr = (sizeof(Shared) + 15) & ~size_t(15);
@@ -892,5 +894,5 @@ extern "C" int pcr_ransac_batch(const float *src_xyz, const float *tgt_xyz, int3
     PCR_REQUIRE(P <= 65535, PCR_ERR_ARG, "ransac: P=%d > 65535 pairs per call", P);
     return pcr::ransac_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, corres, n_corres, Kmax,
                             pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask,
-                            pcr::as_stream(stream));
+                            pcr::as_stream(stream), nullptr);
 }
