@@ -693,9 +693,10 @@ def _traffic_file():
     return _newest("pmc_traffic.json")
 
 
-def _pmc_traffic(kernel):
-    """HBM bytes per launch (fetch + write) of `kernel` from the newest committed PMC
-    summary (tools/pmc_traffic.sh on this bench), or None when absent."""
+def _pmc_traffic(kernel, *more):
+    """HBM bytes per launch (fetch + write) of the kernel whose name holds `kernel`
+    (and every string of `more`) from the newest committed PMC summary
+    (tools/pmc_traffic.sh on this bench), or None when absent."""
     f = _traffic_file()
     if f is None:
         return None
@@ -705,7 +706,7 @@ def _pmc_traffic(kernel):
     except (OSError, ValueError, KeyError):
         return None
     for k, v in ks.items():
-        if kernel in k:
+        if kernel in k and all(m in k for m in more):
             return v.get("fetch_size_bytes", 0.0) + v.get("write_size_bytes", 0.0)
     return None
 
@@ -848,10 +849,10 @@ def grid_candidates(src, tgt, T, d):
 # Per 32 x 32 tile and wave, the inner loop of the shipped build's screens
 # (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 8
 # column tiles, D = 32 -> NCH = 7 k-chunks of 16):
-#  pass 1 featnn_row7<7,8,true,2>:  7 v_mfma_f32_32x32x16_f16, 48 VALU (32 v_med3
+#  pass 1 featnn_row7<2,8,true,2>:  7 v_mfma_f32_32x32x16_f16, 48 VALU (32 v_med3
 #    for the top-2 update, 16 v_and_or packing the column code), 3.5 ds_read_b128
 #    (each B fragment shared by the 2 row tiles), ~1.2 SALU;
-#  pass 2 featnn_row7<7,8,false,2>: 7 MFMA, 32 v_med3 (values only), 3.5 LDS,
+#  pass 2 featnn_row7<2,8,false,2>: 7 MFMA, 32 v_med3 (values only), 3.5 LDS,
 #    0.44 s_nop.
 # SIMD issue cycles (MI355X guide, 'vector-instruction ISSUE cost'): an MFMA holds
 # vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the two waves of a
@@ -1151,11 +1152,11 @@ def main():
                    "inputs": "resident in HBM (see host_resident for the PCIe-inclusive rate)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_F16_MFMA_TFLOPS,
-                     "traffic": _pmc_traffic("featnn_row7<7, 8, true"),
+                     "traffic": _pmc_traffic("featnn_row7<", "true"),
                      "traffic_source": f"{_traffic_source()} (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this bench; FETCH_SIZE x2 per the "
                                        "gfx950 note)",
-                     "kernel": "featnn_row7<7,8,true,2> (pass 1: v_mfma_f32_32x32x16_f16, f16x3 "
+                     "kernel": "featnn_row7<2,8,true,2> (pass 1: v_mfma_f32_32x32x16_f16, f16x3 "
                                "split, row top-2 with packed column code)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,
@@ -1163,12 +1164,12 @@ def main():
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS,
                      "issue_model": _screen_issue_model(tiles1, per_launch_ms, SCREEN_TILE_ISSUE),
-                     "pass2": {"kernel": "featnn_row7<7,8,false,2> (target rows J = unique(nn12), "
+                     "pass2": {"kernel": "featnn_row7<2,8,false,2> (target rows J = unique(nn12), "
                                          "values only)",
                                "kernel_ms_per_launch": per2_ms, "launches": launches2,
                                "j_rows_mean": float(jrows.mean()),
                                "flops_per_launch": 2.0 * float(jrows.sum()) * N * D,
-                               "traffic": _pmc_traffic("featnn_row7<7, 8, false"),
+                               "traffic": _pmc_traffic("featnn_row7<", "false"),
                                "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN2_TILE_ISSUE)},
                      "screen_stage": {"ms_per_launch": stage_ms, "achieved": stage_tf,
                                       "frac": stage_tf / PEAK_F16_MFMA_TFLOPS,
