@@ -253,26 +253,18 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
     const float s = pair_scale5(mx[p], sp.T);
     const int rr = l & 31, h = l >> 5;
     const bool valid = rr < nrows;
-    // the wave's 32-row tile is contiguous: 16-byte loads of consecutive words
-    // (a lane per row read 32 rows 128 B apart per instruction and thrashed
-    // the L1: ~3x the bytes from L2), scaled and staged through LDS (row stride
-    // D + 1: the row reads below hit distinct banks)
-    __shared__ float xs[4][32][D + 1];
-    {
-        const float4 *tile = reinterpret_cast<const float4 *>(X + ((size_t)p * Nmax + (size_t)t * 32) * D);
-        constexpr int Q4 = D / 4;
-#pragma unroll
-        for (int e = l; e < 32 * Q4; e += 64) {
-            const int r = e / Q4, k = (e - r * Q4) * 4;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (r < nrows) v = tile[e];
-            xs[w][r][k] = v.x * s; xs[w][r][k + 1] = v.y * s; xs[w][r][k + 2] = v.z * s; xs[w][r][k + 3] = v.w * s;
-        }
-    }
-    __syncthreads();
     float x[D];
+    if (valid) {
+        const float4 *row = reinterpret_cast<const float4 *>(X + ((size_t)p * Nmax + (size_t)t * 32 + rr) * D);
 #pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = xs[w][rr][k];
+        for (int q = 0; q < D / 4; ++q) {
+            const float4 v = row[q];
+            x[4 * q] = v.x * s; x[4 * q + 1] = v.y * s; x[4 * q + 2] = v.z * s; x[4 * q + 3] = v.w * s;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = 0.0f;
+    }
     double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
