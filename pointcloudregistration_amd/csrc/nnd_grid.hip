@@ -34,6 +34,7 @@ struct NgArgs {
     const float *xyz[2];  // set 0: xyz1 (B, n0, 3), set 1: xyz2 (B, n1, 3)
     int n[2];
     int B, S, nmax;
+    float cf;             // cell factor (0.6; PCR_NND_CELL overrides, tuning hook)
     float *cell;          // [2][B]
     int *flag;            // [B]: 1 = use the reference loop
     int *hcnt;            // [2][B][S]
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
     if (m > 0.0) {
         double v = 1.0;
         for (int c = 0; c < 3; ++c) v *= fmax(e[c], 1e-3 * m);
-        cell = 0.6 * cbrt(v / (double)(n > 0 ? n : 1));
+        cell = (double)a.cf * cbrt(v / (double)(n > 0 ? n : 1));
     }
     // integer cell coordinates must stay far from int overflow
     if (!(amax / cell < 1e9)) bad = 1;
@@ -267,6 +268,11 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
     a.start = a.hcnt + hc;
     a.dist[0] = dist1; a.dist[1] = dist2; a.idx[0] = idx1; a.idx[1] = idx2;
     a.gate = current_gate();
+    a.cf = 0.6f;
+    if (const char *e = getenv("PCR_NND_CELL")) {
+        const float v = (float)atof(e);
+        if (v >= 0.1f && v <= 4.0f) a.cf = v;
+    }
     const bool lds_build = S <= kLdsSlots;
     PCR_HIP_CHECK(hipMemsetAsync(a.flag, 0, sizeof(int) * (lds_build ? (size_t)b : b + hc), s));
     hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(1024), 0, s, a);
