@@ -221,15 +221,22 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
         }
         dst[(size_t)c * 64] = o;
     }
-    // the pair's max norm: one atomic per wave (a per-lane atomicMax on the
-    // pair's one word serialised 8K same-address atomics per cloud)
-    // (max of the bit patterns: the same word the per-lane atomics left, NaN included)
+    // the pair's max norm: one atomic per WORKGROUP.  The P words share a few
+    // cache lines, and one atomic per wave (256 per cloud) serialised at the
+    // L2: ~80 us per launch whatever the batch.  Max of the bit patterns: the
+    // same word per-lane atomics would leave, NaN included.
     const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
     if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
     unsigned rb = __float_as_uint(r);
 #pragma unroll
     for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
-    if (l == 0 && rb != 0u) atomicMax(nmax + p, rb);
+    __shared__ unsigned wmax[4];
+    if (l == 0) wmax[w] = rb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m != 0u) atomicMax(nmax + p, m);
+    }
 }
 
 // Register-resident pack for a compile-time D (the hot D = 32): one lane per
@@ -320,15 +327,22 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
         const f16x8 a = frag(2 * c), b = frag(2 * c + 1);
         dst[(size_t)c * 64] = h ? b : a;
     }
-    // the pair's max norm: one atomic per wave (a per-lane atomicMax on the
-    // pair's one word serialised 8K same-address atomics per cloud)
-    // (max of the bit patterns: the same word the per-lane atomics left, NaN included)
+    // the pair's max norm: one atomic per WORKGROUP.  The P words share a few
+    // cache lines, and one atomic per wave (256 per cloud) serialised at the
+    // L2: ~80 us per launch whatever the batch.  Max of the bit patterns: the
+    // same word per-lane atomics would leave, NaN included.
     const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
     if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
     unsigned rb = __float_as_uint(r);
 #pragma unroll
     for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
-    if (l == 0 && rb != 0u) atomicMax(nmax + p, rb);
+    __shared__ unsigned wmax[4];
+    if (l == 0) wmax[w] = rb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m != 0u) atomicMax(nmax + p, m);
+    }
 }
 
 // certification threshold for a top-2 gap in scaled units (see header)
