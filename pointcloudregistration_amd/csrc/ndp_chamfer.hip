@@ -80,7 +80,6 @@ struct NcArgs {
     int *cnt;               // counting-sort counts, zero between builds
     int *fb;                // K + M: listed queries (dir 0 at 0, dir 1 at K)
     unsigned long long *fbkey;  // K + M: their (d bits, j) minima
-    int *gdone;                 // per 64-query group of the list: slices finished (0 between steps)
     const double *gate;
 };
 
@@ -310,8 +309,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
 // 2,048-candidate slice of the other cloud), persistent blocks over all items.
 // The slice is staged in LDS (float4 of the grid copy); wave w holds queries
 // 16w..16w+15 as eight packed pairs, lane l takes candidates l, l + 64, ...;
-// each query's (d, j) minimum over the slice goes to its key by atomicMin, and
-// the last slice of a group to finish emits the group's answers.
+// each query's (d, j) minimum over the slice goes to its key by atomicMin.
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
@@ -336,8 +334,7 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
         __syncthreads();  // the previous item's tile is consumed
         for (int c = threadIdx.x; c < tn; c += 256) tile[c] = cand[t0 + c];
         __syncthreads();
-        const bool act = wv * kFbQW < qn;  // this wave holds listed queries (every wave meets the barriers)
-        if (act) {
+        if (wv * kFbQW >= qn) continue;  // no listed query for this wave (barriers are above)
         f2v qx[H], qy[H], qz[H], best[H];
         int bj[kFbQW];
 #pragma unroll
@@ -380,26 +377,20 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
             if (lane == u && e < qn && jj != 0x7fffffff)
                 atomicMin(a.fbkey + lbase + e, ((unsigned long long)__float_as_uint(bb) << 32) | (unsigned)jj);
         }
-        }
-        // the group's last slice to finish emits its queries (no separate launch)
-        __shared__ bool last;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            int *gd = a.gdone + (dir ? g0 : 0) + grp;
-            last = atomicAdd(gd, 1) == ns - 1;
-            if (last) *gd = 0;
-        }
-        __syncthreads();
-        if (last && (int)threadIdx.x < qn) {
-            __threadfence();
-            const int e = lbase + threadIdx.x;
-            const unsigned long long k = __hip_atomic_load(a.fbkey + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            emit(a, dir, a.fb[e], __uint_as_float((unsigned)(k >> 32)), (int)(unsigned)(k & 0xffffffffu));
-        }
     }
 }
 
+// the listed queries' answers from their keys
+__global__ __launch_bounds__(256) void nc_fallback_emit(NcArgs a) {
+    if (gated_off(a.gate)) return;
+    const int c0 = a.hdr->fb_cnt[0], c1 = a.hdr->fb_cnt[1];
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= c0 + c1) return;
+    const int dir = w < c0 ? 0 : 1;
+    const int e = dir ? a.K + (w - c0) : w;
+    const unsigned long long k = a.fbkey[e];
+    emit(a, dir, a.fb[e], __uint_as_float((unsigned)(k >> 32)), (int)(unsigned)(k & 0xffffffffu));
+}
 
 // the scan's dynamic LDS limit, set once outside any stream capture (prepare
 // runs eagerly before a level graph is captured)
@@ -410,7 +401,7 @@ hipError_t nc_scan_attr() {
 }
 
 struct NcLayout {
-    size_t hdr, cnt, fb, fbkey, gdone, total;
+    size_t hdr, cnt, fb, fbkey, total;
     size_t start[2], pts[2];  // [0] target, [1] subset
     int S[2];
 };
@@ -436,7 +427,6 @@ NcLayout nc_layout(int K, int M) {
     L.cnt = o; o = up256(o + sizeof(int) * (size_t)std::max(L.S[0], L.S[1]));
     L.fb = o; o = up256(o + sizeof(int) * ((size_t)K + M));
     L.fbkey = o; o = up256(o + sizeof(unsigned long long) * ((size_t)K + M));
-    L.gdone = o; o = up256(o + sizeof(int) * (size_t)((K + kFbQ - 1) / kFbQ + (M + kFbQ - 1) / kFbQ));
     L.total = o;
     return L;
 }
@@ -472,7 +462,6 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     a.cnt = (int *)(s + L.cnt);
     a.fb = (int *)(s + L.fb);
     a.fbkey = (unsigned long long *)(s + L.fbkey);
-    a.gdone = (int *)(s + L.gdone);
     a.gate = current_gate();
     return PCR_OK;
 }
@@ -512,8 +501,6 @@ extern "C" int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs
     hipStream_t s = pcr::as_stream(stream);
     PCR_HIP_CHECK(pcr::nc_scan_attr());
     PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, sizeof(pcr::NcHdr), s));
-    PCR_HIP_CHECK(hipMemsetAsync(a.gdone, 0, sizeof(int) * (size_t)((a.K + pcr::kFbQ - 1) / pcr::kFbQ +
-                                                                    (a.M + pcr::kFbQ - 1) / pcr::kFbQ), s));
     PCR_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * (size_t)(a.St > a.Ss ? a.St : a.Ss), s));
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, a.tgt, a.M, &a.hdr->cell_t, &a.hdr->tflag);
     PCR_LAUNCH_CHECK();
@@ -551,6 +538,8 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
     PCR_LAUNCH_CHECK();
     prof_end(s, pcr::kProfNndGrid);
     hipLaunchKernelGGL(pcr::nc_fallback, dim3(pcr::kFbBlocks), dim3(256), 0, s, a);
+    PCR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(pcr::nc_fallback_emit, dim3((a.K + a.M + 255) / 256), dim3(256), 0, s, a);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
