@@ -48,7 +48,7 @@ using nng::take;
 constexpr double kFixScale = 17592186044416.0;  // 2^44
 constexpr int kRep = PCR_NDP_GACC_REPLICAS;     // gradient sum replicas (query index mod kRep)
 constexpr int kFbQW = 16;                       // nc_fallback: listed queries per wave (8 packed pairs)
-constexpr int kFbQ = 4 * kFbQW, kFbSlice = 2048;  // work item: listed queries x candidates
+constexpr int kFbQ = 4 * kFbQW, kFbSlice = 1024;  // work item: listed queries x candidates
 constexpr int kFbBlocks = 2048;                 // nc_fallback: persistent 256-thread blocks
 
 struct NcHdr {
@@ -306,10 +306,13 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
 }
 
 // the listed queries: work item = (64 listed queries of one direction, a
-// 2,048-candidate slice of the other cloud), persistent blocks over all items.
-// The slice is staged in LDS (float4 of the grid copy); wave w holds queries
-// 16w..16w+15 as eight packed pairs, lane l takes candidates l, l + 64, ...;
-// each query's (d, j) minimum over the slice goes to its key by atomicMin.
+// 1,024-candidate slice of the other cloud in index order), persistent blocks
+// over all items.  The slice is staged in LDS; wave w holds queries
+// 16w..16w+15 as eight packed pairs, lane l takes candidates l, l + 64, ...
+// in increasing index, so a strict < keeps the lowest index of a tie (one
+// compare and two selects per query, no mask arithmetic); the lanes merge
+// lexicographically and each query's (d, j) minimum over the slice goes to
+// its key by atomicMin.
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
@@ -327,12 +330,15 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
         const int grp = r / ns, sl = r - grp * ns;
         const int cnt = dir ? c1 : c0, nc = dir ? a.K : a.M;
         const float *Q = dir ? a.tgt : a.xs;
-        const float4 *cand = (dir ? a.cs : a.ct).pts;
+        const float *C = dir ? a.xs : a.tgt;
         const int lbase = (dir ? a.K : 0) + grp * kFbQ;
         const int qn = min(kFbQ, cnt - grp * kFbQ);
         const int t0 = sl * kFbSlice, tn = min(kFbSlice, nc - t0);
         __syncthreads();  // the previous item's tile is consumed
-        for (int c = threadIdx.x; c < tn; c += 256) tile[c] = cand[t0 + c];
+        for (int c = threadIdx.x; c < tn; c += 256) {
+            const float *cp = C + 3 * (size_t)(t0 + c);
+            tile[c] = make_float4(cp[0], cp[1], cp[2], 0.0f);
+        }
         __syncthreads();
         if (wv * kFbQW >= qn) continue;  // no listed query for this wave (barriers are above)
         f2v qx[H], qy[H], qz[H], best[H];
@@ -347,9 +353,21 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
             best[u >> 1][u & 1] = __builtin_inff();
             bj[u] = 0x7fffffff;
         }
-        for (int c = lane; c < tn; c += 64) {
+        // the lane's first candidate seeds its minima (so a d = inf still names an index)
+        if (lane < tn) {
+            const float4 p = tile[lane];
+            const f2v px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const f2v dx = px - qx[h], dy = py - qy[h], dz = pz - qz[h];
+                best[h] = (dx * dx + dy * dy) + dz * dz;
+                bj[2 * h] = bj[2 * h + 1] = t0 + lane;
+            }
+        }
+#pragma unroll 2
+        for (int c = lane + 64; c < tn; c += 64) {
             const float4 p = tile[c];
-            const int j = __float_as_int(p.w);
+            const int j = t0 + c;
             const f2v px = {p.x, p.x}, py = {p.y, p.y}, pz = {p.z, p.z};
 #pragma unroll
             for (int h = 0; h < H; ++h) {
@@ -357,9 +375,9 @@ __global__ __launch_bounds__(256) void nc_fallback(NcArgs a) {
                 const f2v d = (dx * dx + dy * dy) + dz * dz;  // d2f's roundings, two queries at once
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
-                    float bb = best[h][b];
-                    nng::take_sel(d[b], j, bb, bj[2 * h + b]);
-                    best[h][b] = bb;
+                    const bool lt = d[b] < best[h][b];
+                    best[h][b] = lt ? d[b] : best[h][b];
+                    bj[2 * h + b] = lt ? j : bj[2 * h + b];
                 }
             }
         }

@@ -65,12 +65,33 @@ __device__ __forceinline__ bool ring_walk(const View &v, float qx, float qy, flo
     const double cell = (double)v.cell, ic = 1.0 / cell;
     const int cx = ccoord(qx, ic), cy = ccoord(qy, ic), cz = ccoord(qz, ic);
     const double margin = 1e-6 * (fabs((double)qx) + fabs((double)qy) + fabs((double)qz) + cell);
-    auto scan_cell = [&](int x, int y, int z) {
-        const unsigned h = nhash(x, y, z, v.S);
-        const int s1 = v.start[h + 1];
-        for (int s = v.start[h]; s < s1; ++s) {
-            const float4 p = v.pts[s];
-            take(d2f(p.x, p.y, p.z, qx, qy, qz), __float_as_int(p.w), best, bj);
+    // up to three cells (x, y, z0 + t dz), t < n: every slot bound is loaded
+    // first, then each cell's points four at a time, so a lane waits on one
+    // round trip per batch instead of one per cell and one per point (the walk
+    // is bound by the latency of these dependent loads; take() is order-free)
+    auto scan_cells = [&](int x, int y, int z0, int dz, int n) {
+        int s0[3], s1[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            s0[t] = 0;
+            s1[t] = 0;
+            if (t < n) {
+                const unsigned h = nhash(x, y, z0 + t * dz, v.S);
+                s0[t] = v.start[h];
+                s1[t] = v.start[h + 1];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            for (int s = s0[t]; s < s1[t]; s += 4) {
+                float4 p[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (s + u < s1[t]) p[u] = v.pts[s + u];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (s + u < s1[t]) take(d2f(p[u].x, p[u].y, p[u].z, qx, qy, qz), __float_as_int(p[u].w), best, bj);
+            }
         }
     };
     for (int k = 0; k <= kmax; ++k) {
@@ -79,10 +100,9 @@ __device__ __forceinline__ bool ring_walk(const View &v, float qx, float qy, flo
         for (int c = sub; c < side * side; c += LPQ) {
             const int cq = c / side, dx = cq - k, dy = c - cq * side - k;
             if (dx == -k || dx == k || dy == -k || dy == k) {
-                for (int dz = -k; dz <= k; ++dz) scan_cell(cx + dx, cy + dy, cz + dz);
+                for (int z = cz - k; z <= cz + k; z += 3) scan_cells(cx + dx, cy + dy, z, 1, min(3, cz + k - z + 1));
             } else {
-                scan_cell(cx + dx, cy + dy, cz - k);
-                scan_cell(cx + dx, cy + dy, cz + k);
+                scan_cells(cx + dx, cy + dy, cz - k, 2 * k, 2);
             }
         }
         merge();

@@ -484,6 +484,10 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
         if ev is not None:
             info[-1]["replay_ms"] = ev[0].elapsed_time(ev[1])
             info[-1]["capture_ms"] = (lv.capture_done - t1) * 1e3
+        if getattr(lv, "use_nc", False):
+            # listed (uncertified) queries per direction of the last evaluated iteration
+            hdr = lv.nc_raw[(lv.nc.scratch - lv.nc_raw.data_ptr()):][:28].cpu().numpy().view(np.int32)
+            info[-1]["fb_cnt"] = (int(hdr[5]), int(hdr[6]))
         info[-1]["setup_ms"] = (t1 - t0) * 1e3
         info[-1]["level_ms"] = (t2 - t0) * 1e3
         hist.append((lv.warped + tgt_mean).cpu().numpy())

@@ -46,4 +46,4 @@ for rep in range(int(os.environ.get("REPS", "2"))):
           f"{[round(i.get('replay_ms', 0), 1) for i in info]}, setup_ms "
           f"{[round(i.get('setup_ms', 0), 1) for i in info]}, capture_ms "
           f"{[round(i.get('capture_ms', 0), 1) for i in info]}, level_ms "
-          f"{[round(i.get('level_ms', 0), 1) for i in info]}", flush=True)
+          f"{[round(i.get('level_ms', 0), 1) for i in info]}, fb_cnt {[i.get('fb_cnt') for i in info]}", flush=True)

@@ -32,4 +32,4 @@ for rep in range(2):
                                                fused=os.environ.get("FUSED", "1") == "1")
     torch.cuda.synchronize()
     rp = [round(i.get("replay_ms", 0.0), 2) for i in out[3]]
-    print(rep, (time.perf_counter() - t0) * 1e3, "ms; replay ms per level", rp, "sum", round(sum(rp), 2))
+    print(rep, (time.perf_counter() - t0) * 1e3, "ms; replay ms per level", rp, "sum", round(sum(rp), 2), "fb_cnt", [i.get("fb_cnt") for i in out[3]])
