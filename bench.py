@@ -1022,6 +1022,67 @@ def measure_host_resident(batch, params, pair_ids, steps, warmup, world, total_p
                     "batch's pipeline; records all-gathered and copied back to the host"}
 
 
+def measure_s8d_job(batch, params, pair_ids, world, total_pairs, warmup=3, runs=10):
+    """SURVEY 8d / BASELINE.md's C4 definition, literally: throughput = the job's
+    pairs / the wall time of ONE job from "inputs resident on the host" to "all
+    (R,t) gathered on rank 0" (H2D and the RCCL gather included, data generation
+    excluded); 3 warm-up jobs, the median of 10.  Each job is a synchronous unit
+    (nothing carried over from the previous one); inside it the rank's shard is
+    split into C chunks whose H2D copy (pinned host -> HBM, own stream) overlaps
+    the pipeline of the previous chunk, so the job costs ~ one chunk's copy plus
+    the C pipelines instead of the whole copy plus the pipeline."""
+    from pointcloudregistration_amd.multigpu import gather_records
+    from pointcloudregistration_amd.pipeline import PairPipeline
+    P = batch.src.shape[0]
+    C = 4 if P >= 128 else (2 if P >= 32 else 1)
+    bounds = [P * c // C for c in range(C + 1)]
+    hosts, devs, pipes = [], [], []
+    for c in range(C):
+        a, b = bounds[c], bounds[c + 1]
+        h = [torch.from_numpy(np.ascontiguousarray(x[a:b])).pin_memory()
+             for x in (batch.src, batch.tgt, batch.src_feat, batch.tgt_feat)]
+        d = [torch.empty(t.shape, dtype=t.dtype, device="cuda") for t in h]
+        hosts.append(h)
+        devs.append(d)
+        pipes.append(PairPipeline(*d, params, pair_ids=pair_ids[a:b]))
+    rows = -(-total_pairs // world)
+    rec_host = torch.empty((rows * world, 40), dtype=torch.float64).pin_memory()
+    rec_dev = torch.empty((P, 40), dtype=torch.float64, device="cuda")
+    copy_s = torch.cuda.Stream()
+    comp = torch.cuda.current_stream()
+    copied = [torch.cuda.Event() for _ in range(C)]
+
+    def job():
+        with torch.cuda.stream(copy_s):
+            for c in range(C):
+                for d, h in zip(devs[c], hosts[c]):
+                    d.copy_(h, non_blocking=True)
+                copied[c].record(copy_s)
+        for c in range(C):
+            comp.wait_event(copied[c])
+            pipes[c].run()
+            rec_dev[bounds[c]:bounds[c + 1]].copy_(pipes[c].records())
+        rec = gather_records(rec_dev, world, rows)
+        rec_host.copy_(rec, non_blocking=True)
+        torch.cuda.synchronize()
+
+    for _ in range(warmup):
+        job()
+    times = []
+    for _ in range(runs):
+        barrier(world)
+        t0 = time.perf_counter()
+        job()
+        times.append(max_over_ranks(time.perf_counter() - t0, world))
+    med = float(np.median(times))
+    return {"value": total_pairs / med, "unit": "pairs/s", "ms_per_job": med * 1e3,
+            "ms_per_job_min": min(times) * 1e3, "ms_per_job_max": max(times) * 1e3,
+            "warmup_jobs": warmup, "timed_jobs": runs, "chunks_per_rank": C,
+            "note": "SURVEY 8d: one job of the whole C4 batch, pinned host inputs -> (R,t) records "
+                    "all-gathered and on the host of rank 0; median of 10 after 3 warm-ups; the "
+                    "contract's `value` is the HBM-resident rate (inputs already on the GPU)"}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -1193,6 +1254,8 @@ def main():
         torch.cuda.empty_cache()
         out["host_resident"] = measure_host_resident(batch, params, pair_ids, args.steps,
                                                      args.warmup, world, args.pairs)
+        torch.cuda.empty_cache()
+        out["s8d_job"] = measure_s8d_job(batch, params, pair_ids, world, args.pairs)
     if world > 1:
         # secondary: weak scaling, `pairs` pairs on EVERY rank
         wfirst = rank * args.pairs
@@ -1235,9 +1298,14 @@ def main():
                             "c5_flow": measure_c5(wc)}
     if rank == 0:
         print(json.dumps(out))
+    if os.environ.get("PCR_DUMP_MAPS"):
+        # diagnostics: the library map of this process, to symbolise a crash at exit
+        with open("/proc/self/maps") as f, open(os.environ["PCR_DUMP_MAPS"], "w") as g:
+            g.write(f.read())
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    _lib.shutdown()   # the library's device objects, before the runtime's teardown
 
 
 if __name__ == "__main__":

@@ -42,6 +42,10 @@ typedef void *pcr_stream_t; /* hipStream_t */
 const char *pcr_last_error(void);
 int pcr_version(void);
 int pcr_workspace_release(void);
+/* end of process: synchronise every device the library used and free its
+ * workspace, retired buffers and pooled profiling events (idempotent; the
+ * library stays usable).  The Python layer runs it from atexit. */
+int pcr_shutdown(void);
 
 /* Optional per-kernel timing with HIP events recorded on the launch stream
  * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,
@@ -71,6 +75,24 @@ int pcr_featmut_debug_copy(void *dst, int64_t bytes, pcr_stream_t stream);
 int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, int32_t n, int32_t m,
                     float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                     pcr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * a1/a3 -- the same search over RAGGED batches, and in f64.  Replaces
+ * pytorch3d.knn_points(x, y, lengths1, lengths2, K=1) inside
+ * compute_truncated_chamfer_distance (c2p-net/deformationpyramid/model/
+ * loss.py:60-160: x_lengths / y_lengths, computed in the inputs' dtype).
+ *   n1 (b) / n2 (b) i32 device: valid points of each cloud (NULL = n / m);
+ *   rows i < n1[k] search the first n2[k] points of the other cloud with
+ *   pcr_nnd_forward's contract (same formula and first-index rule, in f32 or
+ *   f64); rows past a length, and rows whose other cloud is empty, get
+ *   (0, 0).  Outputs are (b,n) / (b,m) like pcr_nnd_forward.
+ * ------------------------------------------------------------------------- */
+int pcr_nnd_forward_ragged(const float *xyz1, const float *xyz2, int32_t b, int32_t n, int32_t m,
+                           const int32_t *n1, const int32_t *n2, float *dist1, float *dist2,
+                           int32_t *idx1, int32_t *idx2, pcr_stream_t stream);
+int pcr_nnd_forward_f64(const double *xyz1, const double *xyz2, int32_t b, int32_t n, int32_t m,
+                        const int32_t *n1, const int32_t *n2, double *dist1, double *dist2,
+                        int32_t *idx1, int32_t *idx2, pcr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * a2 -- gradient of (dist1, dist2) w.r.t. (xyz1, xyz2).
@@ -254,6 +276,11 @@ int pcr_radius_nn(const float *tgt_xyz, int32_t P, int32_t Mmax, const int32_t *
 int pcr_procrustes_batch(const float *src, const float *tgt, const float *weights, int32_t B,
                          int32_t N, int32_t abs_weights, double eps, double *T,
                          pcr_stream_t stream);
+/* the same for f64 inputs (the reference functions are dtype-generic: f64
+ * tensors run weighted_icp's torch.svd in f64, model_utils.py:120-133) */
+int pcr_procrustes_batch_f64(const double *src, const double *tgt, const double *weights,
+                             int32_t B, int32_t N, int32_t abs_weights, double eps, double *T,
+                             pcr_stream_t stream);
 
 /* out (B,N,3) f32 = (float)(R p + t) in f64 for each item's T (B,16) f64
  * row-major 4x4 (registration outputs).  Replaces the per-pair
@@ -506,9 +533,8 @@ typedef struct pcr_ndp_train {
     float *xs;
     const float *gsub;
     /* optional (null = off): the subset gradient as pcr_ndp_chamfer_step leaves
-     * it -- gacc[0] nonzero = a non-finite term, the sum over r of
-     * gacc[1 + 3 (r K + k) + c] = dL/dxs[k][c] in 2^-44 fixed point; read
-     * instead of gsub; K = gacc_k */
+     * it (pcr_ndp_chamfer_gacc_words(K) int64, layout there); read instead of
+     * gsub; K = gacc_k */
     const long long *gacc;
     int32_t gacc_k, reserved;
 } pcr_ndp_train;
@@ -532,11 +558,15 @@ int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
  *   for the loop (csrc/ndp_chamfer.hip).  xs (K,3) = x_out[inds] (written by
  *   pcr_ndp_train_forward through inv), tgt (M,3) fixed for the level.
  *   d1/i1 (K), d2/i2 (M): pcr_nnd_forward's outputs bit for bit.  gacc
- *   (1 + 3 K PCR_NDP_GACC_REPLICAS int64): the gradient of sum(d1')/K +
- *   sum(d2')/M w.r.t. xs (d' = d where d < trunc, else 0) in 2^-44 fixed point,
- *   as PCR_NDP_GACC_REPLICAS partial sums gacc[1 + 3 (r K + k) + c] (the
- *   gradient is their sum), gacc[0] != 0 when a term was not finite -- consumed
- *   by pcr_ndp_train_backward (pcr_ndp_train.gacc).  K, M <= 32768.
+ *   (pcr_ndp_chamfer_gacc_words(K) = 1 + 6 K R int64, R =
+ *   PCR_NDP_GACC_REPLICAS): the gradient of sum(d1')/K + sum(d2')/M w.r.t. xs
+ *   (d' = d where d < trunc, else 0), each term exactly in a two-word fixed
+ *   point whose exponent s follows the iteration's extents (every integer sum
+ *   provably below 2^63): dL/dxs[k][c] = sum over r of
+ *   hi[r][k][c] 2^-s + lo[r][k][c] 2^-(s+40), hi at gacc[1 + 3 (r K + k) + c],
+ *   lo at gacc[1 + 3 K R + 3 (r K + k) + c]; gacc[0] = ((s + 2048) << 8) | f,
+ *   f = 1 when a term was not finite -- consumed by pcr_ndp_train_backward
+ *   (pcr_ndp_train.gacc).  K, M <= pcr_ndp_chamfer_max_points() (32768).
  *   scratch: pcr_ndp_chamfer_scratch_bytes(K, M) bytes, 256-byte aligned,
  *   owned by the caller for the level.
  * pcr_ndp_chamfer_prepare: the target grid and the subset cell (from xs0, the
@@ -564,6 +594,8 @@ typedef struct pcr_ndp_chamfer {
     void *scratch;
 } pcr_ndp_chamfer;
 int64_t pcr_ndp_chamfer_scratch_bytes(int32_t K, int32_t M);
+int64_t pcr_ndp_chamfer_gacc_words(int32_t K);
+int32_t pcr_ndp_chamfer_max_points(void);
 int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs0, pcr_stream_t stream);
 int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t stream);
 

@@ -86,6 +86,8 @@ def _setup_sigs():
     L.oracle_icp.restype = c.c_int
     L.oracle_icp.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_double,
                              c.c_int, c.c_double, c.c_double, c.c_void_p, c.c_void_p, c.c_void_p]
+    L.oracle_icp_trace.restype = c.c_int
+    L.oracle_icp_trace.argtypes = L.oracle_icp.argtypes + [c.c_void_p, c.c_void_p]
     L.oracle_radius_nn.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_double, c.c_int,
                                    c.c_void_p, c.c_void_p]
     L.oracle_featnn.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
@@ -262,6 +264,37 @@ def icp(src, tgt, max_corr_dist, init=None, max_iteration=30, relative_fitness=1
                         float(max_corr_dist), int(max_iteration), float(relative_fitness),
                         float(relative_rmse), _p(T), _p(fr), _p(it))
     return dict(T=T.reshape(4, 4), fitness=fr[0], inlier_rmse=fr[1], n_corr=nc, iters=int(it[0]))
+
+
+def icp_trace(src, tgt, max_corr_dist, init=None, max_iteration=30, relative_fitness=1e-6,
+              relative_rmse=1e-6):
+    """oracle.icp plus, per iteration, the f64 working copy the Umeyama step saw
+    (iters, n, 3) and its correspondences (iters, n) (-1 = no target within d)."""
+    src, tgt = _f32(src), _f32(tgt)
+    n = src.shape[0]
+    init = _f64(np.eye(4) if init is None else init).reshape(16)
+    T = np.zeros(16, np.float64)
+    fr = np.zeros(2, np.float64)
+    it = np.zeros(1, np.int32)
+    P = np.zeros((max_iteration, n, 3), np.float64)
+    cj = np.full((max_iteration, n), -1, np.int32)
+    nc = L().oracle_icp_trace(_p(src), n, _p(tgt), tgt.shape[0], _p(init), float(max_corr_dist),
+                              int(max_iteration), float(relative_fitness), float(relative_rmse),
+                              _p(T), _p(fr), _p(it), _p(P), _p(cj))
+    k = int(it[0])
+    return dict(T=T.reshape(4, 4), fitness=fr[0], inlier_rmse=fr[1], n_corr=nc, iters=k,
+                P=P[:k].copy(), cj=cj[:k].copy())
+
+
+def ransac_sample(seed, pair_id, itr, K, ransac_n=3):
+    """The correspondence indices hypothesis `itr` draws (sample_indices in
+    pcr_oracle.c: Philox4x32-10 words scaled to [0, K))."""
+    out = []
+    for j in range(ransac_n):
+        if j % 4 == 0:
+            w = philox(seed, pair_id, itr, j >> 2)
+        out.append(int((int(w[j & 3]) * int(K)) >> 32))
+    return np.array(out, np.int32)
 
 
 def lrf_count(pts, q, kernel):

@@ -837,10 +837,34 @@ static void umeyama_masked(const double *P, const double *Tg, const int32_t *cj,
     }
 }
 
-/* returns #correspondences of the final result; out: T16, fit_rmse[2], iters */
+/* returns #correspondences of the final result; out: T16, fit_rmse[2], iters. */
+/* Trace (test infrastructure, may be NULL): for every iteration it the       */
+/* working copy the estimate saw (P_tr[it*3n]) and its correspondences        */
+/* (cj_tr[it*n], -1 = none), so an independent estimator can be run on the    */
+/* very sets this loop estimated from.                                       */
+static int icp_core(const float *srcf, int n, const float *tgtf, int m, const double *init16,
+                    double d, int max_iter, double rel_fit, double rel_rmse, double *T16,
+                    double *fit_rmse, int32_t *iters, double *P_tr, int32_t *cj_tr);
+
 int oracle_icp(const float *srcf, int n, const float *tgtf, int m, const double *init16, double d,
                int max_iter, double rel_fit, double rel_rmse, double *T16, double *fit_rmse,
                int32_t *iters)
+{
+    return icp_core(srcf, n, tgtf, m, init16, d, max_iter, rel_fit, rel_rmse, T16, fit_rmse, iters,
+                    NULL, NULL);
+}
+
+int oracle_icp_trace(const float *srcf, int n, const float *tgtf, int m, const double *init16,
+                     double d, int max_iter, double rel_fit, double rel_rmse, double *T16,
+                     double *fit_rmse, int32_t *iters, double *P_tr, int32_t *cj_tr)
+{
+    return icp_core(srcf, n, tgtf, m, init16, d, max_iter, rel_fit, rel_rmse, T16, fit_rmse, iters,
+                    P_tr, cj_tr);
+}
+
+static int icp_core(const float *srcf, int n, const float *tgtf, int m, const double *init16,
+                    double d, int max_iter, double rel_fit, double rel_rmse, double *T16,
+                    double *fit_rmse, int32_t *iters, double *P_tr, int32_t *cj_tr)
 {
     memcpy(T16, init16, sizeof(double) * 16);
     fit_rmse[0] = fit_rmse[1] = 0.0;
@@ -869,6 +893,8 @@ int oracle_icp(const float *srcf, int n, const float *tgtf, int m, const double 
     for (it = 0; it < max_iter; it++) {
         if (cnt == 0) break; /* Umeyama on an empty set is undefined in Eigen; stop */
         double U[12], U16[16], Tn[16];
+        if (P_tr) memcpy(P_tr + (size_t)it * 3 * n, P, sizeof(double) * 3 * (size_t)n);
+        if (cj_tr) memcpy(cj_tr + (size_t)it * n, cj, sizeof(int32_t) * (size_t)n);
         umeyama_masked(P, Tg, cj, n, c0, sk, U);
         t12_to_16(U, U16);
         mat4_mul(U16, T, Tn);

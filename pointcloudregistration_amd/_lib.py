@@ -8,6 +8,7 @@ path or the test oracle).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -54,6 +55,8 @@ _ip = ctypes.POINTER(IcpParams)
 SIGNATURES = {
     "pcr_nnd_forward": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p],
     "pcr_nnd_backward": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p],
+    "pcr_nnd_forward_ragged": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p],
+    "pcr_nnd_forward_f64": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p],
     "pcr_feature_match": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p],
     "pcr_feature_correspondences": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p, _p],
     "pcr_correspondences": [_p, _p, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p],
@@ -64,6 +67,7 @@ SIGNATURES = {
     "pcr_icp_batch": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _ip, _p, _p, _p, _p, _p],
     "pcr_radius_nn": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _p, _p, _p],
     "pcr_procrustes_batch": [_p, _p, _p, _i32, _i32, _i32, _f64, _p, _p],
+    "pcr_procrustes_batch_f64": [_p, _p, _p, _i32, _i32, _i32, _f64, _p, _p],
     "pcr_lrf_count": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _p, _p],
     "pcr_lrf_compute": [_p, _i32, _i32, _p, _p, _i32, _p, _f64, _i32, _p, _i32, _p, _p, _p, _p],
     "pcr_ndp_warp": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
@@ -129,24 +133,43 @@ def load():
         lib.pcr_ndp_chamfer_scratch_bytes.argtypes = [_i32, _i32]
         lib.pcr_ndp_loss_scratch_bytes.restype = _i64
         lib.pcr_ndp_loss_scratch_bytes.argtypes = []
+        lib.pcr_ndp_chamfer_gacc_words.restype = _i64
+        lib.pcr_ndp_chamfer_gacc_words.argtypes = [_i32]
+        lib.pcr_ndp_chamfer_max_points.restype = _i32
+        lib.pcr_ndp_chamfer_max_points.argtypes = []
+        lib.pcr_shutdown.restype = ctypes.c_int
+        lib.pcr_shutdown.argtypes = []
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
             fn.argtypes = args
         _lib = lib
+        # free the library's device objects (workspace, profiling events) at
+        # interpreter exit, before torch's and the HIP runtime's own teardown
+        # (round 3 saw a crash in exit() after a profiled run)
+        atexit.register(shutdown)
         return lib
 
 
 def exported_symbols():
     return ["pcr_last_error", "pcr_version", "pcr_workspace_release", "pcr_profile_enable", "pcr_profile_read",
             "pcr_featnn_rescan_rows", "pcr_ndp_train_partial_floats", "pcr_ndp_chamfer_scratch_bytes",
-            "pcr_ndp_loss_scratch_bytes"] + \
+            "pcr_ndp_loss_scratch_bytes", "pcr_ndp_chamfer_gacc_words", "pcr_ndp_chamfer_max_points",
+            "pcr_shutdown"] + \
         list(SIGNATURES)
 
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
 PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID, PROF_FEAT_SCREEN2 = 5, 6, 7, 8
 PROF_SLOTS = 9   # pcr_internal.h kProfSlots
+
+
+def shutdown():
+    """pcr_shutdown(): synchronise and free the library's per-device workspace and
+    profiling events (idempotent; the library stays usable and re-allocates on
+    the next call).  Registered with atexit when the library is loaded."""
+    if _lib is not None:
+        _lib.pcr_shutdown()
 
 
 def profile_enable(on=True):

@@ -1,40 +1,115 @@
 """a3: Chamfer reductions on the nnd kernels (libpcr), with autograd.
 
-* ``compute_truncated_chamfer_distance(x, y, trunc=1e9, ...)`` mirrors
-  c2p-net/deformationpyramid/model/loss.py:60-218 as called by the NDP loop
-  (registration.py:236): squared 1-NN distances both ways, entries >= trunc
-  zeroed, point mean over the FULL length (the divisor keeps masked entries,
-  loss.py:151-154,187-195), batch mean, cham_x + cham_y.  pytorch3d.knn_points
-  is replaced by torch_nndistance's kernel (same squared-distance definition:
-  (dx*dx+dy*dy)+dz*dz in f32, first index on ties).
+* ``compute_truncated_chamfer_distance(x, y, x_lengths=None, y_lengths=None,
+  x_normals=None, y_normals=None, weights=None, trunc=0.2,
+  batch_reduction="mean", point_reduction="mean")`` -- the reference's own
+  signature and defaults (c2p-net/deformationpyramid/model/loss.py:60-71), so
+  positional calls bind as they do there.  Semantics of loss.py:104-218:
+  squared 1-NN distances both ways (pytorch3d.knn_points(lengths1, lengths2,
+  K=1) there, the nnd kernels here: (dx*dx+dy*dy)+dz*dz, first index on ties),
+  entries >= trunc and rows past a cloud's length zeroed, the point mean over
+  the cloud's LENGTH (masked entries stay in the divisor, loss.py:151-154,
+  187-195), optional per-cloud weights, batch mean/sum, cham_x + cham_y.
+  The normals are validated and, as in the reference (which computes
+  cham_norm_* and returns only cham_dist, loss.py:199-218), do not enter the
+  result.
 * ``chamfer_distance(x, y)`` = pytorch3d.loss.chamfer_distance's default
   (mean/mean) as used by dip/train.py:84,113 (returns (loss, None)).
 
-Homogeneous batches only (x (N,P1,3), y (N,P2,3)); the reference's
-heterogeneous-length path (x_lengths) is not used by its callers.
+dtypes: f32 and f64, each computed in its own precision (the reference runs
+knn_points in the inputs' dtype; validationScript.py:273-283 passes f64).  A
+homogeneous f32 batch takes the torch_nndistance kernels (pcr_nnd_forward /
+_backward); ragged or f64 batches take pcr_nnd_forward_ragged / _f64 for the
+indices, and the distances are formed from them with the same per-op-rounded
+expression in torch, so autograd differentiates them.  Other dtypes raise.
 """
 from __future__ import annotations
 
 import torch
 
+from . import _lib
 from .nndistance import nnd
 
 
-def _check(x, y):
-    if x.dim() != 3 or y.dim() != 3 or x.shape[2] != 3 or y.shape[2] != 3:
-        raise ValueError("x, y must be (N, P, 3)")
-    if x.shape[0] != y.shape[0]:
-        raise ValueError("y does not have the correct shape.")
-
-
-def compute_truncated_chamfer_distance(x, y, trunc=1e9, batch_reduction="mean",
-                                       point_reduction="mean", weights=None):
-    _check(x, y)
-    if point_reduction not in ("mean", "sum"):
-        raise ValueError('point_reduction must be one of ["mean", "sum"]')
-    if batch_reduction not in (None, "mean", "sum"):
+def _validate_reductions(batch_reduction, point_reduction):
+    # loss.py:9-16 (_validate_chamfer_reduction_inputs)
+    if batch_reduction is not None and batch_reduction not in ["mean", "sum"]:
         raise ValueError('batch_reduction must be one of ["mean", "sum"] or None')
-    N, P1, P2 = x.shape[0], x.shape[1], y.shape[1]
+    if point_reduction not in ["mean", "sum"]:
+        raise ValueError('point_reduction must be one of ["mean", "sum"]')
+
+
+def _handle_input(X, lengths, normals):
+    # loss.py:19-57 (_handle_pointcloud_input) for tensors; pytorch3d's
+    # Pointclouds class is absent (pytorch3d is not installed)
+    if not torch.is_tensor(X) or X.ndim != 3:
+        raise ValueError("The input pointclouds should be either Pointclouds objects or "
+                         "torch.Tensor of shape (minibatch, num_points, 3).")
+    if lengths is not None and (lengths.ndim != 1 or lengths.shape[0] != X.shape[0]):
+        raise ValueError("Expected lengths to be of shape (N,)")
+    if lengths is None:
+        lengths = torch.full((X.shape[0],), X.shape[1], dtype=torch.int64, device=X.device)
+    if normals is not None and normals.ndim != 3:
+        raise ValueError("Expected normals to be of shape (N, P, 3")
+    return X, lengths, normals
+
+
+def _sqdist(q, c):
+    d = c - q
+    return (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+
+
+def _nn_dists(x, y, x_lengths, y_lengths, hetero):
+    """(cham_x (N,P1), cham_y (N,P2)) squared 1-NN distances, differentiable."""
+    N, P1, _ = x.shape
+    P2 = y.shape[1]
+    if x.dtype == torch.float32 and not hetero:
+        return nnd(x.contiguous(), y.contiguous())
+    xc, yc = x.detach().contiguous(), y.detach().contiguous()
+    f64 = x.dtype == torch.float64
+    n1 = x_lengths.to(device=x.device, dtype=torch.int32).contiguous()
+    n2 = y_lengths.to(device=x.device, dtype=torch.int32).contiguous()
+    d1 = torch.empty(N, P1, dtype=x.dtype, device=x.device)
+    d2 = torch.empty(N, P2, dtype=x.dtype, device=x.device)
+    i1 = torch.empty(N, P1, dtype=torch.int32, device=x.device)
+    i2 = torch.empty(N, P2, dtype=torch.int32, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.call("pcr_nnd_forward_f64" if f64 else "pcr_nnd_forward_ragged", _lib.ptr(xc),
+                  _lib.ptr(yc), N, P1, P2, _lib.ptr(n1), _lib.ptr(n2), _lib.ptr(d1), _lib.ptr(d2),
+                  _lib.ptr(i1), _lib.ptr(i2), _lib.stream_handle(x.device))
+    # the kernel's distances re-formed from its indices with the same roundings,
+    # so autograd sees them; rows whose other cloud is empty keep the kernel's 0
+    cx = _sqdist(x, torch.gather(y, 1, i1.long()[..., None].expand(N, P1, 3)))
+    cy = _sqdist(y, torch.gather(x, 1, i2.long()[..., None].expand(N, P2, 3)))
+    cx = torch.where((n2 > 0)[:, None], cx, d1)
+    cy = torch.where((n1 > 0)[:, None], cy, d2)
+    return cx, cy
+
+
+def compute_truncated_chamfer_distance(x, y, x_lengths=None, y_lengths=None, x_normals=None,
+                                       y_normals=None, weights=None, trunc=0.2,
+                                       batch_reduction="mean", point_reduction="mean"):
+    _validate_reductions(batch_reduction, point_reduction)
+    x, x_lengths, x_normals = _handle_input(x, x_lengths, x_normals)
+    y, y_lengths, y_normals = _handle_input(y, y_lengths, y_normals)
+    N, P1, D = x.shape
+    P2 = y.shape[1]
+    if y.shape[0] != N or y.shape[2] != D:
+        raise ValueError("y does not have the correct shape.")
+    if D != 3:
+        raise ValueError("the nnd kernels take 3-D points (every caller of the reference passes xyz)")
+    if x.dtype != y.dtype or x.dtype not in (torch.float32, torch.float64):
+        raise TypeError(f"x and y must both be float32 or float64, got {x.dtype} / {y.dtype}")
+    if not x.is_cuda or x.device != y.device:
+        raise _lib.PcrError("compute_truncated_chamfer_distance: libpcr needs x, y on one GPU")
+    for nm, nrm, P in (("x_normals", x_normals, P1), ("y_normals", y_normals, P2)):
+        if nrm is not None and tuple(nrm.shape) != (N, P, D):
+            raise ValueError(f"{nm} must be of shape (N, P, D)")
+    x_lengths = x_lengths.to(x.device)
+    y_lengths = y_lengths.to(x.device)
+    hetero = bool((x_lengths != P1).any()) or bool((y_lengths != P2).any())
+    x_mask = torch.arange(P1, device=x.device)[None] >= x_lengths[:, None]  # (N, P1)
+    y_mask = torch.arange(P2, device=x.device)[None] >= y_lengths[:, None]  # (N, P2)
     if weights is not None:  # loss.py:127-139
         if weights.size(0) != N:
             raise ValueError("weights must be of shape (N,).")
@@ -45,17 +120,20 @@ def compute_truncated_chamfer_distance(x, y, trunc=1e9, batch_reduction="mean",
             if batch_reduction in ("mean", "sum"):
                 return ((x.sum((1, 2)) * w).sum() * 0.0, (x.sum((1, 2)) * w).sum() * 0.0)
             return ((x.sum((1, 2)) * w) * 0.0, (x.sum((1, 2)) * w) * 0.0)
-    dist1, dist2 = nnd(x.float().contiguous(), y.float().contiguous())
-    cham_x = torch.where(dist1 >= trunc, torch.zeros_like(dist1), dist1)
-    cham_y = torch.where(dist2 >= trunc, torch.zeros_like(dist2), dist2)
+    cham_x, cham_y = _nn_dists(x, y, x_lengths, y_lengths, hetero)
+    # truncation and lengths (loss.py:148-160)
+    x_mask = x_mask | (cham_x >= trunc)
+    y_mask = y_mask | (cham_y >= trunc)
+    cham_x = torch.where(x_mask, torch.zeros_like(cham_x), cham_x)
+    cham_y = torch.where(y_mask, torch.zeros_like(cham_y), cham_y)
     if weights is not None:
         cham_x = cham_x * weights.view(N, 1)
         cham_y = cham_y * weights.view(N, 1)
     cham_x = cham_x.sum(1)
     cham_y = cham_y.sum(1)
     if point_reduction == "mean":
-        cham_x = cham_x / P1
-        cham_y = cham_y / P2
+        cham_x = cham_x / x_lengths
+        cham_y = cham_y / y_lengths
     if batch_reduction is not None:
         cham_x = cham_x.sum()
         cham_y = cham_y.sum()
@@ -68,5 +146,6 @@ def compute_truncated_chamfer_distance(x, y, trunc=1e9, batch_reduction="mean",
 
 def chamfer_distance(x, y, batch_reduction="mean", point_reduction="mean"):
     """pytorch3d.loss.chamfer_distance(x, y) (no normals) -> (loss, None)."""
-    return compute_truncated_chamfer_distance(x, y, float("inf"), batch_reduction,
-                                              point_reduction), None
+    return compute_truncated_chamfer_distance(x, y, trunc=float("inf"),
+                                              batch_reduction=batch_reduction,
+                                              point_reduction=point_reduction), None

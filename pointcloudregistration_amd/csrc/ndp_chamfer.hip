@@ -19,9 +19,18 @@
 //     general kernel run a whole-cloud scan (428 us per C5 iteration);
 //   * the gradient dL/dxs is accumulated in the same epilogue: query i of the
 //     subset adds 2 gd1 (x_i - y_j), query k of the target subtracts
-//     2 gd2 (y_k - x_i) at its answer i, each rounded to 2^-44 fixed point and
-//     added with integer atomics (exact and order-free: the same bits on every
-//     replay), gd = 1/K, 1/M where d < trunc (else 0) as pcr_ndp_chamfer_glue;
+//     2 gd2 (y_k - x_i) at its answer i, each taken exactly to a two-word fixed
+//     point and added with integer atomics (exact and order-free: the same bits
+//     on every replay), gd = 1/K, 1/M where d < trunc (else 0) as
+//     pcr_ndp_chamfer_glue.  The scale follows the data (round 4): per
+//     iteration, from the subset's and the target's largest finite |coordinate|
+//     A_s, A_t, every finite term is at most T = 2 max(gd) (A_s + A_t), and an
+//     entry sums at most M + 1 of them, so with 2^s <= 2^60 / ((M + 2) T) no
+//     integer sum can overflow; a term v goes in as hi = rint(v 2^s) plus
+//     lo = rint((v 2^s - hi) 2^40), i.e. with a quantum 2^-(s+40) (~1e-29 at
+//     the C5 level's s = 57) -- relative precision for any term that matters,
+//     at unit or millimetre scale alike.  Only a non-finite term sets the flag
+//     (the gradient is then NaN, as the reference's would be);
 //     pcr_ndp_train_backward reads the sums.  This replaces the five-launch
 //     deterministic bucket backward of pcr_nnd_backward (~110 us per C5
 //     iteration).  Distances and indices are those of pcr_nnd_forward bit for
@@ -45,7 +54,6 @@ using nng::d2f;
 using nng::nhash;
 using nng::take;
 
-constexpr double kFixScale = 17592186044416.0;  // 2^44
 constexpr int kRep = PCR_NDP_GACC_REPLICAS;     // gradient sum replicas (query index mod kRep)
 constexpr int kFbQW = 16;                       // nc_fallback: listed queries per wave (8 packed pairs)
 constexpr int kFbQ = 4 * kFbQW, kFbSlice = 1024;  // work item: listed queries x candidates
@@ -58,6 +66,10 @@ struct NcHdr {
     int mode;       // sflag | tflag as nc_scan saw it (read by the queries)
     int fb_cnt[2];  // listed (uncertified) queries per direction
     int pad;
+    unsigned amax_t;  // the target's largest finite |coordinate| (f32 bits), prepare
+    unsigned amax_s;  // the subset's, this iteration (nc_count; nc_scan consumes and clears)
+    int shift;        // this iteration's fixed-point exponent s (nc_scan)
+    int pad2;
 };
 
 // one cloud's hashed grid (nng.h)
@@ -74,8 +86,9 @@ struct NcArgs {
     float trunc, g1, g2;    // g1 = 1/K, g2 = 1/M (as the glue)
     float *d1, *d2;
     int32_t *i1, *i2;
-    long long *gacc;        // [0]: non-finite contribution flag; [1 + 3 (r K + k) + c]: replica r of
-                            // dL/dxs[k][c] in fixed point (pcr_ndp_train_backward sums the replicas)
+    long long *gacc;        // [0]: bit 0 non-finite term, bits 8..: s + 2048; [1 + 3 (r K + k) + c]:
+                            // replica r of dL/dxs[k][c] hi words (2^-s), [1 + 3 K R + ...] lo words
+                            // (2^-(s+40)) (pcr_ndp_train_backward sums the replicas)
     NcHdr *hdr;
     int *cnt;               // counting-sort counts, zero between builds
     int *fb;                // K + M: listed queries (dir 0 at 0, dir 1 at K)
@@ -90,18 +103,25 @@ __device__ __forceinline__ bool cell_ok(float x, float y, float z, double ic) {
 
 // cell = 0.6 cbrt(bbox volume / n) of one cloud (nng_bbox's rule); flag on a
 // non-finite point.  One workgroup.
-__global__ __launch_bounds__(1024) void nc_bbox(const float *P, int n, float *cell, int *flag) {
+__global__ __launch_bounds__(1024) void nc_bbox(const float *P, int n, float *cell, int *flag,
+                                                unsigned *amax) {
     const int t = threadIdx.x;
     float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
     int bad = 0;
+    float am = 0.0f;  // largest finite |coordinate|
     for (int i = t; i < n; i += 1024)
         for (int c = 0; c < 3; ++c) {
             const float v = P[3 * i + c];
             bad |= !__builtin_isfinite(v);
             lo[c] = fminf(lo[c], v);
             hi[c] = fmaxf(hi[c], v);
+            if (__builtin_isfinite(v)) am = fmaxf(am, fabsf(v));
         }
+    if (amax) {
+        for (int o = 32; o; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+        if ((t & 63) == 0) atomicMax(amax, __float_as_uint(am));  // >= 0: bits order as values
+    }
     __shared__ float sl[3][16], sh[3][16];
     __shared__ int sb[16];
     for (int c = 0; c < 3; ++c)
@@ -139,19 +159,37 @@ __global__ __launch_bounds__(1024) void nc_bbox(const float *P, int n, float *ce
 // gradient sums of the subset), scan, scatter.  cnt is all-zero before count
 // and after scatter (scatter counts down).
 __global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, int *cnt, int *flag,
-                         long long *gacc, const double *gate) {
+                         long long *gacc, unsigned *amax, const double *gate) {
     if (gated_off(gate)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (gacc)
+    float am = 0.0f;
+    bool ok = false;
+    float x = 0.f, y = 0.f, z = 0.f;
+    double ic = 1.0;
+    if (i < n) {
+        if (gacc)
 #pragma unroll
-        for (int r = 0; r < kRep; ++r)
+            for (int r = 0; r < kRep; ++r)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) gacc[1 + 3 * ((size_t)r * n + i) + c] = 0;
-    const float x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
-    const double ic = 1.0 / (double)*cellp;
-    if (!cell_ok(x, y, z, ic)) { atomicOr(flag, 1); return; }
-    atomicAdd(cnt + nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), g.S), 1);
+                for (int c = 0; c < 3; ++c) {
+                    gacc[1 + 3 * ((size_t)r * n + i) + c] = 0;                      // hi words
+                    gacc[1 + 3 * ((size_t)kRep * n + (size_t)r * n + i) + c] = 0;   // lo words
+                }
+        x = P[3 * i]; y = P[3 * i + 1]; z = P[3 * i + 2];
+        ic = 1.0 / (double)*cellp;
+        ok = cell_ok(x, y, z, ic);
+        if (!ok) atomicOr(flag, 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float v = c == 0 ? x : (c == 1 ? y : z);
+            if (__builtin_isfinite(v)) am = fmaxf(am, fabsf(v));
+        }
+    }
+    if (amax) {  // the subset's largest finite |coordinate|, one atomic per wave
+        for (int o = 32; o; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+        if ((threadIdx.x & 63) == 0 && am > 0.0f) atomicMax(amax, __float_as_uint(am));
+    }
+    if (ok) atomicAdd(cnt + nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), g.S), 1);
 }
 
 // one workgroup: starts of the subset (or target) grid; the per-iteration
@@ -161,7 +199,7 @@ __global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, i
 constexpr int kScanLds = 32768;
 
 __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr *h, long long *gacc,
-                                                const double *gate) {
+                                                float gmax, int Mq, const double *gate) {
     if (gated_off(gate)) return;
     // LDS index i + i / 16: thread t's span [t per, (t+1) per) starts 17 t words
     // apart at per = 16 (no bank conflicts; the plain layout was 16-way)
@@ -198,7 +236,18 @@ __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr
         h->sflag = 0;
         h->fb_cnt[0] = 0;
         h->fb_cnt[1] = 0;
-        gacc[0] = 0;
+        // the fixed-point exponent of this iteration (header comment): every
+        // finite term <= T = 2 gmax (A_s + A_t), an entry sums <= M + 1 of them
+        const double T = 2.0 * (double)gmax *
+                         ((double)__uint_as_float(h->amax_s) + (double)__uint_as_float(h->amax_t)) *
+                         (1.0 + 0x1p-20);
+        const double B = (double)(Mq + 2) * T;
+        int sh = 60;
+        if (B > 0.0 && __builtin_isfinite(B)) sh = 59 - ilogb(B);  // B < 2^(ilogb+1): B 2^s < 2^60
+        sh = sh < -900 ? -900 : (sh > 900 ? 900 : sh);
+        h->shift = sh;
+        h->amax_s = 0u;
+        gacc[0] = (long long)(sh + 2048) << 8;
     }
 }
 
@@ -213,13 +262,21 @@ __global__ void nc_scatter(const float *P, int n, const float *cellp, NcCloud g,
     g.pts[g.start[hs] + atomicSub(cnt + hs, 1) - 1] = make_float4(x, y, z, __int_as_float(i));
 }
 
-__device__ __forceinline__ void fix_add(long long *dst, float v, long long *flag) {
-    if (!__builtin_isfinite(v) || fabs((double)v) >= 4096.0) {  // |v| 2^12: sums stay below 2^63
+// v exactly into the two words (hi at 2^-s, lo at 2^-(s+40)): t = v 2^s is exact
+// (a power-of-two scale of an f32), hi = rint(t), t - hi is exact (|t - hi| <=
+// 1/2), lo = rint((t - hi) 2^40); |hi| < 2^60 / (M + 2) by the choice of s
+__device__ __forceinline__ void fix_add(long long *hi, long long *lo, float v, int sh, long long *flag) {
+    if (!__builtin_isfinite(v)) {
         __hip_atomic_fetch_or(flag, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    __hip_atomic_fetch_add(dst, (long long)__builtin_rint((double)v * kFixScale), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    const double t = __builtin_ldexp((double)v, sh);
+    const double h = __builtin_rint(t);
+    const double l = __builtin_rint((t - h) * 0x1p40);
+    if (h != 0.0)
+        __hip_atomic_fetch_add(hi, (long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l != 0.0)
+        __hip_atomic_fetch_add(lo, (long long)l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the answer (best, bj) of query q in direction dir: outputs and gradient
@@ -227,22 +284,25 @@ __device__ __forceinline__ void fix_add(long long *dst, float v, long long *flag
 // The far target points of a partial overlap share a few boundary answers (up to
 // ~350 terms on one subset point in C5): the terms go to replica q mod kRep, so
 // same-address atomics stay short (integer sums: the replica split changes no bit)
-__device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best, int bj) {
+__device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best, int bj, int sh) {
     long long *rep = a.gacc + 1 + (size_t)(q & (kRep - 1)) * 3 * a.K;
+    const size_t lo = (size_t)3 * kRep * a.K;  // lo words after all hi words
     if (dir == 0) {
         a.d1[q] = best;
         a.i1[q] = bj;
         const float g = (!(best >= a.trunc) ? a.g1 : 0.0f) * 2;
         if (bj < 0 || bj >= a.M) return;
         for (int c = 0; c < 3; ++c)
-            fix_add(rep + 3 * q + c, g * (a.xs[3 * q + c] - a.tgt[3 * bj + c]), a.gacc);
+            fix_add(rep + 3 * q + c, rep + lo + 3 * q + c, g * (a.xs[3 * q + c] - a.tgt[3 * bj + c]), sh,
+                    a.gacc);
     } else {
         a.d2[q] = best;
         a.i2[q] = bj;
         const float g = (!(best >= a.trunc) ? a.g2 : 0.0f) * 2;
         if (bj < 0 || bj >= a.K) return;
         for (int c = 0; c < 3; ++c)
-            fix_add(rep + 3 * bj + c, -(g * (a.tgt[3 * q + c] - a.xs[3 * bj + c])), a.gacc);
+            fix_add(rep + 3 * bj + c, rep + lo + 3 * bj + c, -(g * (a.tgt[3 * q + c] - a.xs[3 * bj + c])), sh,
+                    a.gacc);
     }
 }
 
@@ -259,6 +319,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
     const int nq = dir ? a.M : a.K, nc = dir ? a.K : a.M;
     if (qslot >= nq) return;  // a query's lanes leave together
     const bool brute = a.hdr->mode != 0;
+    const int sh = a.hdr->shift;
     const float *Q = dir ? a.tgt : a.xs;
     const float *C = dir ? a.xs : a.tgt;
     int qi = qslot;
@@ -281,7 +342,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
             const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
             if (d < best) { best = d; bj = j; }
         }
-        emit(a, dir, qi, best, bj);
+        emit(a, dir, qi, best, bj, sh);
         return;
     }
     const nng::View v = dir ? nng::View{a.hdr->cell_s, a.cs.S, a.cs.start, a.cs.pts}
@@ -302,7 +363,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
             a.fbkey[e] = ~0ULL;
         }
     }
-    if (sub == 0 && done) emit(a, dir, qi, best, bj);
+    if (sub == 0 && done) emit(a, dir, qi, best, bj, sh);
 }
 
 // the listed queries: work item = (64 listed queries of one direction, a
@@ -407,7 +468,8 @@ __global__ __launch_bounds__(256) void nc_fallback_emit(NcArgs a) {
     const int dir = w < c0 ? 0 : 1;
     const int e = dir ? a.K + (w - c0) : w;
     const unsigned long long k = a.fbkey[e];
-    emit(a, dir, a.fb[e], __uint_as_float((unsigned)(k >> 32)), (int)(unsigned)(k & 0xffffffffu));
+    emit(a, dir, a.fb[e], __uint_as_float((unsigned)(k >> 32)), (int)(unsigned)(k & 0xffffffffu),
+         a.hdr->shift);
 }
 
 // the scan's dynamic LDS limit, set once outside any stream capture (prepare
@@ -492,16 +554,25 @@ extern "C" int64_t pcr_ndp_chamfer_scratch_bytes(int32_t K, int32_t M) {
     return (int64_t)pcr::nc_layout(K, M).total;
 }
 
+extern "C" int64_t pcr_ndp_chamfer_gacc_words(int32_t K) {
+    return K < 1 ? 0 : 1 + 6 * (int64_t)K * PCR_NDP_GACC_REPLICAS;
+}
+
+extern "C" int32_t pcr_ndp_chamfer_max_points(void) { return pcr::kScanLds; }
+
 namespace pcr {
 namespace {
 // count, scan, scatter and the coarse boxes of one cloud (cell from the header)
 int nc_build(const NcArgs &a, const float *P, int n, const float *cellp, const NcCloud &g, int *flag,
              long long *gacc, const double *gate, hipStream_t s) {
     const int nb = (n + 255) / 256;
-    hipLaunchKernelGGL(nc_count, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, flag, gacc, gate);
+    // the subset build (gacc given) also measures the subset's extent for the
+    // gradient's fixed-point exponent
+    hipLaunchKernelGGL(nc_count, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, flag, gacc,
+                       gacc ? &a.hdr->amax_s : (unsigned *)nullptr, gate);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1 + (g.S >> 4) + 1), s, (const int *)a.cnt, g,
-                       a.hdr, gacc, gate);
+                       a.hdr, gacc, a.g1 > a.g2 ? a.g1 : a.g2, a.M, gate);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(nc_scatter, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, gate);
     PCR_LAUNCH_CHECK();
@@ -520,9 +591,11 @@ extern "C" int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs
     PCR_HIP_CHECK(pcr::nc_scan_attr());
     PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, sizeof(pcr::NcHdr), s));
     PCR_HIP_CHECK(hipMemsetAsync(a.cnt, 0, sizeof(int) * (size_t)(a.St > a.Ss ? a.St : a.Ss), s));
-    hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, a.tgt, a.M, &a.hdr->cell_t, &a.hdr->tflag);
+    hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, a.tgt, a.M, &a.hdr->cell_t, &a.hdr->tflag,
+                       &a.hdr->amax_t);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, xs0, a.K, &a.hdr->cell_s, (int *)nullptr);
+    hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, xs0, a.K, &a.hdr->cell_s, (int *)nullptr,
+                       (unsigned *)nullptr);
     PCR_LAUNCH_CHECK();
     // the target grids, once (ungated: prepare runs outside the level graph)
     return pcr::nc_build(a, a.tgt, a.M, &a.hdr->cell_t, a.ct, &a.hdr->tflag, nullptr, nullptr, s);

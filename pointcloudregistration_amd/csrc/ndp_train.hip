@@ -195,16 +195,25 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
         const float x[3] = {a.x[3 * pt], a.x[3 * pt + 1], a.x[3 * pt + 2]};
         float g[3];
         if (a.inv && a.gacc) {
+            // the two-word fixed point of ndp_chamfer.hip: header word = flag bit 0,
+            // (s + 2048) << 8; hi words at 2^-s, lo words (after all hi) at 2^-(s+40)
             const int k = a.inv[pt];
-            const float bad = a.gacc[0] ? __builtin_nanf("") : 0.0f;
-            constexpr double kInv = 1.0 / 17592186044416.0;  // 2^-44
+            const long long hw = a.gacc[0];
+            const float bad = (hw & 1) ? __builtin_nanf("") : 0.0f;
+            const int sh = (int)(hw >> 8) - 2048;
+            const size_t lo = (size_t)3 * PCR_NDP_GACC_REPLICAS * a.gacc_k;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                long long v = 0;
+                long long vh = 0, vl = 0;
                 if (k >= 0)
 #pragma unroll
-                    for (int r = 0; r < PCR_NDP_GACC_REPLICAS; ++r) v += a.gacc[1 + 3 * ((size_t)r * a.gacc_k + k) + c];
-                g[c] = k >= 0 ? (float)((double)v * kInv) + bad : 0.0f;
+                    for (int r = 0; r < PCR_NDP_GACC_REPLICAS; ++r) {
+                        const size_t o = 1 + 3 * ((size_t)r * a.gacc_k + k) + c;
+                        vh += a.gacc[o];
+                        vl += a.gacc[o + lo];
+                    }
+                const double v = __builtin_ldexp((double)vh, -sh) + __builtin_ldexp((double)vl, -sh - 40);
+                g[c] = k >= 0 ? (float)v + bad : 0.0f;
             }
         } else if (a.inv) {
             const int k = a.inv[pt];

@@ -21,13 +21,16 @@ __device__ inline void tree256x(double (*red)[9], int nv) {
     }
 }
 
-__global__ __launch_bounds__(256) void procrustes_kernel(const float *src, const float *tgt,
-                                                         const float *w, int N, int absw, double eps,
+// Scalar = float (the f32 tensors of the drop-ins) or double (f64 callers:
+// the same sums, no narrowing of the inputs)
+template <typename Scalar>
+__global__ __launch_bounds__(256) void procrustes_kernel(const Scalar *src, const Scalar *tgt,
+                                                         const Scalar *w, int N, int absw, double eps,
                                                          double *T) {
     const int b = blockIdx.x, t = threadIdx.x;
-    const float *S = src + (size_t)b * N * 3;
-    const float *G = tgt + (size_t)b * N * 3;
-    const float *Wt = w + (size_t)b * N;
+    const Scalar *S = src + (size_t)b * N * 3;
+    const Scalar *G = tgt + (size_t)b * N * 3;
+    const Scalar *Wt = w + (size_t)b * N;
     __shared__ double red[256][9];
     double v = 0.0;
     for (int i = t; i < N; i += 256) {
@@ -75,17 +78,32 @@ __global__ __launch_bounds__(256) void procrustes_kernel(const float *src, const
 }  // namespace
 }  // namespace pcr
 
-extern "C" int pcr_procrustes_batch(const float *src, const float *tgt, const float *weights,
-                                    int32_t B, int32_t N, int32_t abs_weights, double eps,
-                                    double *T, pcr_stream_t stream) {
-    pcr::clear_error();
+namespace pcr {
+template <typename Scalar>
+static int procrustes_launch(const Scalar *src, const Scalar *tgt, const Scalar *weights, int32_t B,
+                             int32_t N, int32_t abs_weights, double eps, double *T,
+                             pcr_stream_t stream) {
+    clear_error();
     PCR_REQUIRE(B >= 0 && N >= 0, PCR_ERR_ARG, "procrustes: negative size");
     if (B == 0) return PCR_OK;
     PCR_REQUIRE(src && tgt && weights && T, PCR_ERR_ARG, "procrustes: null pointer");
-    hipLaunchKernelGGL(pcr::procrustes_kernel, dim3(B), dim3(256), 0, pcr::as_stream(stream), src,
+    hipLaunchKernelGGL(procrustes_kernel<Scalar>, dim3(B), dim3(256), 0, as_stream(stream), src,
                        tgt, weights, N, abs_weights, eps, T);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
+}
+}  // namespace pcr
+
+extern "C" int pcr_procrustes_batch(const float *src, const float *tgt, const float *weights,
+                                    int32_t B, int32_t N, int32_t abs_weights, double eps,
+                                    double *T, pcr_stream_t stream) {
+    return pcr::procrustes_launch(src, tgt, weights, B, N, abs_weights, eps, T, stream);
+}
+
+extern "C" int pcr_procrustes_batch_f64(const double *src, const double *tgt, const double *weights,
+                                        int32_t B, int32_t N, int32_t abs_weights, double eps,
+                                        double *T, pcr_stream_t stream) {
+    return pcr::procrustes_launch(src, tgt, weights, B, N, abs_weights, eps, T, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -719,15 +719,12 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     // be captured).  Its slots hold max_iteration - kRound0 hypotheses per pair;
     // past kAsyncSlots slots in all (huge batches) or with PCR_RANSAC_SYNC=1 the
     // host loop of kRoundN-hypothesis rounds runs instead (same results: a
-    // round boundary cannot change the sequential decisions).
-    constexpr long long kAsyncSlots = 1LL << 26;
+    // round boundary cannot change the sequential decisions).  The round's
+    // slots are capped by BYTES (kAsyncBytes; C4's 256 pairs x 98,976 slots take
+    // ~3.3 GB of the 288 GB), and when their allocation fails the host loop's
+    // kRoundN slots are used instead of failing (decided below, after split).
+    constexpr double kAsyncBytes = 16.0 * (1 << 30);
     const int span1 = a.max_iter > kRound0 ? (a.max_iter - kRound0 + 255) / 256 * 256 : 0;
-    const bool gated = env_int("PCR_RANSAC_SYNC", 0) == 0 &&
-                       (long long)P * std::max(span1, kRound0) <= kAsyncSlots;
-    // hypotheses per round slot: the largest round that can run (kRound0 when
-    // max_iteration fits the first round), a multiple of 256
-    a.hcap = a.max_iter > kRound0 ? (gated ? std::max(span1, kRound0) : kRoundN)
-                                  : std::max(256, (std::max(a.max_iter, 1) + 255) / 256 * 256);
     // target slots of the first tasks of every pair (the best's are kept from
     // there; a best without one is swept again at the end): up to 32 per pair
     // within 256 MB
@@ -736,14 +733,9 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.nslots = std::max(0, std::min(a.nslots, env_int("PCR_RANSAC_SLOTS", a.nslots)));
     a.bestbuf = (int32_t *)workspace(21, per);
     a.state = (RState *)workspace(22, sizeof(RState) * (size_t)P);
-    a.hypT = (double *)workspace(23, sizeof(double) * 12 * (size_t)P * a.hcap);
-    a.hypbits = (unsigned long long *)workspace(24, sizeof(unsigned long long) * (size_t)P * (a.hcap / 64));
     a.hdr = (RHeader *)workspace(25, 2 * sizeof(RHeader) + sizeof(int) * (size_t)P);
-    a.tasks = (int *)workspace(29, sizeof(int) * (size_t)P * a.hcap);
-    a.res = (TaskRes *)workspace(30, sizeof(TaskRes) * (size_t)P * a.hcap);
     a.slots = (int32_t *)workspace(31, a.nslots > 0 ? per * a.nslots : 16);
-    PCR_REQUIRE(a.bestbuf && a.state && a.hypT && a.hypbits && a.hdr && a.tasks && a.res && a.slots,
-                PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
+    PCR_REQUIRE(a.bestbuf && a.state && a.hdr && a.slots, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
     a.ntask = (int *)(a.hdr + 2);
     a.prev_active = nullptr;
     a.grid = GridBatch{};
@@ -795,10 +787,29 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     PCR_REQUIRE(split == 1 || split == 2 || split == 4 || split == 8, PCR_ERR_ARG,
                 "ransac: PCR_RANSAC_SPLIT=%d (1, 2, 4 or 8)", split);
     a.split = split;
-    a.parts = nullptr;
-    if (a.split > 1) {
-        a.parts = (TaskPart *)workspace(32, sizeof(TaskPart) * (size_t)a.split * P * a.hcap);
-        PCR_REQUIRE(a.parts, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
+    // the per-hypothesis slots of a round: transforms, pass bits, task list,
+    // results (+ split parts)
+    const double slot_bytes = 12.0 * sizeof(double) + sizeof(unsigned long long) / 64.0 + sizeof(int) +
+                              sizeof(TaskRes) + (split > 1 ? (double)split * sizeof(TaskPart) : 0.0);
+    bool gated = env_int("PCR_RANSAC_SYNC", 0) == 0 &&
+                 (double)P * std::max(span1, kRound0) * slot_bytes <= kAsyncBytes;
+    auto alloc_slots = [&](bool g) {
+        // hypotheses per round slot: the largest round that can run (kRound0 when
+        // max_iteration fits the first round), a multiple of 256
+        a.hcap = a.max_iter > kRound0 ? (g ? std::max(span1, kRound0) : kRoundN)
+                                      : std::max(256, (std::max(a.max_iter, 1) + 255) / 256 * 256);
+        a.hypT = (double *)workspace(23, sizeof(double) * 12 * (size_t)P * a.hcap);
+        a.hypbits = (unsigned long long *)workspace(24, sizeof(unsigned long long) * (size_t)P * (a.hcap / 64));
+        a.tasks = (int *)workspace(29, sizeof(int) * (size_t)P * a.hcap);
+        a.res = (TaskRes *)workspace(30, sizeof(TaskRes) * (size_t)P * a.hcap);
+        a.parts = split > 1 ? (TaskPart *)workspace(32, sizeof(TaskPart) * (size_t)split * P * a.hcap) : nullptr;
+        return a.hypT && a.hypbits && a.tasks && a.res && (split == 1 || a.parts);
+    };
+    if (!alloc_slots(gated)) {
+        PCR_REQUIRE(gated, PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
+        clear_error();
+        gated = false;  // the host loop's smaller rounds (same results)
+        PCR_REQUIRE(alloc_slots(false), PCR_ERR_NOMEM, "ransac: %s", pcr_last_error());
     }
     const int rnarg = a.rn;
     const bool stats_env = env_int("PCR_RANSAC_STATS", 0) != 0;

@@ -190,5 +190,60 @@ extern "C" int pcr_workspace_release(void) {
     return PCR_OK;
 }
 
+// Process-end teardown (round 4): a profiled run (rocprofv3 --kernel-trace) of
+// round 3 crashed inside exit() after its last output, in a library finaliser;
+// the library's process-lifetime device objects -- workspace slots, retired
+// buffers, pooled profiling events -- were never released and outlived the
+// runtime's own teardown.  pcr_shutdown() releases all of them while the runtime
+// is intact (Python's atexit runs it first; bench.py also calls it).  Idempotent;
+// the library re-allocates on its next call.
+extern "C" int pcr_shutdown(void) {
+    pcr::clear_error();
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return PCR_OK; }
+    int rc = PCR_OK;
+    {
+        std::lock_guard<std::mutex> lk(pcr::g_pmu);
+        pcr::g_prof_on = false;
+        for (auto &r : pcr::g_pending) {
+            (void)hipEventSynchronize(r.e);
+            (void)hipEventDestroy(r.b);
+            (void)hipEventDestroy(r.e);
+        }
+        pcr::g_pending.clear();
+        for (hipEvent_t e : pcr::g_free) (void)hipEventDestroy(e);
+        pcr::g_free.clear();
+    }
+    {
+        std::lock_guard<std::mutex> lk(pcr::g_mu);
+        for (int dev = 0; dev < pcr::kMaxDevices; ++dev) {
+            bool any = false;
+            for (auto &sl : pcr::g_slots[dev]) any = any || sl.ptr;
+            for (auto &r : pcr::g_retired) any = any || r.first == dev;
+            if (!any) continue;
+            if (hipSetDevice(dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                (void)hipGetLastError();
+                pcr::set_error("shutdown: device %d not synchronisable", dev);
+                rc = PCR_ERR_HIP;
+                continue;
+            }
+            for (auto &sl : pcr::g_slots[dev]) {
+                if (sl.ptr) (void)hipFree(sl.ptr);
+                sl.ptr = nullptr;
+                sl.bytes = 0;
+            }
+        }
+        std::vector<std::pair<int, void *>> keep;
+        for (auto &r : pcr::g_retired) {
+            if (hipSetDevice(r.first) == hipSuccess) (void)hipFree(r.second);
+            else keep.push_back(r);
+        }
+        pcr::g_retired.swap(keep);
+    }
+    (void)hipSetDevice(cur);
+    (void)hipGetLastError();
+    return rc;
+}
+
 extern "C" const char *pcr_last_error(void) { return pcr::g_err; }
 extern "C" int pcr_version(void) { return 1; }

@@ -368,13 +368,19 @@ class _LevelFused(_Level):
             t.inv, t.xs, t.gsub = self.inv.data_ptr(), self.xs.data_ptr(), self.gsub.data_ptr()
         # the level's Chamfer with its gradient in one pass (csrc/ndp_chamfer.hip):
         # the target grid built once here, the subset grid rebuilt per iteration
-        self.use_nc = self.use_inv and K >= 1 and M >= 1 and os.environ.get("PCR_NDP_CHAMFER", "1") != "0"
+        # the fused pass holds each cloud's grid starts in one workgroup's LDS
+        # (K, M <= pcr_ndp_chamfer_max_points()); larger clouds -- an unsampled
+        # target above 32K points (c2p.register_c2p passes tgt whole, as the
+        # reference's t_sample = tgt_pcd does) -- take the nnd drop-in path
+        lim = int(_lib.load().pcr_ndp_chamfer_max_points())
+        self.use_nc = (self.use_inv and 1 <= K <= lim and 1 <= M <= lim
+                       and os.environ.get("PCR_NDP_CHAMFER", "1") != "0")
         if self.use_nc:
             lib = _lib.load()
             nbytes = int(lib.pcr_ndp_chamfer_scratch_bytes(K, M))
             self.nc_raw = torch.empty(nbytes + 256, dtype=torch.uint8, device=dev)
             off = (-self.nc_raw.data_ptr()) % 256
-            self.gacc = torch.zeros(1 + 3 * K * GACC_REPLICAS, dtype=torch.int64, device=dev)
+            self.gacc = torch.zeros(int(lib.pcr_ndp_chamfer_gacc_words(K)), dtype=torch.int64, device=dev)
             c = _ChamferC()
             c.xs, c.tgt, c.K, c.M, c.trunc = self.xs.data_ptr(), self.t3.data_ptr(), K, M, 1e9
             c.d1, c.d2, c.i1, c.i2 = (self.d1.data_ptr(), self.d2.data_ptr(), self.i1.data_ptr(),
@@ -479,7 +485,11 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
         st = lv.state.cpu().numpy()
         t2 = time.perf_counter()
         info.append({"steps": int(st[3]), "evaluated": int(st[6]), "last_loss": float(st[4]),
-                     "losses": lv.log[:int(st[6])].cpu().numpy()})
+                     "losses": lv.log[:int(st[6])].cpu().numpy(),
+                     # which path ran: the fused HIP MLP kernels (width 128) or torch
+                     # autograd, and the fused level Chamfer or the nnd drop-in kernels
+                     "mlp": "fused" if use_fused else "torch",
+                     "chamfer": "fused" if getattr(lv, "use_nc", False) else "nnd"})
         ev = getattr(lv, "replay_events", None)
         if ev is not None:
             info[-1]["replay_ms"] = ev[0].elapsed_time(ev[1])

@@ -51,7 +51,13 @@ def default_params(seed=0):
 
 
 class PairPipeline:
-    """Holds device-resident inputs and per-stage outputs for P pairs."""
+    """Holds device-resident inputs and per-stage outputs for P pairs.
+
+    Buffer lifetime: the results of ``run()`` (the BatchResults' tensors, the
+    Chamfer column) and ``records()`` are VIEWS of buffers preallocated once
+    and rewritten by the next ``run()`` -- so a step allocates nothing and the
+    whole step is one C-ABI call.  A caller that keeps results across steps
+    takes ``records(copy=True)`` (or ``.clone()``s what it keeps)."""
 
     def __init__(self, src, tgt, src_feat, tgt_feat, params: PipelineParams, pair_ids=None,
                  device=None):
@@ -151,9 +157,10 @@ class PairPipeline:
         ev = self.stage_events
         return [ev[k].elapsed_time(ev[k + 1]) for k in range(5)]
 
-    def records(self):
+    def records(self, copy=False):
         """(P, RECORD_WIDTH) f64 per-pair result records (device), written by the
         step (pcr_pipeline_records): T_ransac (16), T_icp (16), RANSAC fitness /
         rmse, ICP fitness / rmse, Chamfer, RANSAC iterations, RANSAC status,
-        correspondences after the mutual filter."""
-        return self.rec
+        correspondences after the mutual filter.  The buffer itself (valid until
+        the next run()) unless copy=True."""
+        return self.rec.clone() if copy else self.rec

@@ -20,18 +20,22 @@ from . import _lib
 
 
 def procrustes_batch(src, tgt, weights, abs_weights, eps):
-    """(B,N,3),(B,N,3),(B,N) -> T (B,3,4) f64 on the GPU: tgt ~ R src + t."""
+    """(B,N,3),(B,N,3),(B,N) -> T (B,3,4) f64 on the GPU: tgt ~ R src + t.
+    f64 sources run on f64 inputs (pcr_procrustes_batch_f64), anything else on
+    f32 (pcr_procrustes_batch); the sums and the solve are f64 either way."""
     S = torch.as_tensor(src)
     dev = S.device if S.is_cuda else torch.device("cuda", torch.cuda.current_device())
-    S = S.to(dev, torch.float32).contiguous()
-    G = torch.as_tensor(tgt).to(dev, torch.float32).contiguous()
-    W = torch.as_tensor(weights).to(dev, torch.float32).reshape(S.shape[0], S.shape[1]).contiguous()
+    dt = torch.float64 if S.dtype == torch.float64 else torch.float32
+    S = S.to(dev, dt).contiguous()
+    G = torch.as_tensor(tgt).to(dev, dt).contiguous()
+    W = torch.as_tensor(weights).to(dev, dt).reshape(S.shape[0], S.shape[1]).contiguous()
     if S.dim() != 3 or S.shape[2] != 3 or G.shape != S.shape:
         raise ValueError("src/tgt must both be (B, N, 3)")
     B, N = S.shape[0], S.shape[1]
     T = torch.empty(B, 3, 4, dtype=torch.float64, device=dev)
     with torch.cuda.device(dev):
-        _lib.call("pcr_procrustes_batch", _lib.ptr(S), _lib.ptr(G), _lib.ptr(W), B, N,
+        _lib.call("pcr_procrustes_batch_f64" if dt == torch.float64 else "pcr_procrustes_batch",
+                  _lib.ptr(S), _lib.ptr(G), _lib.ptr(W), B, N,
                   int(abs_weights), float(eps), _lib.ptr(T), _lib.stream_handle(dev))
     return T
 

@@ -79,6 +79,10 @@ def test_c5_ndp_stage_vs_reference_loop(c5):
     info, hist = res["info"], res["hist"]
     assert len(info) == CFG["m"]
     for lvl in range(CFG["m"]):
+        # the fused HIP path ran (width 128 MLP kernels, the level Chamfer pass,
+        # graph replays) -- not the torch-autograd or nnd fallbacks
+        assert info[lvl]["mlp"] == "fused" and info[lvl]["chamfer"] == "fused", info[lvl]
+        assert "replay_ms" in info[lvl], lvl
         want = g[f"loss/l{lvl}"]
         got = info[lvl]["losses"]
         assert info[lvl]["evaluated"] == len(want), (lvl, info[lvl]["evaluated"], len(want))

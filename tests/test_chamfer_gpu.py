@@ -101,3 +101,178 @@ def test_chamfer_distance_pytorch3d_default(oracle, golden_nnd):
     assert nrm is None
     ref = np_truncated_chamfer(oracle, x, y, np.inf)
     np.testing.assert_allclose(float(loss), ref, rtol=1e-6)
+
+
+# --------------------------------------------------------------------------
+# the reference's full interface (loss.py:60-71): lengths, normals, f64
+# --------------------------------------------------------------------------
+def np_chamfer_full(oracle, x, y, xl, yl, trunc, br="mean", pr="mean", weights=None):
+    """loss.py:104-218 in numpy on ragged clouds: per cloud the oracle's nnd of
+    x[k,:xl[k]] vs y[k,:yl[k]] (f32) or an f64 brute force (f64 inputs)."""
+    N = x.shape[0]
+    cx_s, cy_s = np.zeros(N), np.zeros(N)
+    for k in range(N):
+        a, b = x[k, :xl[k]], y[k, :yl[k]]
+        if x.dtype == np.float32:
+            d1, d2, _, _ = oracle.nnd_forward(a[None], b[None])
+            d1, d2 = d1[0].astype(np.float64), d2[0].astype(np.float64)
+        else:
+            d1, d2 = np_nn_f64(a, b)[0], np_nn_f64(b, a)[0]
+        cx = np.where(d1 >= trunc, 0.0, d1)
+        cy = np.where(d2 >= trunc, 0.0, d2)
+        if weights is not None:
+            cx, cy = cx * weights[k], cy * weights[k]
+        cx_s[k], cy_s[k] = cx.sum(), cy.sum()
+    if pr == "mean":
+        cx_s, cy_s = cx_s / xl, cy_s / yl
+    if br is not None:
+        cx_s, cy_s = cx_s.sum(), cy_s.sum()
+        if br == "mean":
+            div = weights.sum() if weights is not None else N
+            cx_s, cy_s = cx_s / div, cy_s / div
+    return cx_s + cy_s
+
+
+def np_nn_f64(q, c):
+    """f64 1-NN: d = (dx*dx + dy*dy) + dz*dz, dx = c - q, first index of the min."""
+    if len(c) == 0:
+        return np.zeros(len(q)), np.zeros(len(q), np.int64)
+    d = c[None, :, :] - q[:, None, :]
+    D = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+    j = np.argmin(D, axis=1)
+    return D[np.arange(len(q)), j], j
+
+
+def _ragged(seed, N, P1, P2, dtype=np.float32):
+    rng = np.random.default_rng(seed)
+    x = rng.random((N, P1, 3)).astype(dtype)
+    y = (rng.random((N, P2, 3)) * 1.2 - 0.1).astype(dtype)
+    xl = rng.integers(P1 // 3, P1 + 1, N)
+    yl = rng.integers(P2 // 3, P2 + 1, N)
+    xl[0], yl[-1] = P1, P2
+    return x, y, xl, yl
+
+
+def test_chamfer_reference_signature_and_defaults(oracle):
+    """Positional binding and defaults of loss.py:60-71 (trunc=0.2, mean/mean)."""
+    x, y = _clouds(5, 2, 900, 1100)
+    X, Y = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    got = compute_truncated_chamfer_distance(X, Y)
+    ref = np_truncated_chamfer(oracle, x, y, 0.2)
+    np.testing.assert_allclose(float(got), ref, rtol=1e-6)
+    w = np.array([0.7, 1.5], np.float32)
+    xl, yl = np.array([900, 600]), np.array([800, 1100])
+    got = compute_truncated_chamfer_distance(
+        X, Y, torch.from_numpy(xl).cuda(), torch.from_numpy(yl).cuda(), None, None,
+        torch.from_numpy(w).cuda(), 0.01, "sum", "mean")
+    ref = np_chamfer_full(oracle, x, y, xl, yl, 0.01, "sum", "mean", w.astype(np.float64))
+    np.testing.assert_allclose(float(got), ref, rtol=1e-6)
+    with pytest.raises(TypeError):
+        compute_truncated_chamfer_distance(X.half(), Y.half())
+    with pytest.raises(ValueError):
+        compute_truncated_chamfer_distance(X, Y, point_reduction="max")
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("br,pr", [("mean", "mean"), ("sum", "sum"), (None, "mean")])
+def test_chamfer_ragged_lengths_vs_numpy(oracle, dtype, br, pr):
+    x, y, xl, yl = _ragged(17, 4, 1500, 1200, dtype)
+    # padding rows hold far-away junk that must not be found or counted
+    for k in range(4):
+        x[k, xl[k]:] = 50.0
+        y[k, yl[k]:] = -50.0
+    got = compute_truncated_chamfer_distance(
+        torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda(), torch.from_numpy(xl).cuda(),
+        torch.from_numpy(yl).cuda(), trunc=0.004, batch_reduction=br, point_reduction=pr)
+    assert got.dtype == (torch.float64 if dtype == np.float64 else torch.float32)
+    ref = np_chamfer_full(oracle, x, y, xl, yl, 0.004, br, pr)
+    np.testing.assert_allclose(got.detach().cpu().numpy(), ref, rtol=1e-12 if dtype == np.float64 else 1e-6)
+
+
+def test_nnd_ragged_kernel_bitexact_vs_oracle(oracle):
+    """pcr_nnd_forward_ragged: per cloud == the reference-pinned oracle on the
+    cloud's own points (ties, duplicates, NaN rows, an empty cloud); rows past
+    a length and rows whose other cloud is empty are (0, 0)."""
+    from pointcloudregistration_amd import _lib
+    rng = np.random.default_rng(3)
+    N, P1, P2 = 5, 1300, 700
+    x = (np.round(rng.random((N, P1, 3)) * 8) / 8).astype(np.float32)   # many ties
+    y = (np.round(rng.random((N, P2, 3)) * 8) / 8).astype(np.float32)
+    x[1, 5] = np.nan
+    y[2, 0] = np.nan                                 # candidate-0 NaN seed rule
+    xl = np.array([P1, 1000, 1, 77, 1300], np.int32)
+    yl = np.array([P2, 650, 700, 0, 1], np.int32)    # cloud 3 has an empty y
+    X, Y = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    out = [torch.full((N, P), 7, dtype=t, device="cuda") for P, t in
+           ((P1, torch.float32), (P2, torch.float32), (P1, torch.int32), (P2, torch.int32))]
+    n1, n2 = torch.from_numpy(xl).cuda(), torch.from_numpy(yl).cuda()
+    _lib.call("pcr_nnd_forward_ragged", _lib.ptr(X), _lib.ptr(Y), N, P1, P2, _lib.ptr(n1),
+              _lib.ptr(n2), *[_lib.ptr(o) for o in out], _lib.stream_handle(X.device))
+    d1, d2, i1, i2 = (o.cpu().numpy() for o in out)
+    for k in range(N):
+        a, b = x[k, :xl[k]], y[k, :yl[k]]
+        if len(b):
+            e1, _, j1, _ = oracle.nnd_forward(a[None], b[None])
+            assert np.array_equal(d1[k, :xl[k]].view(np.int32) & 0x7fffffff,
+                                  e1[0].view(np.int32) & 0x7fffffff), k
+            assert np.array_equal(i1[k, :xl[k]], j1[0]), k
+        else:
+            assert not d1[k, :xl[k]].any() and not i1[k, :xl[k]].any()
+        if len(a) and len(b):
+            _, e2, _, j2 = oracle.nnd_forward(a[None], b[None])
+            assert np.array_equal(d2[k, :yl[k]].view(np.int32) & 0x7fffffff,
+                                  e2[0].view(np.int32) & 0x7fffffff), k
+            assert np.array_equal(i2[k, :yl[k]], j2[0]), k
+        assert not d1[k, xl[k]:].any() and not i1[k, xl[k]:].any()
+        assert not d2[k, yl[k]:].any() and not i2[k, yl[k]:].any()
+
+
+def test_nnd_f64_kernel_vs_numpy():
+    from pointcloudregistration_amd import _lib
+    rng = np.random.default_rng(8)
+    N, P1, P2 = 3, 2000, 900
+    x = rng.standard_normal((N, P1, 3)) * 1e3          # mm-scale, f64 resolution matters
+    y = x[:, :P2] + rng.standard_normal((N, P2, 3)) * 1e-9
+    X, Y = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    d1 = torch.empty(N, P1, dtype=torch.float64, device="cuda")
+    d2 = torch.empty(N, P2, dtype=torch.float64, device="cuda")
+    i1 = torch.empty(N, P1, dtype=torch.int32, device="cuda")
+    i2 = torch.empty(N, P2, dtype=torch.int32, device="cuda")
+    _lib.call("pcr_nnd_forward_f64", _lib.ptr(X), _lib.ptr(Y), N, P1, P2, None, None, _lib.ptr(d1),
+              _lib.ptr(d2), _lib.ptr(i1), _lib.ptr(i2), _lib.stream_handle(X.device))
+    for k in range(N):
+        e1, j1 = np_nn_f64(x[k], y[k])
+        e2, j2 = np_nn_f64(y[k], x[k])
+        assert np.array_equal(d1[k].cpu().numpy(), e1) and np.array_equal(i1[k].cpu().numpy(), j1)
+        assert np.array_equal(d2[k].cpu().numpy(), e2) and np.array_equal(i2[k].cpu().numpy(), j2)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_chamfer_ragged_gradient(oracle, dtype):
+    """d loss / d x for ragged clouds: 2 (x - y_nn) / (N len_x) on kept rows plus
+    the scatter of the y-side terms, zero on padding rows."""
+    x, y, xl, yl = _ragged(23, 3, 800, 600, dtype)
+    X = torch.from_numpy(x).cuda().requires_grad_(True)
+    Y = torch.from_numpy(y).cuda().requires_grad_(True)
+    compute_truncated_chamfer_distance(X, Y, torch.from_numpy(xl).cuda(), torch.from_numpy(yl).cuda(),
+                                       trunc=1e9).backward()
+    gx = np.zeros(x.shape)
+    gy = np.zeros(y.shape)
+    N = 3
+    for k in range(N):
+        a, b = x[k, :xl[k]].astype(np.float64), y[k, :yl[k]].astype(np.float64)
+        if dtype == np.float32:   # the f32 argmin (reference-pinned oracle)
+            _, _, j1, j2 = oracle.nnd_forward(x[k:k + 1, :xl[k]], y[k:k + 1, :yl[k]])
+            j1, j2 = j1[0], j2[0]
+        else:
+            _, j1 = np_nn_f64(a, b)
+            _, j2 = np_nn_f64(b, a)
+        t1 = 2 * (a - b[j1]) / (N * xl[k])
+        t2 = 2 * (b - a[j2]) / (N * yl[k])
+        gx[k, :xl[k]] += t1
+        np.add.at(gy[k], j1, -t1)
+        gy[k, :yl[k]] += t2
+        np.add.at(gx[k], j2, -t2)
+    tol = 1e-12 if dtype == np.float64 else 2e-6
+    np.testing.assert_allclose(X.grad.cpu().numpy(), gx, atol=tol * np.abs(gx).max())
+    np.testing.assert_allclose(Y.grad.cpu().numpy(), gy, atol=tol * np.abs(gy).max())

@@ -6,13 +6,18 @@ my_lib.cpp: test_nnd_gpu.py).
   (PCR_NDP_CHAMFER_RINGS 0..3: more or fewer queries go to the tiled exact
   scan), on a partially overlapping pair (a third of the target far from the
   subset), quantised ties, and with a NaN (the reference loop);
-* the gradient (2^-44 fixed-point sums): vs pcr_nnd_backward with
-  gd1 = 1/K, gd2 = 1/M (0 where d >= trunc), 2e-6 of the largest entry + 1e-12
-  (f32 terms summed exactly vs summed in f32 in index order);
+* the gradient (exact two-word fixed-point sums of the f32 terms, the exponent
+  taken from the iteration's extents): per entry within 1e-12 relative of the
+  exact sum of the same f32 terms (numpy, f64) -- on unit-scale, near-converged
+  (1e-9 offsets) and millimetre / 1e7-scale pairs, where the round-3 2^-44
+  quantum lost small entries and |terms| >= 4096 turned the gradient into NaN;
+  and vs pcr_nnd_backward (f32 sums in the reference's index order) within
+  2e-6 of the largest entry;
 * repeated steps (the per-iteration resets) give the same bits; a closed gate
   skips the step.
 """
 import ctypes
+import math
 import os
 
 import numpy as np
@@ -35,7 +40,7 @@ class _Nc:
         self.d1, self.d2 = torch.zeros(K, **f), torch.zeros(M, **f)
         self.i1 = torch.zeros(K, dtype=torch.int32, **f)
         self.i2 = torch.zeros(M, dtype=torch.int32, **f)
-        self.gacc = torch.zeros(1 + 3 * K * GACC_REPLICAS, dtype=torch.int64, **f)
+        self.gacc = torch.zeros(int(_lib.load().pcr_ndp_chamfer_gacc_words(K)), dtype=torch.int64, **f)
         nb = int(_lib.load().pcr_ndp_chamfer_scratch_bytes(K, M))
         self.raw = torch.empty(nb + 256, dtype=torch.uint8, **f)
         c = _ChamferC()
@@ -52,9 +57,20 @@ class _Nc:
         _lib.call("pcr_ndp_chamfer_step", ctypes.byref(self.c), _lib.stream_handle())
         torch.cuda.synchronize()
 
+    def grad64(self):
+        """(dL/dxs (K, 3) f64 decoded from the two words, non-finite flag, s)."""
+        a = self.gacc.cpu().numpy()
+        hw = int(a[0])
+        sh = (hw >> 8) - 2048
+        n = 3 * self.K * GACC_REPLICAS
+        hi = a[1:1 + n].reshape(GACC_REPLICAS, self.K, 3).sum(0)
+        lo = a[1 + n:1 + 2 * n].reshape(GACC_REPLICAS, self.K, 3).sum(0)
+        g = np.ldexp(hi.astype(np.float64), -sh) + np.ldexp(lo.astype(np.float64), -sh - 40)
+        return g, hw & 1, sh
+
     def grad(self):
-        g = self.gacc[1:].reshape(GACC_REPLICAS, self.K, 3).sum(0).double() * 2.0 ** -44
-        return g.float(), int(self.gacc[0])
+        g, bad, _ = self.grad64()
+        return torch.from_numpy(g).float().cuda(), bad
 
 
 def _reference(xs, tgt, trunc):
@@ -69,6 +85,28 @@ def _reference(xs, tgt, trunc):
     nnd_backward_cuda(xs[None].contiguous(), tgt[None].contiguous(), g1, g2, gd1, gd2, i1, i2)
     torch.cuda.synchronize()
     return d1[0], d2[0], i1[0], i2[0], g1[0]
+
+
+def _exact_grad(xs, tgt, d1, d2, i1, i2, trunc):
+    """The kernel's f32 terms (emit: g = f32(1/K) * 2 where d < trunc, term =
+    g * (x - y) in f32; the target side -(g2 * (y - x))) summed in f64."""
+    xs, tgt = xs.cpu().numpy(), tgt.cpu().numpy()
+    d1, d2, i1, i2 = (t.cpu().numpy() for t in (d1, d2, i1, i2))
+    K, M = len(xs), len(tgt)
+    g1 = np.where(d1 >= trunc, np.float32(0), np.float32(1.0 / K)) * np.float32(2)
+    g2 = np.where(d2 >= trunc, np.float32(0), np.float32(1.0 / M)) * np.float32(2)
+    t0 = (g1[:, None] * (xs - tgt[i1])).astype(np.float64)
+    t1 = (-(g2[:, None] * (tgt - xs[i2]))).astype(np.float64)
+    # correctly rounded sums per entry (math.fsum): the fixed point is exact, so
+    # the comparison must not carry f64 summation error of its own
+    order = np.argsort(i2, kind="stable")
+    starts = np.searchsorted(i2[order], np.arange(K + 1))
+    out = np.empty((K, 3))
+    for k in range(K):
+        rows = order[starts[k]:starts[k + 1]]
+        for c in range(3):
+            out[k, c] = math.fsum([t0[k, c], *t1[rows, c]])
+    return out
 
 
 def _partial_pair(seed, K=6000, M=12000):
@@ -100,7 +138,18 @@ def _check(xs, tgt, trunc=1e9, rings=None):
     assert bad == 0
     tol = 2e-6 * float(g1.abs().max()) + 1e-12
     assert torch.allclose(g, g1, atol=tol, rtol=0), float((g - g1).abs().max())
+    _check_exact(nc, trunc)
     return nc
+
+
+def _check_exact(nc, trunc):
+    """Per entry: the two-word sums == the exact sum of the f32 terms."""
+    g, bad, sh = nc.grad64()
+    assert bad == 0
+    want = _exact_grad(nc.xs, nc.tgt, nc.d1, nc.d2, nc.i1, nc.i2, trunc)
+    err = np.abs(g - want)
+    assert np.all(err <= 1e-12 * np.abs(want) + 2.0 ** (-sh - 30)), (float(err.max()), sh)
+    return g, want
 
 
 @pytest.mark.parametrize("rings", [0, 1, 2, 3])
@@ -139,7 +188,7 @@ def test_nan_switches_to_reference_loop():
     assert torch.equal(nc.i1, i1) and torch.equal(nc.i2, i2)
     assert torch.equal(torch.nan_to_num(nc.d1, nan=-1.0), torch.nan_to_num(d1, nan=-1.0))
     assert torch.equal(torch.nan_to_num(nc.d2, nan=-1.0), torch.nan_to_num(d2, nan=-1.0))
-    assert nc.grad()[1] != 0  # the NaN term is flagged (the backward returns NaN)
+    assert nc.grad64()[1] != 0  # the NaN term is flagged (the backward returns NaN)
 
 
 def test_repeated_steps_and_moving_subset():
@@ -159,6 +208,30 @@ def test_repeated_steps_and_moving_subset():
     assert torch.equal(nc.d2, d2) and torch.equal(nc.i2, i2)
     g, _ = nc.grad()
     assert torch.allclose(g, g1, atol=2e-6 * float(g1.abs().max()) + 1e-12, rtol=0)
+    _check_exact(nc, 1e9)   # the exponent follows the moved (larger) subset
+
+
+@pytest.mark.parametrize("scale,offset", [(1.0, 0.0), (1000.0, 500.0), (1e7, 0.0)])
+def test_gradient_relative_precision_any_scale(scale, offset):
+    """Near-converged pair (every subset point 1e-9 x scale from a target
+    point) at unit, millimetre (x1000, +500) and 1e7 scale: the small terms keep
+    their relative precision; at 1e7 the terms reach 2e6 x 2/K >= 4096, where
+    round 3 flagged the whole gradient NaN -- now finite and exact."""
+    rng = np.random.default_rng(31)
+    t = rng.uniform(-1, 1, (4000, 3))
+    s = t[:1500] + rng.normal(0, 1e-9, (1500, 3))
+    tgt = torch.from_numpy((t * scale + offset).astype(np.float32)).cuda()
+    xs = torch.from_numpy((s * scale + offset).astype(np.float32)).cuda()
+    nc = _Nc(xs, tgt)
+    nc.step()
+    d1, d2, i1, i2, g1 = _reference(xs, tgt, 1e9)
+    assert torch.equal(nc.d1, d1) and torch.equal(nc.i1, i1)
+    assert torch.equal(nc.d2, d2) and torch.equal(nc.i2, i2)
+    g, want = _check_exact(nc, 1e9)
+    assert np.isfinite(g).all()
+    small = np.abs(want) > 0
+    rel = np.abs(g[small] - want[small]) / np.abs(want[small])
+    assert rel.max() <= 1e-12, rel.max()
 
 
 def test_gate_closed_skips_step():

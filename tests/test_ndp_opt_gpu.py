@@ -96,3 +96,31 @@ def test_early_stop_rule_on_device():
             prev = L
             host.append(1)
         assert dev_steps == host, (ratio, mb, dev_steps, host)
+
+
+def test_large_target_takes_nnd_path():
+    """a target above pcr_ndp_chamfer_max_points() (32,768: an
+    unsampled target, c2p.register_c2p passes tgt whole) runs the level Chamfer
+    on the nnd drop-in kernels instead of failing; the same level with the
+    target cut to the limit runs the fused pass."""
+    from pointcloudregistration_amd import _lib
+    lim = int(_lib.load().pcr_ndp_chamfer_max_points())
+    rng = np.random.default_rng(5)
+    tgt = rng.uniform(-0.5, 0.5, (lim + 7000, 3)).astype(np.float32)
+    src = (tgt[:3000] + rng.normal(0, 0.01, (3000, 3))).astype(np.float32)
+    cfg = dict(CFG, iters=3, m=1)
+    torch.manual_seed(0)
+    P = ndp_opt.DeformationPyramid(cfg["depth"], cfg["width"], torch.device("cuda"), cfg["k0"], 1, True)
+    sd = {k: v.clone() for k, v in P.pyramid[0].state_dict().items()}
+    _, _, _, info = ndp_opt.optimize_deformation_pyramid(torch.from_numpy(src).cuda(),
+                                                         torch.from_numpy(tgt).cuda(),
+                                                         np.arange(0, 3000, 2), cfg, NDP=P)
+    assert info[0]["chamfer"] == "nnd" and info[0]["mlp"] == "fused"
+    assert np.isfinite(info[0]["losses"]).all()
+    # the same level with the target cut below the limit runs the fused pass
+    P2 = ndp_opt.DeformationPyramid(cfg["depth"], cfg["width"], torch.device("cuda"), cfg["k0"], 1, True)
+    P2.pyramid[0].load_state_dict(sd)
+    _, _, _, info2 = ndp_opt.optimize_deformation_pyramid(torch.from_numpy(src).cuda(),
+                                                          torch.from_numpy(tgt[:lim]).cuda(),
+                                                          np.arange(0, 3000, 2), cfg, NDP=P2)
+    assert info2[0]["chamfer"] == "fused"

@@ -150,3 +150,31 @@ def test_oracle_voxel_down_sample_known_answer(oracle):
     assert np.allclose(got, [[0.1, 1.0 / 30.0, 1.0 / 30.0], [1.0, 1.0, 1.0]], rtol=0, atol=1e-15)
     with pytest.raises(ValueError):
         oracle.voxel_down_sample(pts, 0.0)
+
+
+def test_oracle_estimation_vs_reference_kabsch_c1(oracle):
+    """The RANSAC / ICP estimation of the oracle (== the GPU, tests/) against the
+    reference's own f64 SVD Kabsch (ROPNet weighted_icp in f64) on the C1 pair's
+    correspondence sets (tests/golden/estimation_golden.npz): the RANSAC result
+    is the best hypothesis' 3-point estimate (||dR||_F, ||dt|| <= 1e-12), every
+    ICP update within 1e-10 (the exact sums' 2^-k quantum); icp_trace is the
+    loop itself."""
+    g = np.load(os.path.join(GOLD, "estimation_golden.npz"))
+    s, t, corr = g["c1/src"], g["c1/tgt"], g["c1/corr"]
+    o = oracle.ransac(s, t, corr, 0.04, seed=0, pair_id=0)
+    assert np.array_equal(o["T"], g["c1/T_ransac"])
+    samp = oracle.ransac_sample(0, 0, o["best_itr"], len(corr))
+    assert np.array_equal(samp, g["c1/sample"])
+    ref = g["c1/T_sample_ref64"]
+    assert np.linalg.norm(o["T"][:3, :3] - ref[:3, :3]) <= 1e-12
+    assert np.linalg.norm(o["T"][:3, 3] - ref[:3, 3]) <= 1e-12
+    tr = oracle.icp_trace(s, t, 0.02, init=o["T"])
+    full = oracle.icp(s, t, 0.02, init=o["T"])
+    assert np.array_equal(tr["T"], full["T"]) and tr["iters"] == full["iters"]
+    Tk, dT = g["c1/T_icp_k"], g["c1/dT_icp_ref64"]
+    assert len(Tk) == tr["iters"] + 1
+    for k in range(1, len(Tk)):
+        want = dT[k - 1] @ Tk[k - 1]
+        assert np.linalg.norm(Tk[k][:3, :3] - want[:3, :3]) <= 1e-10
+        assert np.linalg.norm(Tk[k][:3, 3] - want[:3, 3]) <= 1e-10
+        assert int((tr["cj"][k - 1] >= 0).sum()) == int(g["c1/icp_ncorr"][k - 1])
