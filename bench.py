@@ -53,6 +53,9 @@ def parse():
                     help="skip the PCIe-inclusive (host-resident inputs) measurement")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the C2 / a4 / a10 / f1 / f4 side measurements")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="split the rank's shard into this many sub-batches run concurrently on "
+                         "their own HIP streams (1..4)")
     return ap.parse_args()
 
 
@@ -1119,10 +1122,32 @@ def main():
                         pair_ids=pair_ids)
 
     rows = -(-args.pairs // world)   # equal-size record blocks for the all-gather
+    S = max(1, min(args.streams, 4, P))
+    if S > 1:
+        # the shard as S sub-batches, each a pipeline with its own workspace
+        # context on its own stream: one sub-batch's latency-bound stages (RANSAC
+        # rounds, ICP iterations) overlap another's screens
+        _lib.call("pcr_set_concurrency", S)
+        cuts = [P * k // S for k in range(S + 1)]
+        subs = [PairPipeline(batch.src[a:b], batch.tgt[a:b], batch.src_feat[a:b], batch.tgt_feat[a:b],
+                             params, pair_ids=pair_ids[a:b], context=k)
+                for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:]))]
+        sub_streams = [torch.cuda.Stream() for _ in range(S)]
+        rec_all = torch.empty((P, 40), dtype=torch.float64, device="cuda")
 
     def step():
-        pipe.run()
-        return gather_records(pipe.records(), world, rows)
+        if S == 1:
+            pipe.run()
+            return gather_records(pipe.records(), world, rows)
+        cur = torch.cuda.current_stream()
+        for k in range(S):
+            sub_streams[k].wait_stream(cur)
+            with torch.cuda.stream(sub_streams[k]):
+                subs[k].run()
+                rec_all[cuts[k]:cuts[k + 1]].copy_(subs[k].records())
+        for k in range(S):
+            cur.wait_stream(sub_streams[k])
+        return gather_records(rec_all, world, rows)
 
     for _ in range(args.warmup):
         step()
@@ -1132,6 +1157,8 @@ def main():
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
     wall, rec = run_timed(step, args.steps, 0, world)
+    if S > 1:
+        _lib.call("pcr_set_concurrency", 1)
     prof = {name: _lib.profile_read(pid) for name, pid in
             (("feature_screen", _lib.PROF_FEAT_SCREEN), ("nnd_fwd", _lib.PROF_NND_FWD),
              ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
@@ -1208,6 +1235,7 @@ def main():
                 f"descriptors (noise {args.feat_noise}), generated per rank (seeds 1000+pair)",
         "config": {"workload": "C4: batch of augmented TOF/PC pairs (featNN+RANSAC+ICP+Chamfer)",
                    "pairs_total": args.pairs, "pairs_per_gpu": P, "points": N, "feature_dim": D,
+                   "streams_per_gpu": S,
                    "ransac": "d=0.04 mutual n=3 edge0.9 dist0.04 (100000,0.999)",
                    "icp": "d=0.02 (1e-6,1e-6,30)", "parallelism": f"pair-sharded x{world}",
                    "inputs": "resident in HBM (see host_resident for the PCIe-inclusive rate)"},

@@ -46,6 +46,14 @@ int pcr_workspace_release(void);
  * workspace, retired buffers and pooled profiling events (idempotent; the
  * library stays usable).  The Python layer runs it from atexit. */
 int pcr_shutdown(void);
+/* Concurrent sub-batches.  pcr_set_workspace_context(ctx) (thread-local, 0..3)
+ * selects which copy of the library's scratch the calling thread's next calls
+ * use: calls that run concurrently on different streams must use different
+ * contexts.  pcr_set_concurrency(k) (1..4): k launches share the device, so
+ * cooperative grids (ICP's workgroups per pair) are sized to CUs / k and k of
+ * them can be resident at once. */
+int pcr_set_workspace_context(int32_t ctx);
+int pcr_set_concurrency(int32_t k);
 
 /* Optional per-kernel timing with HIP events recorded on the launch stream
  * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,

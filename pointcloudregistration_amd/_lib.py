@@ -55,6 +55,8 @@ _ip = ctypes.POINTER(IcpParams)
 SIGNATURES = {
     "pcr_nnd_forward": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p],
     "pcr_nnd_backward": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p],
+    "pcr_set_workspace_context": [_i32],
+    "pcr_set_concurrency": [_i32],
     "pcr_nnd_forward_ragged": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p],
     "pcr_nnd_forward_f64": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p],
     "pcr_feature_match": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p],

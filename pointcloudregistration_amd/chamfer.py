@@ -90,6 +90,9 @@ def compute_truncated_chamfer_distance(x, y, x_lengths=None, y_lengths=None, x_n
                                        y_normals=None, weights=None, trunc=0.2,
                                        batch_reduction="mean", point_reduction="mean"):
     _validate_reductions(batch_reduction, point_reduction)
+    # without lengths the batch is homogeneous by construction: no device read
+    # (the NDP loop calls this inside a captured HIP graph, ndp_opt.py)
+    given = x_lengths is not None or y_lengths is not None
     x, x_lengths, x_normals = _handle_input(x, x_lengths, x_normals)
     y, y_lengths, y_normals = _handle_input(y, y_lengths, y_normals)
     N, P1, D = x.shape
@@ -107,7 +110,7 @@ def compute_truncated_chamfer_distance(x, y, x_lengths=None, y_lengths=None, x_n
             raise ValueError(f"{nm} must be of shape (N, P, D)")
     x_lengths = x_lengths.to(x.device)
     y_lengths = y_lengths.to(x.device)
-    hetero = bool((x_lengths != P1).any()) or bool((y_lengths != P2).any())
+    hetero = given and (bool((x_lengths != P1).any()) or bool((y_lengths != P2).any()))
     x_mask = torch.arange(P1, device=x.device)[None] >= x_lengths[:, None]  # (N, P1)
     y_mask = torch.arange(P2, device=x.device)[None] >= y_lengths[:, None]  # (N, P2)
     if weights is not None:  # loss.py:127-139

@@ -882,12 +882,26 @@ struct RowArgs5 {
     float *e;
     int *list, *count;
     float *w1, *w2;             // pass 2: top-2 values by original row index
+    const float *Fr, *Gc;       // pass 1: the f32 rows / columns (the winner's tile in its group)
 };
 
 // RT row tiles per wave share every B fragment read (two MFMAs per ds_read):
 // a workgroup covers 8 * RT * 32 rows per pass over the pair's column stream,
 // which halves the L2 -> LDS traffic at RT = 2 (at RT = 1 the stream of the
 // packed columns ran near the chip's LDS-DMA rate: waves parked ~35 %).
+//
+// Pass 1's index (round 4): the row top-2 runs on the raw values (2 VALU per
+// distance), and the index is kept per LDS GROUP of G column tiles, not per
+// tile: at the end of a group every running minimum that changed during it
+// (bits != its copy from the group start) gets the group number in its low
+// ctbits mantissa bits (4 VALU per row value per group, i.e. 0.5 per distance
+// at G = 8, against 1 per distance for the per-tile code).  After the lane
+// merge a row's minimum names (group, column lane), i.e. G candidate columns;
+// for a certified row the winner is the exact f64 argmin among those G (a
+// certified winner is the row's exact argmin, so it is the argmin of any
+// candidate set holding it).  A minimum replaced by a value with the same bits
+// keeps its older group: then the row's top-2 holds two equal values, so it
+// is uncertified and rescanned exactly.
 template <int S, int G, bool kIdx, int RT>
 __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     constexpr int W = 8;              // waves per workgroup, RT 32-row tiles each
@@ -931,10 +945,16 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         }
     }
     float b1[RT][16], b2[RT][16];
+    float s1[kIdx ? RT : 1][16];  // pass 1: b1 at the start of the current group
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { b1[t][r] = __builtin_inff(); b2[t][r] = __builtin_inff(); }
+    if constexpr (kIdx)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s1[t][r] = __builtin_inff();
     const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
     auto issue = [&](int grp, int bufi) {
         for (int c = wid; c < G * NM; c += W) {
@@ -944,28 +964,40 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                 (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
         }
     };
-    // row top-2 of the tile's 16 values per lane: pass 1 with the column tile
-    // index in the low ctbits bits (3 VALU per value), pass 2 values only (2).
+    // row top-2 of the tile's 16 values per lane, values only (2 VALU per
+    // value; pass 1's group code is applied at the group's end, above).
     // No inline asm here: the compiler must see every instruction that touches
     // the accumulators (its MFMA hazard wait states are not placed around
     // inline asm; with asm v_min / v_med3 the first registers of some tiles
     // read stale values).  min(a, b) is written med3(a, b, -FLT_MAX): the min
     // builtin would add a NaN canonicalisation per operand.  A NaN value makes
     // the row's top-2 NaN (uncertified: the exact rescan decides it).
-    auto epilogue = [&](const f32x16 (&acc)[RT], unsigned ct) {
-        asm("" : "+s"(ct));
+    auto epilogue = [&](const f32x16 (&acc)[RT], unsigned) {
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                float vr;
-                if constexpr (kIdx) vr = __uint_as_float((__float_as_uint(acc[t][r]) & keep_r) | ct);
-                else vr = acc[t][r];
+                const float vr = acc[t][r];
                 b2[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], b2[t][r], vr);
                 b1[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], vr, -3.40282347e+38f);
             }
     };
-    constexpr int kV = (kIdx ? 48 : 32) * RT / NX + 1;  // VALU per MFMA slot below
+    // pass 1, end of group grp: the minima that changed during it take its number
+    auto group_code = [&](unsigned grp) {
+        asm("" : "+s"(grp));
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const unsigned cur = __float_as_uint(b1[t][r]);
+                unsigned pk;  // one v_and_or (the compiler splits the expression in two)
+                asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(pk) : "v"(cur), "v"(keep_r), "s"(grp));
+                const unsigned nv = cur != __float_as_uint(s1[t][r]) ? pk : cur;
+                b1[t][r] = __uint_as_float(nv);
+                s1[t][r] = __uint_as_float(nv);
+            }
+    };
+    constexpr int kV = 32 * RT / NX + 1;  // VALU per MFMA slot below
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1007,6 +1039,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             __builtin_amdgcn_sched_barrier(0);
         }
         epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1));
+        if constexpr (kIdx) group_code((unsigned)grp);
         // the next group's DMA has landed for every wave, and every wave is done
         // reading this buffer before the group after next overwrites it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1045,15 +1078,35 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                 a.e[o] = 0.0f;
                 continue;
             }
-            a.nn[o] = mi1;
             const double Gm = (double)__uint_as_float(a.cmax[p]);
             const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
             const double bnd = bound5(qn, Gm, 16 * NX, a.D);
             const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
             a.v[o] = (double)mb1;
             a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-            if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
+            if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)))) {
+                a.nn[o] = 0;  // the exact rescan writes it
                 a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
+                continue;
+            }
+            // certified: the exact argmin among the G columns of the winning
+            // group in the winning lane, f64 distances in the oracle's order
+            const int gw = mi1 >> 5, col = mi1 & 31, D = a.D;
+            const float *fr = a.Fr + ((size_t)p * a.Rmax + row) * D;
+            double best = __builtin_inf();
+            int bj = gw * G * 32 + col;
+            for (int u = 0; u < G; ++u) {
+                const int j = (gw * G + u) * 32 + col;
+                if (j >= m) break;
+                const float *gc = a.Gc + ((size_t)p * a.Cmax + j) * D;
+                double acc = 0.0;
+                for (int k = 0; k < D; ++k) {
+                    const double df = (double)fr[k] - (double)gc[k];
+                    acc = acc + df * df;
+                }
+                if (acc < best) { best = acc; bj = j; }
+            }
+            a.nn[o] = bj;
         } else {
 #pragma unroll
             for (int o = 1; o < 32; o <<= 1) {
@@ -1351,6 +1404,8 @@ static int feature_match_v5(const float *F, const float *G, int P, int Nmax, int
 // (two up to D = 32; one above, where two tiles' accumulators and fragments
 // spilled at S = 4: 256 VGPRs + 179 spilled)
 constexpr int row_tiles(int S) { return S <= 2 ? 2 : 1; }
+// column tiles per LDS group of the row screens (featnn_row7's G)
+constexpr int row_group(int S) { return S <= 2 ? 8 : 4; }
 
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
@@ -1360,7 +1415,7 @@ static int launch_row7(const RowArgs5 &r, int S, hipStream_t s) {
     switch (S) {
 #define PCR_R7CASE(K)                                                                            \
     case K:                                                                                      \
-        hipLaunchKernelGGL((featnn_row7<K, (K <= 2 ? 8 : 4), kIdx, row_tiles(K)>), dim3((unsigned)nblk), \
+        hipLaunchKernelGGL((featnn_row7<K, row_group(K), kIdx, row_tiles(K)>), dim3((unsigned)nblk), \
                            dim3(512), 0, s, r);                                                  \
         break;
         PCR_R7CASE(1) PCR_R7CASE(2) PCR_R7CASE(3) PCR_R7CASE(4)
@@ -1408,7 +1463,9 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.Ap = v.Ap; r.Bp = v.Bp; r.rnr = v.fnr; r.cmax = v.gmax; r.n_rows = n_src; r.n_cols = n_tgt;
     r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
     r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * row_tiles(v.S)); r.D = D; r.ctbits = 1;
-    while ((1 << r.ctbits) < ntm) ++r.ctbits;
+    // pass 1 codes the LDS group of column tiles (featnn_row7's G), not the tile
+    while ((1 << r.ctbits) < cdiv(ntm, row_group(v.S))) ++r.ctbits;
+    r.Fr = F; r.Gc = G;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;
     prof_begin(s, kProfFeatScreen);

@@ -13,6 +13,15 @@
 #include <hip/hip_runtime.h>
 #include "geom.h"
 
+// grid_query's candidate test: 0 = one 16-byte read (x, y, z, index) and the
+// f64 distance; 1 = an 8-byte read of (x, y), the f64 partial (dx^2 + dy^2) --
+// exactly the first rounded term of dist2's ((dx^2 + dy^2) + dz^2), which
+// rounding can only raise, so a partial >= thr rejects the candidate as the
+// full test would -- and (z, index) read only for the survivors
+#ifndef PCR_GQ_XY
+#define PCR_GQ_XY 0
+#endif
+
 namespace pcr {
 
 __device__ __forceinline__ int cell_coord(double v, double cell) {
@@ -38,6 +47,8 @@ struct GridView {
         ax = v.x; ay = v.y; az = v.z; aw = v.w;
     }
     __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
+    __device__ __forceinline__ float2 load_xy(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s]; }
+    __device__ __forceinline__ float2 load_zw(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s + 1]; }
 };
 
 // LDS copy for the consumers that own a pair (RANSAC, ICP): one float4 per
@@ -55,6 +66,8 @@ struct GridP4 {
         ax = v.x; ay = v.y; az = v.z; aw = v.w;
     }
     __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
+    __device__ __forceinline__ float2 load_xy(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s]; }
+    __device__ __forceinline__ float2 load_zw(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s + 1]; }
 };
 
 // squared distance from p to cell c's box [c*cell, (c+1)*cell] along one axis,
@@ -155,6 +168,29 @@ __device__ __forceinline__ int grid_query(const View &g, double r, double thr, d
                 s = (int)(q[0] & 0xffffu);
                 e = (int)(q[0] >> 16);
             }
+#if PCR_GQ_XY
+            float2 cxy[kW];
+#pragma unroll
+            for (int u = 0; u < kW; ++u) cxy[u] = g.load_xy(sl[u]);
+            double pxy[kW];
+#pragma unroll
+            for (int u = 0; u < kW; ++u) {
+                const double dx = (double)cxy[u].x - px, dy = (double)cxy[u].y - py;
+                pxy[u] = dx * dx + dy * dy;
+            }
+#pragma unroll
+            for (int u = 0; u < kW; ++u) {
+                if (ok[u] && pxy[u] < thr) {
+                    const float2 zw = g.load_zw(sl[u]);
+                    const double dz = (double)zw.x - pz;
+                    const double d2 = pxy[u] + dz * dz;
+                    if (d2 < thr) {
+                        const int j = g.index_of(sl[u], zw.y);
+                        if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; if constexpr (kSlot) bs = sl[u]; }
+                    }
+                }
+            }
+#else
             float cx[kW], cy[kW], cz[kW], cw[kW];
 #pragma unroll
             for (int u = 0; u < kW; ++u) g.load(sl[u], cx[u], cy[u], cz[u], cw[u]);
@@ -168,6 +204,7 @@ __device__ __forceinline__ int grid_query(const View &g, double r, double thr, d
                     if (dd[u] < best || (dd[u] == best && j < bj)) { best = dd[u]; bj = j; if constexpr (kSlot) bs = sl[u]; }
                 }
             }
+#endif
         }
     } else {
         for (int x = x0; x <= x1; ++x) {

@@ -90,6 +90,8 @@ struct NcArgs {
                             // replica r of dL/dxs[k][c] hi words (2^-s), [1 + 3 K R + ...] lo words
                             // (2^-(s+40)) (pcr_ndp_train_backward sums the replicas)
     NcHdr *hdr;
+    int fshift;             // diagnostics (PCR_NDP_FIXSHIFT): a fixed exponent, hi words only
+                            // (round 3's 2^-44 quantum at 44); -1: the data-scaled two words
     int *cnt;               // counting-sort counts, zero between builds
     int *fb;                // K + M: listed queries (dir 0 at 0, dir 1 at K)
     unsigned long long *fbkey;  // K + M: their (d bits, j) minima
@@ -199,7 +201,7 @@ __global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, i
 constexpr int kScanLds = 32768;
 
 __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr *h, long long *gacc,
-                                                float gmax, int Mq, const double *gate) {
+                                                float gmax, int Mq, int fshift, const double *gate) {
     if (gated_off(gate)) return;
     // LDS index i + i / 16: thread t's span [t per, (t+1) per) starts 17 t words
     // apart at per = 16 (no bank conflicts; the plain layout was 16-way)
@@ -245,6 +247,7 @@ __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr
         int sh = 60;
         if (B > 0.0 && __builtin_isfinite(B)) sh = 59 - ilogb(B);  // B < 2^(ilogb+1): B 2^s < 2^60
         sh = sh < -900 ? -900 : (sh > 900 ? 900 : sh);
+        if (fshift >= 0) sh = 1000 + fshift;  // marks "hi words only" for fix_add
         h->shift = sh;
         h->amax_s = 0u;
         gacc[0] = (long long)(sh + 2048) << 8;
@@ -270,9 +273,11 @@ __device__ __forceinline__ void fix_add(long long *hi, long long *lo, float v, i
         __hip_atomic_fetch_or(flag, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
+    const bool hi_only = sh >= 1000;  // diagnostics: round 3's single word
+    if (hi_only) sh -= 1000;
     const double t = __builtin_ldexp((double)v, sh);
     const double h = __builtin_rint(t);
-    const double l = __builtin_rint((t - h) * 0x1p40);
+    const double l = hi_only ? 0.0 : __builtin_rint((t - h) * 0x1p40);
     if (h != 0.0)
         __hip_atomic_fetch_add(hi, (long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (l != 0.0)
@@ -543,6 +548,8 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     a.fb = (int *)(s + L.fb);
     a.fbkey = (unsigned long long *)(s + L.fbkey);
     a.gate = current_gate();
+    a.fshift = -1;
+    if (const char *e = getenv("PCR_NDP_FIXSHIFT")) a.fshift = atoi(e);
     return PCR_OK;
 }
 
@@ -572,7 +579,7 @@ int nc_build(const NcArgs &a, const float *P, int n, const float *cellp, const N
                        gacc ? &a.hdr->amax_s : (unsigned *)nullptr, gate);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(nc_scan, dim3(1), dim3(1024), sizeof(int) * ((size_t)g.S + 1 + (g.S >> 4) + 1), s, (const int *)a.cnt, g,
-                       a.hdr, gacc, a.g1 > a.g2 ? a.g1 : a.g2, a.M, gate);
+                       a.hdr, gacc, a.g1 > a.g2 ? a.g1 : a.g2, a.M, a.fshift, gate);
     PCR_LAUNCH_CHECK();
     hipLaunchKernelGGL(nc_scatter, dim3(nb), dim3(256), 0, s, P, n, cellp, g, a.cnt, gate);
     PCR_LAUNCH_CHECK();

@@ -200,7 +200,8 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
             const int k = a.inv[pt];
             const long long hw = a.gacc[0];
             const float bad = (hw & 1) ? __builtin_nanf("") : 0.0f;
-            const int sh = (int)(hw >> 8) - 2048;
+            int sh = (int)(hw >> 8) - 2048;
+            if (sh >= 1000) sh -= 1000;  // diagnostics: hi words only (PCR_NDP_FIXSHIFT)
             const size_t lo = (size_t)3 * PCR_NDP_GACC_REPLICAS * a.gacc_k;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {

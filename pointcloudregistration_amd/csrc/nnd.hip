@@ -12,10 +12,12 @@
 //    4 candidates x Q queries);
 //  * padded candidates are NaN, which the strict '<' update skips, so the inner
 //    loop has no tail branch;
-//  * when the candidate axis is split (small b), partial results merge through
-//    a 64-bit atomicMin on (float bits << 32 | index): for the non-negative
-//    distances this orders by distance then index, i.e. exactly "first index of
-//    the minimum", independent of slice arrival order.
+//  * when the candidate axis is split (small b), every slice writes its (d, j)
+//    partial to scratch and nnd_finalize_kernel takes the minimum over the
+//    slices in slice order (strict <: the earlier slice -- the lower index --
+//    keeps a tie), i.e. exactly "first index of the minimum";
+//  * small problems (C2: one pair of 4096) use 2 queries per lane and
+//    128-candidate tiles, so even b = 1 launches ~512 workgroups.
 // Numerics: d = (dx*dx + dy*dy) + dz*dz, each op rounded (built with
 // -ffp-contract=off), dx = cand.x - query.x as in my_lib.cpp:12-15.
 #include "pcr_internal.h"
@@ -26,7 +28,8 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTileK = 512;  // candidates per LDS stage (6 KiB)
+constexpr int kTileBig = 512;    // candidates per LDS stage (6 KiB)
+constexpr int kTileSmall = 128;  // small problems: more, shorter slices
 
 __device__ __forceinline__ float sqdist(float qx, float qy, float qz, float cx, float cy,
                                         float cz) {
@@ -43,10 +46,11 @@ struct NndArgs {
     float *dist2;
     int32_t *idx1;
     int32_t *idx2;
-    unsigned long long *keys1;  // split-candidate mode only
-    unsigned long long *keys2;
+    float *pd;                  // split-candidate mode: [slice][2][b][nmax] partial minima
+    int32_t *pj;                //   and their indices
     int b, n, m;
-    int slice_len;  // candidates per blockIdx.y slice (multiple of kTileK)
+    int slice_len;  // candidates per blockIdx.y slice (multiple of the tile)
+    int nmax;       // max(n, m): the partial arrays' row stride
     int split;      // 1 if gridDim.y > 1
     const double *gate = nullptr;  // f4 early stop (pcr_internal.h)
 };
@@ -56,7 +60,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // Each lane owns 2*QP queries held as QP float2 pairs; every candidate is
 // broadcast into both halves so one v_pk_add / v_pk_mul serves two queries:
 // 4 packed arithmetic instructions + compare/select per pair-evaluation.
-template <int QP>
+template <int QP, int kTileK>
 __global__ __launch_bounds__(kThreads) void nnd_fwd_kernel(NndArgs a) {
     if (pcr::gated_off(a.gate)) return;
     constexpr int Q = 2 * QP;
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(kThreads) void nnd_fwd_kernel(NndArgs a) {
 
     float *dist = (dir ? a.dist2 : a.dist1) + (size_t)bat * nq;
     int32_t *idx = (dir ? a.idx2 : a.idx1) + (size_t)bat * nq;
-    unsigned long long *keys = (dir ? a.keys2 : a.keys1);
+    const size_t poff = (((size_t)blockIdx.y * 2 + dir) * a.b + bat) * a.nmax;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const int qi = qtile0 + q * kThreads + tid;
@@ -149,9 +153,8 @@ __global__ __launch_bounds__(kThreads) void nnd_fwd_kernel(NndArgs a) {
             dist[qi] = bb;
             idx[qi] = ii;
         } else {
-            const unsigned long long key =
-                ((unsigned long long)__float_as_uint(bq) << 32) | (unsigned)bi[q];
-            atomicMin(keys + (size_t)bat * nq + qi, key);
+            a.pd[poff + qi] = bq;
+            a.pj[poff + qi] = bi[q];
         }
     }
 }
@@ -166,9 +169,15 @@ __global__ __launch_bounds__(kThreads) void nnd_finalize_kernel(NndArgs a) {
     if (qi >= nq) return;
     const float *qp = (dir ? a.xyz2 : a.xyz1) + ((size_t)bat * nq + qi) * 3;
     const float *c0 = (dir ? a.xyz1 : a.xyz2) + (size_t)bat * nc * 3;
-    const unsigned long long key = (dir ? a.keys2 : a.keys1)[(size_t)bat * nq + qi];
-    float d = __uint_as_float((unsigned)(key >> 32));
-    int i = (int)(unsigned)(key & 0xffffffffu);
+    // slices in order: strict < keeps the earlier slice (lower index) on ties
+    const int used = (nc + a.slice_len - 1) / a.slice_len;
+    float d = __builtin_inff();
+    int i = 0;
+    for (int sl = 0; sl < used; ++sl) {
+        const size_t o = (((size_t)sl * 2 + dir) * a.b + bat) * a.nmax + qi;
+        const float v = a.pd[o];
+        if (sl == 0 || v < d) { d = v; i = a.pj[o]; }
+    }
     const float d0 = sqdist(qp[0], qp[1], qp[2], c0[0], c0[1], c0[2]);
     if (d0 != d0) { d = d0; i = 0; }
     (dir ? a.dist2 : a.dist1)[(size_t)bat * nq + qi] = d;
@@ -353,34 +362,43 @@ extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, 
     {
         const char *e = getenv("PCR_NND_ALGO");
         const bool force_brute = e && e[0] == 'b', force_grid = e && e[0] == 'g';
-        if (force_grid || (!force_brute && n >= 1024 && m >= 1024))
+        // the grid's builds cost tens of microseconds of launches; below ~2^27
+        // pair evaluations the brute force finishes first (C2: 2 x 4096^2)
+        const bool big = (long long)b * n * m > (1LL << 27);
+        if (force_grid || (!force_brute && n >= 1024 && m >= 1024 && big))
             return pcr::nnd_forward_grid(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, s);
     }
-    constexpr int QP = 4;  // 8 queries per lane as 4 packed pairs
-    constexpr int Q = 2 * QP;
     const int nmax = n > m ? n : m;
+    // 8 queries per lane (4 packed pairs) and 512-candidate tiles, or -- when that
+    // cannot give the launch ~4 workgroups per CU (C2: one pair) -- 2 queries
+    // per lane and 128-candidate tiles
+    const bool small = (long long)cdiv(nmax, kThreads * 8) * 2 * b * cdiv(nmax, kTileBig) < 4LL * pcr::kCUs;
+    const int Q = small ? 2 : 8, tile = small ? kTileSmall : kTileBig;
     const int qtiles = cdiv(nmax, kThreads * Q);
     const long long base_blocks = (long long)qtiles * 2 * b;
     // split the candidate axis until the launch has >= ~4 blocks per CU
     int slices = 1;
-    while (base_blocks * slices < 4LL * pcr::kCUs && (long long)kTileK * slices * 2 <= nmax)
+    while (base_blocks * slices < 4LL * pcr::kCUs && (long long)tile * slices * (small ? 1 : 2) < nmax)
         slices *= 2;
     NndArgs a{xyz1, xyz2, dist1, dist2, idx1, idx2, nullptr, nullptr, b, n, m, 0, slices > 1};
-    a.slice_len = cdiv(cdiv(nmax, slices), kTileK) * kTileK;
+    a.slice_len = cdiv(cdiv(nmax, slices), tile) * tile;
+    a.nmax = nmax;
     a.gate = pcr::current_gate();
     const int ys = cdiv(nmax, a.slice_len);
+    a.split = ys > 1;
     PCR_REQUIRE(2LL * b <= 65535, PCR_ERR_ARG, "nnd_forward: b=%d too large (max 32767)", b);
     if (a.split) {
-        auto *keys = (unsigned long long *)pcr::workspace(0, sizeof(unsigned long long) *
-                                                                 ((size_t)b * n + (size_t)b * m));
-        PCR_REQUIRE(keys, PCR_ERR_NOMEM, "nnd_forward: %s", pcr_last_error());
-        a.keys1 = keys;
-        a.keys2 = keys + (size_t)b * n;
-        PCR_HIP_CHECK(hipMemsetAsync(keys, 0xff,
-                                     sizeof(unsigned long long) * ((size_t)b * n + (size_t)b * m), s));
+        const size_t cells = (size_t)ys * 2 * b * nmax;
+        char *ws = (char *)pcr::workspace(0, cells * (sizeof(float) + sizeof(int32_t)));
+        PCR_REQUIRE(ws, PCR_ERR_NOMEM, "nnd_forward: %s", pcr_last_error());
+        a.pd = (float *)ws;
+        a.pj = (int32_t *)(ws + cells * sizeof(float));
     }
     pcr::prof_begin(s, pcr::kProfNndFwd);
-    hipLaunchKernelGGL(nnd_fwd_kernel<QP>, dim3(qtiles, ys, 2 * b), dim3(kThreads), 0, s, a);
+    if (small)
+        hipLaunchKernelGGL((nnd_fwd_kernel<1, kTileSmall>), dim3(qtiles, ys, 2 * b), dim3(kThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((nnd_fwd_kernel<4, kTileBig>), dim3(qtiles, ys, 2 * b), dim3(kThreads), 0, s, a);
     PCR_LAUNCH_CHECK();
     pcr::prof_end(s, pcr::kProfNndFwd);
     if (a.split) {

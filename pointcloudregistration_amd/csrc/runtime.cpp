@@ -28,8 +28,16 @@ struct Slot {
 };
 constexpr int kMaxDevices = 64;
 constexpr int kMaxSlots = 40;
+constexpr int kMaxCtx = 4;  // workspace contexts (pcr_set_workspace_context)
 std::mutex g_mu;
-Slot g_slots[kMaxDevices][kMaxSlots];
+Slot g_slots[kMaxDevices][kMaxCtx][kMaxSlots];
+// the calling thread's workspace context: calls that may run concurrently on
+// different streams (sub-batches of one step) use different contexts, so no
+// scratch buffer is shared between them
+thread_local int t_ctx = 0;
+// launches sharing the device (pcr_set_concurrency): cooperative grids are sized
+// to CUs / g_conc so concurrent ones can all be resident at once
+int g_conc = 1;
 // superseded buffers: kept until pcr_workspace_release (a graph captured before a
 // slot grew still points at its old buffer)
 std::vector<std::pair<int, void *>> g_retired;
@@ -44,7 +52,7 @@ void *workspace(int slot, size_t bytes) {
     }
     if (bytes == 0) bytes = 16;
     std::lock_guard<std::mutex> lk(g_mu);
-    Slot &s = g_slots[dev][slot];
+    Slot &s = g_slots[dev][t_ctx][slot];
     if (s.bytes >= bytes) return s.ptr;
     size_t want = bytes + bytes / 4;  // grow with headroom
     want = (want + 4095) & ~size_t(4095);
@@ -72,7 +80,7 @@ int coop_groups(int P, int per_cu, int gmax) {
         (void)hipGetLastError();
         return 1;
     }
-    const long cap = (long)per_cu * cus;
+    const long cap = (long)per_cu * cus / (g_conc > 1 ? g_conc : 1);
     if ((long)P * 2 > cap) return 1;
     const long g = cap / P;
     return (int)(g > gmax ? gmax : g);
@@ -133,6 +141,22 @@ const double *current_gate() { return t_gate; }
 
 }  // namespace pcr
 
+extern "C" int pcr_set_workspace_context(int32_t ctx) {
+    pcr::clear_error();
+    PCR_REQUIRE(ctx >= 0 && ctx < pcr::kMaxCtx, PCR_ERR_ARG, "workspace context %d (0..%d)", ctx,
+                pcr::kMaxCtx - 1);
+    pcr::t_ctx = ctx;
+    return PCR_OK;
+}
+
+extern "C" int pcr_set_concurrency(int32_t k) {
+    pcr::clear_error();
+    PCR_REQUIRE(k >= 1 && k <= pcr::kMaxCtx, PCR_ERR_ARG, "concurrency %d (1..%d)", k, pcr::kMaxCtx);
+    std::lock_guard<std::mutex> lk(pcr::g_mu);
+    pcr::g_conc = k;
+    return PCR_OK;
+}
+
 extern "C" int pcr_set_gate(const double *gate) {
     pcr::t_gate = gate;
     return PCR_OK;
@@ -176,11 +200,12 @@ extern "C" int pcr_workspace_release(void) {
         return PCR_ERR_HIP;
     }
     std::lock_guard<std::mutex> lk(pcr::g_mu);
-    for (auto &s : pcr::g_slots[dev]) {
-        if (s.ptr) (void)hipFree(s.ptr);
-        s.ptr = nullptr;
-        s.bytes = 0;
-    }
+    for (auto &ctx : pcr::g_slots[dev])
+        for (auto &s : ctx) {
+            if (s.ptr) (void)hipFree(s.ptr);
+            s.ptr = nullptr;
+            s.bytes = 0;
+        }
     std::vector<std::pair<int, void *>> keep;
     for (auto &r : pcr::g_retired) {
         if (r.first == dev) (void)hipFree(r.second);
@@ -218,7 +243,8 @@ extern "C" int pcr_shutdown(void) {
         std::lock_guard<std::mutex> lk(pcr::g_mu);
         for (int dev = 0; dev < pcr::kMaxDevices; ++dev) {
             bool any = false;
-            for (auto &sl : pcr::g_slots[dev]) any = any || sl.ptr;
+            for (auto &ctx : pcr::g_slots[dev])
+                for (auto &sl : ctx) any = any || sl.ptr;
             for (auto &r : pcr::g_retired) any = any || r.first == dev;
             if (!any) continue;
             if (hipSetDevice(dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
@@ -227,11 +253,12 @@ extern "C" int pcr_shutdown(void) {
                 rc = PCR_ERR_HIP;
                 continue;
             }
-            for (auto &sl : pcr::g_slots[dev]) {
-                if (sl.ptr) (void)hipFree(sl.ptr);
-                sl.ptr = nullptr;
-                sl.bytes = 0;
-            }
+            for (auto &ctx : pcr::g_slots[dev])
+                for (auto &sl : ctx) {
+                    if (sl.ptr) (void)hipFree(sl.ptr);
+                    sl.ptr = nullptr;
+                    sl.bytes = 0;
+                }
         }
         std::vector<std::pair<int, void *>> keep;
         for (auto &r : pcr::g_retired) {

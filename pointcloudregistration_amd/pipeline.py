@@ -60,8 +60,11 @@ class PairPipeline:
     takes ``records(copy=True)`` (or ``.clone()``s what it keeps)."""
 
     def __init__(self, src, tgt, src_feat, tgt_feat, params: PipelineParams, pair_ids=None,
-                 device=None):
+                 device=None, context=0):
         dev = device or torch.device("cuda", torch.cuda.current_device())
+        # libpcr workspace context (pcr_set_workspace_context): pipelines whose
+        # steps run concurrently on different streams need different ones
+        self.context = int(context)
 
         def d(x, dt):
             return torch.as_tensor(x).to(dev, dt).contiguous()
@@ -113,11 +116,17 @@ class PairPipeline:
         return rr, ir, chamfer
 
     def run(self, time_stages=False):
+        if self.context and time_stages:
+            raise ValueError("time_stages runs the stage calls in workspace context 0")
         if not time_stages:
             # the whole step in one host call, no round trip (csrc/pipeline.cpp)
             with torch.cuda.device(self.device):
-                _lib.call("pcr_pipeline_step", ctypes.byref(self.io), ctypes.byref(self.c_ransac),
-                          ctypes.byref(self.c_icp), _lib.stream_handle(self.device))
+                _lib.call("pcr_set_workspace_context", self.context)
+                try:
+                    _lib.call("pcr_pipeline_step", ctypes.byref(self.io), ctypes.byref(self.c_ransac),
+                              ctypes.byref(self.c_icp), _lib.stream_handle(self.device))
+                finally:
+                    _lib.call("pcr_set_workspace_context", 0)
             rr = reg.BatchResult(self.T_r, self.fr_r[:, 0], self.fr_r[:, 1], self.st_r, None, self.mask)
             ir = reg.BatchResult(self.T_i, self.fr_i[:, 0], self.fr_i[:, 1], self.st_i, None)
             return self._publish(rr, ir, self.b_ncor, self.b_corres, self.b_nn12)
