@@ -163,6 +163,7 @@ static double det_sum(const double *v, const unsigned char *mask, int n)
 
 /* ------------------------------------------------------------------------- */
 /* Largest-eigenvector of a symmetric 4x4 (cyclic Jacobi, + - * / sqrt only).  */
+/* Mirrored bit for bit by horn_rotation (csrc/geom.h).                       */
 /* ------------------------------------------------------------------------- */
 static void jacobi4_max(double A[4][4], double q[4])
 {
@@ -171,7 +172,11 @@ static void jacobi4_max(double A[4][4], double q[4])
         double off = 0.0;
         for (int p = 0; p < 3; p++)
             for (int r = p + 1; r < 4; r++) off = off + A[p][r] * A[p][r];
-        if (off == 0.0) break;
+        /* converged: off-diagonal mass below 2^-120 of the diagonal's (a further
+         * sweep moves the eigenvector by ~1e-18 relative at most) */
+        double dsq = 0.0;
+        for (int k = 0; k < 4; k++) dsq = dsq + A[k][k] * A[k][k];
+        if (off == 0.0 || off <= 0x1p-120 * dsq) break;
         for (int p = 0; p < 3; p++) {
             for (int r = p + 1; r < 4; r++) {
                 const double apr = A[p][r];

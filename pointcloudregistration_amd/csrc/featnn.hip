@@ -902,6 +902,9 @@ struct RowArgs5 {
 // candidate set holding it).  A minimum replaced by a value with the same bits
 // keeps its older group: then the row's top-2 holds two equal values, so it
 // is uncertified and rescanned exactly.
+#ifndef PCR_ROW_TILECODE
+#define PCR_ROW_TILECODE 1  // 0: the group code (measured slower)
+#endif
 template <int S, int G, bool kIdx, int RT>
 __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     constexpr int W = 8;              // waves per workgroup, RT 32-row tiles each
@@ -972,12 +975,14 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     // read stale values).  min(a, b) is written med3(a, b, -FLT_MAX): the min
     // builtin would add a NaN canonicalisation per operand.  A NaN value makes
     // the row's top-2 NaN (uncertified: the exact rescan decides it).
-    auto epilogue = [&](const f32x16 (&acc)[RT], unsigned) {
+    auto epilogue = [&](const f32x16 (&acc)[RT], unsigned ct) {
+        asm("" : "+s"(ct));
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float vr = acc[t][r];
+                float vr = acc[t][r];
+                if constexpr (kIdx && PCR_ROW_TILECODE) vr = __uint_as_float((__float_as_uint(vr) & keep_r) | ct);
                 b2[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], b2[t][r], vr);
                 b1[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], vr, -3.40282347e+38f);
             }
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                 s1[t][r] = __uint_as_float(nv);
             }
     };
-    constexpr int kV = 32 * RT / NX + 1;  // VALU per MFMA slot below
+    constexpr int kV = ((kIdx && PCR_ROW_TILECODE) ? 48 : 32) * RT / NX + 1;  // VALU per MFMA slot below
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1039,7 +1044,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             __builtin_amdgcn_sched_barrier(0);
         }
         epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1));
-        if constexpr (kIdx) group_code((unsigned)grp);
+        if constexpr (kIdx && !PCR_ROW_TILECODE) group_code((unsigned)grp);
         // the next group's DMA has landed for every wave, and every wave is done
         // reading this buffer before the group after next overwrites it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1069,44 +1074,82 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 if (lr == r) { mb1 = b1[t][r]; mb2 = b2[t][r]; mi1 = i1[r]; }
-            const int row = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
-            if (lr >= 16 || row >= nr) continue;
+            const int rin = (lr & 3) + 8 * (lr >> 2) + 4 * h;  // this lane's row of the tile
+            const int row = qt * 32 + rin;
+            const bool own = lr < 16 && row < nr;
             const size_t o = (size_t)p * a.Rmax + row;
-            if (m == 0) {
+            int want = -1;  // certified rows: (group, column lane) of the winner
+            if (own && m == 0) {
                 a.nn[o] = 0;
                 a.v[o] = __builtin_inf();
                 a.e[o] = 0.0f;
-                continue;
-            }
-            const double Gm = (double)__uint_as_float(a.cmax[p]);
-            const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
-            const double bnd = bound5(qn, Gm, 16 * NX, a.D);
-            const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
-            a.v[o] = (double)mb1;
-            a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-            if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)))) {
-                a.nn[o] = 0;  // the exact rescan writes it
-                a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
-                continue;
-            }
-            // certified: the exact argmin among the G columns of the winning
-            // group in the winning lane, f64 distances in the oracle's order
-            const int gw = mi1 >> 5, col = mi1 & 31, D = a.D;
-            const float *fr = a.Fr + ((size_t)p * a.Rmax + row) * D;
-            double best = __builtin_inf();
-            int bj = gw * G * 32 + col;
-            for (int u = 0; u < G; ++u) {
-                const int j = (gw * G + u) * 32 + col;
-                if (j >= m) break;
-                const float *gc = a.Gc + ((size_t)p * a.Cmax + j) * D;
-                double acc = 0.0;
-                for (int k = 0; k < D; ++k) {
-                    const double df = (double)fr[k] - (double)gc[k];
-                    acc = acc + df * df;
+            } else if (own) {
+                const double Gm = (double)__uint_as_float(a.cmax[p]);
+                const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+                const double bnd = bound5(qn, Gm, 16 * NX, a.D);
+                const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
+                a.v[o] = (double)mb1;
+                a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
+                if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)))) {
+                    a.nn[o] = 0;  // the exact rescan writes it
+                    a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
+                } else {
+                    want = mi1;
                 }
-                if (acc < best) { best = acc; bj = j; }
             }
-            a.nn[o] = bj;
+#if PCR_ROW_TILECODE
+            if (own && want >= 0) a.nn[o] = want;
+            continue;
+#endif
+            // certified rows: the exact argmin among the G columns of the winning
+            // group in the winning lane (f64, the oracle's k order), all 64
+            // lanes at once -- lane l takes tile row l & 31 and half (l >> 5) of
+            // its G candidates, the two halves merge (lower distance, then lower
+            // index), and the row's owner lane picks the result up
+            const int R = l & 31;
+            const int w = __shfl(want, (R & 3) + 4 * (R >> 3) + 32 * ((R >> 2) & 1), 64);
+            double best = __builtin_inf();
+            int bj = 0x7fffffff;
+            if (w >= 0) {
+                const int gw = w >> 5, col = w & 31, D = a.D;
+                const float *fr = a.Fr + ((size_t)p * a.Rmax + qt * 32 + R) * D;
+                const bool v4 = (D & 3) == 0 && ((uintptr_t)a.Fr & 15) == 0 && ((uintptr_t)a.Gc & 15) == 0;
+                constexpr int kH = G / 2;
+                for (int u = (l >> 5) * kH; u < ((l >> 5) + 1) * kH; ++u) {
+                    const int j = (gw * G + u) * 32 + col;
+                    if (j >= m) break;
+                    const float *gc = a.Gc + ((size_t)p * a.Cmax + j) * D;
+                    double acc = 0.0;
+                    if (v4) {
+                        const float4 *f4 = reinterpret_cast<const float4 *>(fr);
+                        const float4 *g4 = reinterpret_cast<const float4 *>(gc);
+                        for (int k = 0; k < (D >> 2); ++k) {
+                            const float4 x = f4[k], y = g4[k];
+                            double df = (double)x.x - (double)y.x;
+                            acc = acc + df * df;
+                            df = (double)x.y - (double)y.y;
+                            acc = acc + df * df;
+                            df = (double)x.z - (double)y.z;
+                            acc = acc + df * df;
+                            df = (double)x.w - (double)y.w;
+                            acc = acc + df * df;
+                        }
+                    } else {
+                        for (int k = 0; k < D; ++k) {
+                            const double df = (double)fr[k] - (double)gc[k];
+                            acc = acc + df * df;
+                        }
+                    }
+                    if (acc < best) { best = acc; bj = j; }
+                }
+            }
+            {
+                const double ob = __shfl_xor(best, 32, 64);
+                const int oj = __shfl_xor(bj, 32, 64);
+                if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+            }
+            const int res = __shfl(bj, rin, 64);
+            if (own && want >= 0) a.nn[o] = res;
         } else {
 #pragma unroll
             for (int o = 1; o < 32; o <<= 1) {
@@ -1464,7 +1507,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
     r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * row_tiles(v.S)); r.D = D; r.ctbits = 1;
     // pass 1 codes the LDS group of column tiles (featnn_row7's G), not the tile
-    while ((1 << r.ctbits) < cdiv(ntm, row_group(v.S))) ++r.ctbits;
+    while ((1 << r.ctbits) < (PCR_ROW_TILECODE ? ntm : cdiv(ntm, row_group(v.S)))) ++r.ctbits;
     r.Fr = F; r.Gc = G;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;

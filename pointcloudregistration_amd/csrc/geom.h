@@ -105,7 +105,13 @@ __device__ inline void horn_rotation(const double S[9], double R[9]) {
         for (int p = 0; p < 3; ++p)
 #pragma unroll
             for (int r = p + 1; r < 4; ++r) off = off + A[p][r] * A[p][r];
-        if (off == 0.0) break;
+        // converged: off-diagonal mass below 2^-120 of the diagonal's (another
+        // sweep moves the eigenvector by ~1e-18 relative; ~4 sweeps instead of
+        // the ~6 an exact-zero test takes)
+        double dsq = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dsq = dsq + A[k][k] * A[k][k];
+        if (off == 0.0 || off <= 0x1p-120 * dsq) break;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll

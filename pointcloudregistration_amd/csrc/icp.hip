@@ -19,8 +19,9 @@
 //    then exact, so any split over threads, waves and workgroups gives the same
 //    bits; the means and the cross-covariance (C = Sst - ms' St^T) come out of
 //    the sweep and one reduction, with no correspondence array written or
-//    re-read.  Horn's quaternion solve and the T <- U*T update run redundantly
-//    in every workgroup on the same totals.
+//    re-read (the sums are kept in quanta and scaled by 2^-k once).  Horn's
+//    quaternion solve and the T <- U*T update run redundantly in every
+//    workgroup on the same totals.
 #include "pcr_internal.h"
 #include "coop.h"
 #include "geom.h"
@@ -298,18 +299,22 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                     if (q >= 0) {
                         ++cnt;
                         acc += (unsigned long long)(d2 * scale);
-                        // the exact Umeyama terms of this correspondence
+                        // the exact Umeyama terms of this correspondence, in quanta:
+                        // trunc(s'_a 2^k), trunc(t'_b 2^k), trunc(s'_a t'_b 2^k) -- the
+                        // scaling by 2^k is exact, so (s'_a 2^k) t'_b rounds to the
+                        // same value as (s'_a t'_b) 2^k; the sums (integers below
+                        // 2^52) are scaled back by 2^-k after the reduction
                         const volatile double *skv = &sh.sk;
-                        const double sk = skv[0], isk = skv[1];
-                        const double sp[3] = {x - c0x, y - c0y, z - c0z};
+                        const double sk = skv[0];
+                        const double sps[3] = {(x - c0x) * sk, (y - c0y) * sk, (z - c0z) * sk};
                         const double tp[3] = {(double)qx - c0x, (double)qy - c0y, (double)qz - c0z};
 #pragma unroll
                         for (int cc = 0; cc < 3; ++cc) {
-                            v[cc] = v[cc] + __builtin_trunc(sp[cc] * sk) * isk;
-                            v[3 + cc] = v[3 + cc] + __builtin_trunc(tp[cc] * sk) * isk;
+                            v[cc] = v[cc] + __builtin_trunc(sps[cc]);
+                            v[3 + cc] = v[3 + cc] + __builtin_trunc(tp[cc] * sk);
 #pragma unroll
                             for (int e = 0; e < 3; ++e)
-                                v[6 + 3 * cc + e] = v[6 + 3 * cc + e] + __builtin_trunc((sp[cc] * tp[e]) * sk) * isk;
+                                v[6 + 3 * cc + e] = v[6 + 3 * cc + e] + __builtin_trunc(sps[cc] * tp[e]);
                         }
                     }
                 }
@@ -333,14 +338,15 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             rmse = __builtin_sqrt(((double)sh.acc / scale) / (double)count);
             const double inv = 1.0 / (double)count;
             if (tid == 0) {
-                double msp[3];
+                double tot[kQ], msp[3];
+                for (int q = 0; q < kQ; ++q) tot[q] = sh.tot[q] * sh.isk;  // quanta -> values (exact)
                 for (int c = 0; c < 3; ++c) {
-                    msp[c] = sh.tot[c] * inv;
+                    msp[c] = tot[c] * inv;
                     sh.ms[c] = msp[c] + sh.c0[c];
-                    sh.mt[c] = sh.tot[3 + c] * inv + sh.c0[c];
+                    sh.mt[c] = tot[3 + c] * inv + sh.c0[c];
                 }
                 for (int c = 0; c < 3; ++c)
-                    for (int e = 0; e < 3; ++e) sh.C[3 * c + e] = sh.tot[6 + 3 * c + e] - msp[c] * sh.tot[3 + e];
+                    for (int e = 0; e < 3; ++e) sh.C[3 * c + e] = tot[6 + 3 * c + e] - msp[c] * tot[3 + e];
             }
         } else {
             fit = 0.0;
