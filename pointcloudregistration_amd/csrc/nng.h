@@ -51,8 +51,16 @@ struct View {
 // margin) away, and its computed f32 distance at least g^2 (1 - 8 * 2^-24)
 // (five relative f32 roundings); strictly above the best: final.  Returns
 // whether the answer was certified.
-template <int LPQ>
-__device__ __forceinline__ bool ring_walk(const View &v, float qx, float qy, float qz, int sub, int kmax,
+//
+// Inside a ring a cell (a column of cells) is skipped when its box is provably
+// farther than the lane's best: a lower bound G on the squared distance from q
+// to the box, from q's margin-shrunk distances to its own cell's faces plus
+// whole cells, in f32 (relative error below 16 * 2^-24); a skipped cell's
+// points have computed distances >= G (1 - 8 * 2^-24) >= 0.99999 G > best, so
+// they could neither win nor tie.  A lane's best only falls, and the merged
+// best is at most the lane's: the skips are exact for every LPQ.
+template <int LPQ, typename V>
+__device__ __forceinline__ bool ring_walk(const V &v, float qx, float qy, float qz, int sub, int kmax,
                                           float &best, int &bj) {
     auto merge = [&]() {
 #pragma unroll
@@ -65,18 +73,34 @@ __device__ __forceinline__ bool ring_walk(const View &v, float qx, float qy, flo
     const double cell = (double)v.cell, ic = 1.0 / cell;
     const int cx = ccoord(qx, ic), cy = ccoord(qy, ic), cz = ccoord(qz, ic);
     const double margin = 1e-6 * (fabs((double)qx) + fabs((double)qy) + fabs((double)qz) + cell);
-    // up to three cells (x, y, z0 + t dz), t < n: every slot bound is loaded
-    // first, then each cell's points four at a time, so a lane waits on one
-    // round trip per batch instead of one per cell and one per point (the walk
-    // is bound by the latency of these dependent loads; take() is order-free)
-    auto scan_cells = [&](int x, int y, int z0, int dz, int n) {
+    // q's distances to the low / high faces of its own cell, less the margin
+    const float lx = (float)fmax((double)qx - (double)cx * cell - margin, 0.0);
+    const float hx = (float)fmax((double)(cx + 1) * cell - (double)qx - margin, 0.0);
+    const float ly = (float)fmax((double)qy - (double)cy * cell - margin, 0.0);
+    const float hy = (float)fmax((double)(cy + 1) * cell - (double)qy - margin, 0.0);
+    const float lz = (float)fmax((double)qz - (double)cz * cell - margin, 0.0);
+    const float hz = (float)fmax((double)(cz + 1) * cell - (double)qz - margin, 0.0);
+    const float cf = v.cell;
+    // squared gap along one axis to the cell at offset d (lower bound)
+    auto gap2 = [&](int d, float lo, float hi) -> float {
+        const float g = d == 0 ? 0.f : (d > 0 ? hi : lo) + (float)((d > 0 ? d : -d) - 1) * cf;
+        return g * g;
+    };
+    constexpr float kLb = 0.99999f;
+    // up to three cells (x, y, z0 + t dz), t < n, each unless its box is beyond
+    // the best: every slot bound is loaded first, then each cell's points four
+    // at a time, so a lane waits on one round trip per batch instead of one per
+    // cell and one per point (the walk is bound by the latency of these
+    // dependent loads; take() is order-free)
+    auto scan_cells = [&](int x, int y, int z0, int dz, int n, float gxy) {
         int s0[3], s1[3];
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             s0[t] = 0;
             s1[t] = 0;
-            if (t < n) {
-                const unsigned h = nhash(x, y, z0 + t * dz, v.S);
+            const int z = z0 + t * dz;
+            if (t < n && (gxy + gap2(z - cz, lz, hz)) * kLb <= best) {
+                const unsigned h = nhash(x, y, z, v.S);
                 s0[t] = v.start[h];
                 s1[t] = v.start[h + 1];
             }
@@ -99,10 +123,12 @@ __device__ __forceinline__ bool ring_walk(const View &v, float qx, float qy, flo
         const int side = 2 * k + 1;
         for (int c = sub; c < side * side; c += LPQ) {
             const int cq = c / side, dx = cq - k, dy = c - cq * side - k;
+            const float gxy = gap2(dx, lx, hx) + gap2(dy, ly, hy);
+            if (gxy * kLb > best) continue;  // the whole column lies beyond the best
             if (dx == -k || dx == k || dy == -k || dy == k) {
-                for (int z = cz - k; z <= cz + k; z += 3) scan_cells(cx + dx, cy + dy, z, 1, min(3, cz + k - z + 1));
+                for (int z = cz - k; z <= cz + k; z += 3) scan_cells(cx + dx, cy + dy, z, 1, min(3, cz + k - z + 1), gxy);
             } else {
-                scan_cells(cx + dx, cy + dy, cz - k, 2 * k, 2);
+                scan_cells(cx + dx, cy + dy, cz - k, 2 * k, 2, gxy);
             }
         }
         merge();
