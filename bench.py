@@ -181,6 +181,27 @@ def _events_ms(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
+def _graph_ms(fn, reps):
+    """Device time per call: `reps` calls captured in one HIP graph and replayed
+    (no host dispatch between the launches -- what a caller that captures or
+    batches its calls pays); the eager per-call time is _events_ms."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(4):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / (4 * reps)
+
+
 def measure_lrf(with_cpu):
     """a4 on the C3 shape (dip/demo.py: 2 clouds, 2048 sampled points each,
     kernel 3*sqrt(3), patch 256): synthetic surface clouds of 20k points scaled
@@ -635,9 +656,10 @@ def measure_c2(with_cpu):
     try:
         for algo in ("grid", "brute"):
             os.environ["PCR_NND_ALGO"] = algo
-            ms = _events_ms(lambda: nd.nnd_forward_cuda(t1, t2, d1, d2, i1, i2), 50)
+            call = lambda: nd.nnd_forward_cuda(t1, t2, d1, d2, i1, i2)  # noqa: E731
+            res[f"eager_ms_{algo}"] = _events_ms(call, 50)  # incl. the Python wrapper's dispatch
+            res[f"gpu_ms_{algo}"] = _graph_ms(call, 50)
             outs[algo] = [x.cpu().numpy() for x in (d1, d2, i1, i2)]
-            res[f"gpu_ms_{algo}"] = ms
     finally:
         if old is None:
             os.environ.pop("PCR_NND_ALGO", None)
@@ -650,7 +672,9 @@ def measure_c2(with_cpu):
     res["roofline_brute"] = {"bound": "valu-f32", "achieved": tf, "peak": PEAK_F32_MFMA_TFLOPS,
                              "unit": "TFLOP/s", "frac": tf / PEAK_F32_MFMA_TFLOPS,
                              "note": "one launch of 1 pair: 32 KB of inputs, far from filling "
-                                     "256 CUs; 8 flops/pair-eval, no FMA contraction"}
+                                     "256 CUs; 8 flops/pair-eval, no FMA contraction; gpu_ms = "
+                                     "device time per call from a graph of 50 calls, eager_ms = "
+                                     "one Python call at a time"}
     res["grid_equals_brute"] = all(np.array_equal(a, b) for a, b in zip(outs["grid"], outs["brute"]))
     if with_cpu:
         ref = None

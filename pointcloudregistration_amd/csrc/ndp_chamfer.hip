@@ -40,6 +40,9 @@
 // Non-finite or out-of-range points (no integer cell coordinates) switch the
 // iteration to the reference loop (seed with candidate 0, strict <) as
 // nnd_grid.hip does.
+#ifndef PCR_NC_SKIP
+#define PCR_NC_SKIP false  // ring_walk's per-cell bounds (nng.h): off for the level Chamfer
+#endif
 #include "pcr_internal.h"
 #include "nng.h"
 #include "scan.h"
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
     }
     const nng::View v = dir ? nng::View{a.hdr->cell_s, a.cs.S, a.cs.start, a.cs.pts}
                             : nng::View{a.hdr->cell_t, a.ct.S, a.ct.start, a.ct.pts};
-    const bool done = nng::ring_walk<LPQ>(v, qx, qy, qz, sub, a.kmax, best, bj);
+    const bool done = nng::ring_walk<LPQ, PCR_NC_SKIP>(v, qx, qy, qz, sub, a.kmax, best, bj);
     // listed queries appended with one atomic per wave (thousands of far
     // queries on one counter serialised at the L2); a wave holds one direction
     const bool list = !done && sub == 0;

@@ -58,8 +58,10 @@ struct View {
 // whole cells, in f32 (relative error below 16 * 2^-24); a skipped cell's
 // points have computed distances >= G (1 - 8 * 2^-24) >= 0.99999 G > best, so
 // they could neither win nor tie.  A lane's best only falls, and the merged
-// best is at most the lane's: the skips are exact for every LPQ.
-template <int LPQ, typename V>
+// best is at most the lane's: the skips are exact for every LPQ.  kSkip = false
+// walks every cell of a ring (the NDP level Chamfer: ring cap 1, four lanes per
+// query -- the bounds cost more there than the cells they save).
+template <int LPQ, bool kSkip = true, typename V>
 __device__ __forceinline__ bool ring_walk(const V &v, float qx, float qy, float qz, int sub, int kmax,
                                           float &best, int &bj) {
     auto merge = [&]() {
@@ -99,7 +101,7 @@ __device__ __forceinline__ bool ring_walk(const V &v, float qx, float qy, float 
             s0[t] = 0;
             s1[t] = 0;
             const int z = z0 + t * dz;
-            if (t < n && (gxy + gap2(z - cz, lz, hz)) * kLb <= best) {
+            if (t < n && (!kSkip || (gxy + gap2(z - cz, lz, hz)) * kLb <= best)) {
                 const unsigned h = nhash(x, y, z, v.S);
                 s0[t] = v.start[h];
                 s1[t] = v.start[h + 1];
@@ -124,7 +126,7 @@ __device__ __forceinline__ bool ring_walk(const V &v, float qx, float qy, float 
         for (int c = sub; c < side * side; c += LPQ) {
             const int cq = c / side, dx = cq - k, dy = c - cq * side - k;
             const float gxy = gap2(dx, lx, hx) + gap2(dy, ly, hy);
-            if (gxy * kLb > best) continue;  // the whole column lies beyond the best
+            if (kSkip && gxy * kLb > best) continue;  // the whole column lies beyond the best
             if (dx == -k || dx == k || dy == -k || dy == k) {
                 for (int z = cz - k; z <= cz + k; z += 3) scan_cells(cx + dx, cy + dy, z, 1, min(3, cz + k - z + 1), gxy);
             } else {
