@@ -446,9 +446,11 @@ __device__ inline GridP4 grid_lds4_view(const GridBatch &gb, char *lds) {
 }
 
 // host: spatial (Morton-of-cell) order of each cloud's points, (P, Nmax) i32 in a
-// workspace slot; identity order for clouds too large for the LDS sort
+// workspace slot; with perm, also the points themselves in that order, (P, Nmax, 3)
+// f32 in slot perm_slot (a sweep in spatial order then reads its 64-point chunk
+// as one contiguous run instead of 64 scattered points)
 int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double cell, hipStream_t s,
-                  int ws_slot, const int32_t **order);
+                  int ws_slot, const int32_t **order, const float **perm = nullptr, int perm_slot = -1);
 
 // host: allocate (workspace slot) + build; returns PCR_OK or error
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r,

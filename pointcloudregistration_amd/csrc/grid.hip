@@ -100,7 +100,7 @@ __device__ __forceinline__ unsigned spread10(unsigned v) {
 constexpr int kOrdBits = 5, kOrdBuckets = 1 << (3 * kOrdBits);
 
 __global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, const int32_t *n, int Nmax,
-                                                             double inv_cell, int32_t *order) {
+                                                             double inv_cell, int32_t *order, float *perm) {
     extern __shared__ int bk[];  // kOrdBuckets + 1: counts -> starts -> cursors
     __shared__ int smin[3][16], smax[3][16];
     constexpr int kReg = 8;      // points per thread whose cell coordinates stay in registers
@@ -108,6 +108,11 @@ __global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, c
     const int m = count_of(n, p, Nmax);
     const float *P = pts + (size_t)p * Nmax * 3;
     int32_t *o = order + (size_t)p * Nmax;
+    float *pm = perm ? perm + (size_t)p * Nmax * 3 : nullptr;
+    auto put = [&](int pos, int i) {
+        o[pos] = i;
+        if (pm) { pm[3 * pos] = P[3 * i]; pm[3 * pos + 1] = P[3 * i + 1]; pm[3 * pos + 2] = P[3 * i + 2]; }
+    };
     auto cellq = [&](int i, int c) { return (int)__builtin_floor((double)P[3 * i + c] * inv_cell); };
     int qr[kReg][3];
     int mn[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff}, mx[3] = {-0x7fffffff, -0x7fffffff, -0x7fffffff};
@@ -168,24 +173,30 @@ __global__ __launch_bounds__(1024) void spatial_order_kernel(const float *pts, c
 #pragma unroll
     for (int u = 0; u < kReg; ++u) {
         const int i = t + 1024 * u;
-        if (i < m) o[atomicAdd(&bk[kr[u]], 1)] = i;
+        if (i < m) put(atomicAdd(&bk[kr[u]], 1), i);
     }
-    for (int i = t + 1024 * kReg; i < m; i += 1024) o[atomicAdd(&bk[key(i)], 1)] = i;
+    for (int i = t + 1024 * kReg; i < m; i += 1024) put(atomicAdd(&bk[key(i)], 1), i);
     for (int i = m + t; i < Nmax; i += 1024) o[i] = i;
 }
 
 }  // namespace
 
 int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double cell, hipStream_t s,
-                  int ws_slot, const int32_t **order) {
+                  int ws_slot, const int32_t **order, const float **perm, int perm_slot) {
     int32_t *o = (int32_t *)workspace(ws_slot, sizeof(int32_t) * (size_t)P * Nmax + 64);
     PCR_REQUIRE(o, PCR_ERR_NOMEM, "spatial_order: %s", pcr_last_error());
+    float *pm = nullptr;
+    if (perm) {
+        pm = (float *)workspace(perm_slot, sizeof(float) * 3 * (size_t)P * Nmax + 64);
+        PCR_REQUIRE(pm, PCR_ERR_NOMEM, "spatial_order: %s", pcr_last_error());
+    }
     const size_t sm = sizeof(int) * (size_t)(kOrdBuckets + 1);
     PCR_HIP_CHECK(hipFuncSetAttribute((const void *)spatial_order_kernel,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    hipLaunchKernelGGL(spatial_order_kernel, dim3(P), dim3(1024), sm, s, pts, n, Nmax, 1.0 / cell, o);
+    hipLaunchKernelGGL(spatial_order_kernel, dim3(P), dim3(1024), sm, s, pts, n, Nmax, 1.0 / cell, o, pm);
     PCR_LAUNCH_CHECK();
     *order = o;
+    if (perm) *perm = pm;
     return PCR_OK;
 }
 

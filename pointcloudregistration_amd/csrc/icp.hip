@@ -8,8 +8,10 @@
 // has fewer pairs than the chip has CUs.  Each workgroup holds the pair's target
 // hash grid in LDS.
 //  * The f64 working copy (transformed in place every iteration, as Open3D's
-//    Transform does) is stored by source index; the sweep takes 64-query chunks
-//    of the spatial (Morton-of-cell) order from a counter.
+//    Transform does) is stored by POSITION in the spatial (Morton-of-cell)
+//    order, and the sweep takes 64-query chunks of that order from a counter:
+//    a chunk's loads and stores are one contiguous 1.5 KB run (stored by source
+//    index, every lane touched a line of its own through the order).
 //  * Per iteration ONE sweep: every point is transformed by the last update,
 //    queried in the grid (radius-limited 1-NN), and -- if it has a
 //    correspondence -- its Umeyama terms are added to the thread's sums right
@@ -52,7 +54,8 @@ struct IArgs {
     double d, thr, rel_fit, rel_rmse;
     int max_iter;
     GridBatch grid;
-    double *P3;          // P x Nmax x 3 working copy by source index
+    double *P3;          // P x Nmax x 3 working copy by position in the order
+    const float *srcp;   // (P, Nmax, 3) the source points in that order, or null
     double *T_out, *fit_out;
     int32_t *stats;
     int32_t *corr_tgt;   // optional (P, Nmax): final correspondence per source point
@@ -207,14 +210,16 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     if (valid) {  // working copy = init applied to the f32 input (Open3D's Transform)
         double T0[12];
         for (int q = 0; q < 12; ++q) T0[q] = sh.T[q];
-        for (int i = base; i < n; i += stride) {
-            double x = (double)S[3 * i], y = (double)S[3 * i + 1], z = (double)S[3 * i + 2];
+        const float *Sp = (a.srcp && ord) ? a.srcp + (size_t)p * a.Nmax * 3 : nullptr;
+        for (int k = base; k < n; k += stride) {
+            const float *q = Sp ? Sp + 3 * k : S + 3 * (ord ? ord[k] : k);
+            double x = (double)q[0], y = (double)q[1], z = (double)q[2];
             if (!ident) {
                 double ox, oy, oz;
                 xform12(T0, x, y, z, ox, oy, oz);
                 x = ox; y = oy; z = oz;
             }
-            P3[3 * i] = x; P3[3 * i + 1] = y; P3[3 * i + 2] = z;
+            P3[3 * k] = x; P3[3 * k + 1] = y; P3[3 * k + 2] = z;
         }
         if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);  // (G = 1: the barrier below)
     }
@@ -273,8 +278,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                 if (c >= nch) break;
                 const int k = (c << 6) + lane;
                 if (k < n) {
-                    const int i = ord ? ord[k] : k;
-                    double x = P3[3 * i], y = P3[3 * i + 1], z = P3[3 * i + 2];
+                    double x = P3[3 * k], y = P3[3 * k + 1], z = P3[3 * k + 2];
                     if (with_u) {  // U from LDS per chunk (volatile: not held across the query)
                         const volatile double *Uv = sh.U;
                         double U[12];
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                         double ox, oy, oz;
                         xform12(U, x, y, z, ox, oy, oz);
                         x = ox; y = oy; z = oz;
-                        P3[3 * i] = x; P3[3 * i + 1] = y; P3[3 * i + 2] = z;
+                        P3[3 * k] = x; P3[3 * k + 1] = y; P3[3 * k + 2] = z;
                     }
                     double d2;
                     int q, s;
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                         q = grid_query<GridView, true>(gg, a.d, a.thr, x, y, z, d2, &s);
                         if (q >= 0) { float w; gg.load(s, qx, qy, qz, w); }
                     }
-                    if (CT) CT[i] = q;
+                    if (CT) CT[ord ? ord[k] : k] = q;
                     if (q >= 0) {
                         ++cnt;
                         acc += (unsigned long long)(d2 * scale);
@@ -413,7 +417,8 @@ const void *icp_fn(bool lds) {
 
 int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, const int32_t *n_src,
              const int32_t *n_tgt, const double *init, const pcr_icp_params *prm, double *T_out,
-             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s, const int32_t *order_in) {
+             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s, const int32_t *order_in,
+             const GridBatch *grid_in, const float *perm_in) {
     IArgs a;
     a.src = src; a.tgt = tgt; a.n_src = n_src; a.n_tgt = n_tgt; a.Nmax = Nmax; a.Mmax = Mmax;
     a.init = init;
@@ -424,16 +429,20 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     a.rel_rmse = prm->relative_rmse;
     a.max_iter = prm->max_iteration;
     a.P3 = nullptr;
+    a.srcp = nullptr;
     if (a.d > 0.0) {
-        int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
+        int rc = PCR_OK;
+        if (grid_in) a.grid = *grid_in;  // built by the caller (pcr_pipeline_step's side stream)
+        else rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 7, a.grid);
         if (rc != PCR_OK) return rc;
         if (Nmax > 0) {
             // any spatial order serves (it only groups a wave's queries): the
             // pipeline hands over RANSAC's, sorted by its coarser cells
             if (order_in) {
                 a.order = order_in;
+                a.srcp = perm_in;
             } else {
-                rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 14, &a.order);
+                rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 14, &a.order, &a.srcp, 35);
                 if (rc != PCR_OK) return rc;
             }
         }
@@ -516,5 +525,5 @@ extern "C" int pcr_icp_batch(const float *src_xyz, const float *tgt_xyz, int32_t
     PCR_REQUIRE(src_xyz && tgt_xyz && init && params && T && fitness_rmse && stats, PCR_ERR_ARG,
                 "icp: null pointer");
     return pcr::icp_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, init, params, T,
-                         fitness_rmse, stats, corr_tgt, pcr::as_stream(stream), nullptr);
+                         fitness_rmse, stats, corr_tgt, pcr::as_stream(stream), nullptr, nullptr, nullptr);
 }

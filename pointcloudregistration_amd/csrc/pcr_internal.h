@@ -19,6 +19,11 @@ void *workspace(int slot, size_t bytes);
 
 inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// A second stream of the calling thread's (device, workspace context) and two
+// events for fork / join with the caller's stream; created once, destroyed by
+// pcr_shutdown.
+int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out);
+
 // per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)
 enum ProfId { kProfFeatScreen = 0, kProfNndFwd = 1, kProfRansacValidate = 2, kProfIcp = 3,
               kProfRansacHyp = 4, kProfFeatRescan = 5, kProfFeatPack = 6, kProfNndGrid = 7,

@@ -4,6 +4,10 @@
 // calls cost ~0.3 ms of host time per step, which a 32-pair shard (2.3 ms of
 // kernels) could not hide.
 #include "pcr_internal.h"
+#include "grid.h"
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 namespace pcr {
 int feature_match_impl(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
@@ -19,10 +23,12 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
                 const int32_t *n_src, const int32_t *n_tgt, const int32_t *corres,
                 const int32_t *n_corres, int Kmax, const uint32_t *pair_ids,
                 const pcr_ransac_params *prm, double *T_out, double *fit_out, int32_t *stats,
-                int32_t *corr_tgt, uint32_t *mask, hipStream_t s, const int32_t **order_out);
+                int32_t *corr_tgt, uint32_t *mask, hipStream_t s, const int32_t **order_out,
+                const GridBatch *grid_in, const int32_t *order_in, const float *perm_in);
 int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, const int32_t *n_src,
              const int32_t *n_tgt, const double *init, const pcr_icp_params *prm, double *T_out,
-             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s, const int32_t *order_in);
+             double *fit_out, int32_t *stats, int32_t *corr_tgt, hipStream_t s, const int32_t *order_in,
+             const GridBatch *grid_in, const float *perm_in);
 int pipeline_records(const pcr_pipeline_io *io, hipStream_t s);
 }  // namespace pcr
 
@@ -60,7 +66,8 @@ extern "C" int pcr_register_feature_ransac(const float *src_xyz, const float *tg
     }
     if (rc != PCR_OK) return rc;
     return pcr::ransac_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, corres, n_corres, Nmax,
-                            pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask, s, nullptr);
+                            pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask, s, nullptr,
+                            nullptr, nullptr, nullptr);
 }
 
 static int io_check(const pcr_pipeline_io *io) {
@@ -85,22 +92,64 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     if (io->P == 0) return PCR_OK;
     hipStream_t s = pcr::as_stream(stream);
     const int P = io->P, N = io->N, M = io->M;
+    // debug (PCR_HOST_TIMING): host time of each stage's calls, to stderr
+    const bool ht = getenv("PCR_HOST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_prev = now();
+    auto lap = [&](const char *what) {
+        if (!ht) return;
+        const auto t = now();
+        fprintf(stderr, "pipeline host %-10s %8.1f us\n", what,
+                std::chrono::duration<double, std::micro>(t - t_prev).count());
+        t_prev = t;
+    };
+    // RANSAC's and ICP's target grids and RANSAC's spatial order of the sources
+    // depend on the clouds alone: they are built on a side stream while the
+    // feature stage runs (one workgroup per pair each -- a small shard left
+    // most of the chip idle for them), joined before RANSAC
+    hipStream_t side = nullptr;
+    hipEvent_t ev_in = nullptr, ev_prep = nullptr;
+    rc = pcr::side_stream(&side, &ev_in, &ev_prep);
+    if (rc != PCR_OK) return rc;
+    PCR_HIP_CHECK(hipEventRecord(ev_in, s));
+    PCR_HIP_CHECK(hipStreamWaitEvent(side, ev_in, 0));
+    pcr::GridBatch grid_r{}, grid_i{};
+    const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP
+    const float *perm = nullptr;     // the sources in that order
+    const bool gr = rp->max_correspondence_distance > 0.0, gi = ip->max_correspondence_distance > 0.0;
+    if (gr) {
+        rc = pcr::build_grids(io->tgt_xyz, nullptr, P, M, rp->max_correspondence_distance, side, 4, grid_r);
+        if (rc != PCR_OK) return rc;
+        rc = pcr::spatial_order(io->src_xyz, nullptr, P, N, grid_r.cell, side, 13, &order, &perm, 36);
+        if (rc != PCR_OK) return rc;
+    }
+    if (gi) {
+        rc = pcr::build_grids(io->tgt_xyz, nullptr, P, M, ip->max_correspondence_distance, side, 7, grid_i);
+        if (rc != PCR_OK) return rc;
+    }
+    PCR_HIP_CHECK(hipEventRecord(ev_prep, side));
+    lap("prep");
     rc = pcr::feature_corres_impl(io->src_feat, io->tgt_feat, P, N, M, io->D, nullptr, nullptr,
                                   rp->mutual_filter, rp->ransac_n, io->nn12, io->corres, io->n_corres, s);
     if (rc != PCR_OK) return rc;
-    const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP
+    lap("features");
+    PCR_HIP_CHECK(hipStreamWaitEvent(s, ev_prep, 0));
     rc = pcr::ransac_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->corres, io->n_corres, N,
                           io->pair_ids, rp, io->T_ransac, io->fit_ransac, io->stats_ransac, nullptr,
-                          io->inlier_mask, s, &order);
+                          io->inlier_mask, s, nullptr, gr ? &grid_r : nullptr, order, perm);
     if (rc != PCR_OK) return rc;
+    lap("ransac");
     rc = pcr::icp_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->T_ransac, ip, io->T_icp,
-                       io->fit_icp, io->stats_icp, nullptr, s, order);
+                       io->fit_icp, io->stats_icp, nullptr, s, order, gi ? &grid_i : nullptr, perm);
     if (rc != PCR_OK) return rc;
+    lap("icp");
     rc = pcr_transform_batch(io->src_xyz, P, N, io->T_icp, io->aligned, stream);
     if (rc != PCR_OK) return rc;
     rc = pcr_nnd_forward(io->aligned, io->tgt_xyz, P, N, M, io->d1, io->d2, io->i1, io->i2, stream);
     if (rc != PCR_OK) return rc;
-    return pcr::pipeline_records(io, s);
+    rc = pcr::pipeline_records(io, s);
+    lap("chamfer");
+    return rc;
 }
 
 extern "C" int pcr_pipeline_records(const pcr_pipeline_io *io, pcr_stream_t stream) {

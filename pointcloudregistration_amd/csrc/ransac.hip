@@ -108,6 +108,7 @@ struct RArgs {
     uint32_t *mask;
     int words;
     const int32_t *order;   // (P, Nmax) spatial order of the source points, or null
+    const float *srcp;      // (P, Nmax, 3) the source points in that order, or null
     RState *state;          // (P)
     double *hypT;           // (P, hcap, 12) passing transforms of the round
     unsigned long long *hypbits;  // (P, hcap / 64) pass bits of the round
@@ -291,6 +292,7 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
     const float *Gt = a.tgt + (size_t)p * a.Mmax * 3;
     const int32_t *co = a.corres + (size_t)p * a.Kmax * 2;
     const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
+    const float *Sp = (a.srcp && ord) ? a.srcp + (size_t)p * a.Nmax * 3 : nullptr;
     const double scale = fx_scale(a.thr);
     const int nch = min((n + 63) >> 6, c_hi);
     unsigned long long acc = 0;
@@ -304,12 +306,19 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
         const int k = (c << 6) + lane;
         int j = 0;
         if (k < n) {
-            const int i = ord ? ord[k] : k;
+            // the chunk's points: a contiguous run of the ordered copy, or gathered
+            float sx, sy, sz;
+            if (Sp) {
+                sx = Sp[3 * k]; sy = Sp[3 * k + 1]; sz = Sp[3 * k + 2];
+            } else {
+                const int i = ord ? ord[k] : k;
+                sx = S[3 * i]; sy = S[3 * i + 1]; sz = S[3 * i + 2];
+            }
             double px, py, pz, d2;
-            xform12(Te, (double)S[3 * i], (double)S[3 * i + 1], (double)S[3 * i + 2], px, py, pz);
+            xform12(Te, (double)sx, (double)sy, (double)sz, px, py, pz);
             j = grid_query<Grid, false, PCR_RANSAC_KW>(gr, a.d, a.thr, px, py, pz, d2);
             if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
-            if (cbuf) cbuf[by_order ? k : i] = j;
+            if (cbuf) cbuf[by_order ? k : (ord ? ord[k] : k)] = j;
         }
         const int miss = __popcll(__ballot(k < n && j < 0));
         int tot = 0;
@@ -690,7 +699,8 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
                 const int32_t *n_src, const int32_t *n_tgt, const int32_t *corres,
                 const int32_t *n_corres, int Kmax, const uint32_t *pair_ids,
                 const pcr_ransac_params *prm, double *T_out, double *fit_out, int32_t *stats,
-                int32_t *corr_tgt, uint32_t *mask, hipStream_t s, const int32_t **order_out) {
+                int32_t *corr_tgt, uint32_t *mask, hipStream_t s, const int32_t **order_out,
+                const GridBatch *grid_in, const int32_t *order_in, const float *perm_in) {
     if (order_out) *order_out = nullptr;
     PCR_REQUIRE(prm->ransac_n >= 3 && prm->ransac_n <= kMaxRansacN, PCR_ERR_ARG,
                 "ransac: ransac_n=%d unsupported (3..%d)", prm->ransac_n, kMaxRansacN);
@@ -710,6 +720,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.T_out = T_out; a.fit_out = fit_out; a.stats = stats; a.corr_tgt = corr_tgt; a.mask = mask;
     a.words = (Nmax + 31) / 32;
     a.order = nullptr;
+    a.srcp = nullptr;
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
     // Rounds.  Device-gated (default): [0, kRound0) and, when max_iteration is
     // larger, ONE more round [kRound0, max_iteration) launched right behind it,
@@ -742,13 +753,19 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     a.grid.S = 1;
     a.grid.cell = 1.0;
     if (a.d > 0.0 && Mmax > 0) {
-        int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 4, a.grid);
-        if (rc != PCR_OK) return rc;
-        if (Nmax > 0) {
-            rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 13, &a.order);
+        if (grid_in) {  // built by the caller (pcr_pipeline_step: on its side stream)
+            a.grid = *grid_in;
+            a.order = Nmax > 0 ? order_in : nullptr;
+            a.srcp = Nmax > 0 ? perm_in : nullptr;
+        } else {
+            int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 4, a.grid);
             if (rc != PCR_OK) return rc;
-            if (order_out) *order_out = a.order;
+            if (Nmax > 0) {
+                rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 13, &a.order, &a.srcp, 36);
+                if (rc != PCR_OK) return rc;
+            }
         }
+        if (order_out) *order_out = a.order;
     }
     const size_t hdr = (sizeof(Shared) + 15) & ~size_t(15);
     const size_t budget = 160 * 1024 - hdr;
@@ -905,5 +922,5 @@ extern "C" int pcr_ransac_batch(const float *src_xyz, const float *tgt_xyz, int3
     PCR_REQUIRE(P <= 65535, PCR_ERR_ARG, "ransac: P=%d > 65535 pairs per call", P);
     return pcr::ransac_impl(src_xyz, tgt_xyz, P, Nmax, Mmax, n_src, n_tgt, corres, n_corres, Kmax,
                             pair_ids, params, T, fitness_rmse, stats, corr_tgt, inlier_mask,
-                            pcr::as_stream(stream), nullptr);
+                            pcr::as_stream(stream), nullptr, nullptr, nullptr, nullptr);
 }

@@ -68,6 +68,39 @@ void *workspace(int slot, size_t bytes) {
     return p;
 }
 
+// ---- side stream of a (device, workspace context) -------------------------
+namespace {
+struct Side {
+    hipStream_t s = nullptr;
+    hipEvent_t e[2] = {nullptr, nullptr};
+};
+Side g_side[kMaxDevices][kMaxCtx];
+}  // namespace
+
+int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        (void)hipGetLastError();
+        set_error("side_stream: no current device");
+        return PCR_ERR_HIP;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    Side &d = g_side[dev][t_ctx];
+    if (!d.s) {
+        if (hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&d.e[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d.e[1], hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("side_stream: stream / event creation failed");
+            return PCR_ERR_HIP;
+        }
+    }
+    *s = d.s;
+    *e_in = d.e[0];
+    *e_out = d.e[1];
+    return PCR_OK;
+}
+
 // ---- several workgroups per pair (coop.h) ---------------------------------
 int coop_groups(int P, int per_cu, int gmax) {
     if (const char *e = getenv("PCR_COOP_G")) {  // tests: force a split
@@ -218,8 +251,8 @@ extern "C" int pcr_workspace_release(void) {
 // Process-end teardown (round 4): a profiled run (rocprofv3 --kernel-trace) of
 // round 3 crashed inside exit() after its last output, in a library finaliser;
 // the library's process-lifetime device objects -- workspace slots, retired
-// buffers, pooled profiling events -- were never released and outlived the
-// runtime's own teardown.  pcr_shutdown() releases all of them while the runtime
+// buffers, pooled profiling events, side streams -- were never released and
+// outlived the runtime's own teardown.  pcr_shutdown() releases all of them while the runtime
 // is intact (Python's atexit runs it first; bench.py also calls it).  Idempotent;
 // the library re-allocates on its next call.
 extern "C" int pcr_shutdown(void) {
@@ -260,6 +293,17 @@ extern "C" int pcr_shutdown(void) {
                     sl.bytes = 0;
                 }
         }
+        for (int dev = 0; dev < pcr::kMaxDevices; ++dev)
+            for (auto &sd : pcr::g_side[dev]) {
+                if (!sd.s) continue;
+                if (hipSetDevice(dev) == hipSuccess) {
+                    (void)hipStreamSynchronize(sd.s);
+                    (void)hipStreamDestroy(sd.s);
+                    (void)hipEventDestroy(sd.e[0]);
+                    (void)hipEventDestroy(sd.e[1]);
+                }
+                sd = pcr::Side{};
+            }
         std::vector<std::pair<int, void *>> keep;
         for (auto &r : pcr::g_retired) {
             if (hipSetDevice(r.first) == hipSuccess) (void)hipFree(r.second);
