@@ -108,9 +108,13 @@ inline Split5 split5_params(int D) {
 // gridDim.z 1024-thread blocks per (pair, cloud), each a contiguous slice of
 // float4 loads (several in flight per thread), one atomic per block -- with few
 // pairs one block per cloud was a chain of ~64 dependent load round trips
+// Partial maxima, one plain store per block (mxp[(p * 2 + which) * Z + z]): the
+// packs reduce them, so nothing has to be cleared before this launch.  Block
+// (p, 0, 0) also clears the pair's counters that the later launches of the
+// stage accumulate into (the packs' norm maxima, the rescan list counts).
 __global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_t *nf, int Nmax,
                                                     const float *G, const int32_t *ng, int Mmax,
-                                                    int D, unsigned *mx) {
+                                                    int D, unsigned *mxp, unsigned *clr, int P) {
     const int p = blockIdx.x, which = blockIdx.y, t = threadIdx.x, z = blockIdx.z, Z = gridDim.z;
     const float *X = which ? G : F;
     const int cnt = which ? count_of(ng, p, Mmax) : count_of(nf, p, Nmax);
@@ -139,8 +143,25 @@ __global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_
     if (t == 0) {
         float r = wm[0];
         for (int w = 1; w < 16; ++w) r = fmaxf(r, wm[w]);
-        if (r > 0.0f) atomicMax(mx + p, __float_as_uint(r));
+        mxp[((size_t)p * 2 + which) * Z + z] = __float_as_uint(r);  // r >= 0, never NaN
+        if (which == 0 && z == 0) {  // gmax, fmax, (mx: written by the packs), cnt12, cnt21
+            clr[p] = 0u;
+            clr[P + p] = 0u;
+            clr[3 * P + p] = 0u;
+            clr[4 * P + p] = 0u;
+        }
     }
+}
+
+// the pair's max |element| from feat_maxabs' 2 Z partials (bits of non-negative
+// floats: unsigned order = float order), reduced by every wave on its own
+__device__ __forceinline__ unsigned pair_max_bits(const unsigned *mxp, int Z, int p) {
+    const int l = threadIdx.x & 63;
+    unsigned m = 0u;
+    for (int k = l; k < 2 * Z; k += 64) m = max(m, mxp[(size_t)p * 2 * Z + k]);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+    return m;
 }
 
 __device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
@@ -155,14 +176,16 @@ __device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
 // exact) and every lane emits its 2S + 1 stored 16-byte operand fragments.
 __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t *n, int Nmax, int D,
                                                   int S, int ntiles, int role, Split5 sp,
-                                                  const unsigned *mx, f16x8 *Xp, float *nrm,
-                                                  unsigned *nmax) {
+                                                  const unsigned *mxp, int Z, unsigned *mx, f16x8 *Xp,
+                                                  float *nrm, unsigned *nmax) {
     __shared__ float xs[4][32][65];  // D <= 64 (+1 pad: conflict-free row reads)
     const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
     const int cnt = count_of(n, p, Nmax);
     const int nrows = min(max(cnt - t * 32, 0), 32);
-    const float s = pair_scale5(mx[p], sp.T);
+    const unsigned mb = pair_max_bits(mxp, Z, p);
+    if (blockIdx.x == 0 && threadIdx.x == 0) mx[p] = mb;  // for the rescans (later launches)
+    const float s = pair_scale5(mb, sp.T);
     const float *base = X + ((size_t)p * Nmax + (size_t)t * 32) * D;
     float (*x)[65] = xs[w];
     // e / D by a 64-bit reciprocal (exact for e < 2^16; 2^32/D + 1 needs 33 bits at D = 1)
@@ -248,8 +271,8 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
 template <int D>
 __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t *n, int Nmax,
                                                    int ntiles, int role, Split5 sp,
-                                                   const unsigned *mx, f16x8 *Xp, float *nrm,
-                                                   unsigned *nmax) {
+                                                   const unsigned *mxp, int Z, unsigned *mx, f16x8 *Xp,
+                                                   float *nrm, unsigned *nmax) {
     constexpr int S = (D + 15) / 16;  // chunks per segment
     constexpr int NM = 2 * S + 1;     // stored chunks
     constexpr int G = 2 * S;          // 8-half fragments per segment
@@ -257,7 +280,9 @@ __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t
     const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
     const int cnt = count_of(n, p, Nmax);
     const int nrows = min(max(cnt - t * 32, 0), 32);
-    const float s = pair_scale5(mx[p], sp.T);
+    const unsigned mb = pair_max_bits(mxp, Z, p);
+    if (blockIdx.x == 0 && threadIdx.x == 0) mx[p] = mb;  // for the rescans (later launches)
+    const float s = pair_scale5(mb, sp.T);
     const int rr = l & 31, h = l >> 5;
     const bool valid = rr < nrows;
     float x[D];
@@ -1307,7 +1332,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     const size_t ap = (size_t)P * ntn * NM * 64, bp = (size_t)P * ntm * NM * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
-        16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax));
+        16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax) + 128 * (size_t)P);
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     v.Ap = (f16x8 *)ws;
@@ -1322,28 +1347,28 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.cnt21 = v.cnt12 + P;
     v.list12 = v.cnt21 + P;                    // per pair, stride Nmax
     v.list21 = v.list12 + (size_t)P * Nmax;    // per pair, stride Mmax
-    PCR_HIP_CHECK(hipMemsetAsync(v.gmax, 0, sizeof(unsigned) * 5 * P, s));
+    unsigned *mxp = (unsigned *)(v.list21 + (size_t)P * Mmax);  // [P][2][zsl <= 64] partial maxima
     prof_begin(s, kProfFeatPack);
     // ~1024 blocks whatever the batch (each >= 16 KB of a cloud)
     const long long cloud_f4 = ((long long)std::max(Nmax, Mmax) * D + 3) / 4;
     const int zsl = (int)std::max(1LL, std::min(std::min(64LL, (cloud_f4 + 1023) / 1024),
                                                 (long long)cdiv(1024, 2 * P)));
     hipLaunchKernelGGL(feat_maxabs, dim3(P, 2, zsl), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax,
-                       D, v.mx);
+                       D, mxp, v.gmax, P);
     PCR_LAUNCH_CHECK();
     if (D == 32) {  // the hot shape: register-resident pack
         hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax,
-                           ntn, 0, v.sp, v.mx, v.Ap, v.fnr, v.fmax);
+                           ntn, 0, v.sp, mxp, zsl, v.mx, v.Ap, v.fnr, v.fmax);
         PCR_LAUNCH_CHECK();
         hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax,
-                           ntm, 1, v.sp, v.mx, v.Bp, v.gnr, v.gmax);
+                           ntm, 1, v.sp, mxp, zsl, v.mx, v.Bp, v.gnr, v.gmax);
         PCR_LAUNCH_CHECK();
     } else {
         hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D,
-                           v.S, ntn, 0, v.sp, v.mx, v.Ap, v.fnr, v.fmax);
+                           v.S, ntn, 0, v.sp, mxp, zsl, v.mx, v.Ap, v.fnr, v.fmax);
         PCR_LAUNCH_CHECK();
         hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax, D,
-                           v.S, ntm, 1, v.sp, v.mx, v.Bp, v.gnr, v.gmax);
+                           v.S, ntm, 1, v.sp, mxp, zsl, v.mx, v.Bp, v.gnr, v.gmax);
         PCR_LAUNCH_CHECK();
     }
     prof_end(s, kProfFeatPack);
@@ -1482,7 +1507,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P]
     const size_t pn = (size_t)P * Nmax, pm = (size_t)P * Mmax;
     const size_t bytes = 8 * pn + 4 * pn + 8 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P;
-    char *ws = (char *)workspace(33, bytes + 256);
+    bool fresh = false;
+    char *ws = (char *)workspace(33, bytes + 256, &fresh);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
     MutArgs ma;
     double *v12 = (double *)ws;
@@ -1495,7 +1521,15 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     ma.flag = nn21x + pm;
     ma.nj = ma.flag + pn + P;
     int *zero = ma.nj + P;
-    PCR_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(int) * (size_t)P, s));
+    // a constant zero count per pair (read only): cleared when the slot is new
+    // or was last used for fewer pairs
+    static thread_local const void *z_ptr = nullptr;
+    static thread_local int z_cnt = 0;
+    if (fresh || z_ptr != (const void *)zero || z_cnt < P) {
+        PCR_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(int) * (size_t)P, s));
+        z_ptr = zero;
+        z_cnt = P;
+    }
     ma.nn12 = nn12; ma.n_src = n_src; ma.n_tgt = n_tgt; ma.Nmax = Nmax; ma.Mmax = Mmax;
     ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * v.NX; ma.D = D; ma.ntm = ntm;
     ma.v12 = v12; ma.e12 = e12; ma.w1 = w1; ma.w2 = w2; ma.gnr = v.gnr; ma.fmax = v.fmax;

@@ -36,7 +36,7 @@ struct NgArgs {
     int B, S, nmax;
     float cf;             // cell factor (0.6; PCR_NND_CELL overrides, tuning hook)
     float *cell;          // [2][B]
-    int *flag;            // [B]: 1 = use the reference loop
+    int *flag;            // [2][B]: set s of pair b holds a NaN/Inf or is too far out (both: the reference loop)
     int *hcnt;            // [2][B][S]
     int *start;           // [2][B][S+1]
     float4 *pts;          // [2][B][nmax]
@@ -44,6 +44,9 @@ struct NgArgs {
     int32_t *idx[2];
     const double *gate;   // f4 early stop (pcr_internal.h), or null
 };
+
+// the pair's clouds go to the reference loop (either set flagged by nng_bbox)
+__device__ __forceinline__ bool ref_loop(const NgArgs &a, int b) { return (a.flag[b] | a.flag[a.B + b]) != 0; }
 
 using nng::ccoord;
 using nng::d2f;
@@ -97,13 +100,13 @@ __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
     // integer cell coordinates must stay far from int overflow
     if (!(amax / cell < 1e9)) bad = 1;
     a.cell[s * a.B + b] = (float)cell;
-    if (bad) atomicOr(a.flag + b, 1);
+    a.flag[s * a.B + b] = bad ? 1 : 0;  // every launch writes both sets' flags: no clearing
 }
 
 __global__ void nng_count(NgArgs a) {
     if (gated_off(a.gate)) return;
     const int s = blockIdx.z, b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n[s] || a.flag[b]) return;
+    if (i >= a.n[s] || ref_loop(a, b)) return;
     const float *p = a.xyz[s] + ((size_t)b * a.n[s] + i) * 3;
     const double ic = 1.0 / (double)a.cell[s * a.B + b];
     const unsigned h = nhash(ccoord(p[0], ic), ccoord(p[1], ic), ccoord(p[2], ic), a.S);
@@ -113,7 +116,7 @@ __global__ void nng_count(NgArgs a) {
 __global__ __launch_bounds__(1024) void nng_scan(NgArgs a) {
     if (gated_off(a.gate)) return;
     const int s = blockIdx.y, b = blockIdx.x;
-    if (a.flag[b]) return;
+    if (ref_loop(a, b)) return;
     const size_t g = (size_t)s * a.B + b;
     block_exclusive_scan_1024(a.hcnt + g * a.S, a.start + g * (a.S + 1), a.S, true);
 }
@@ -121,7 +124,7 @@ __global__ __launch_bounds__(1024) void nng_scan(NgArgs a) {
 __global__ void nng_scatter(NgArgs a) {
     if (gated_off(a.gate)) return;
     const int s = blockIdx.z, b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n[s] || a.flag[b]) return;
+    if (i >= a.n[s] || ref_loop(a, b)) return;
     const float *p = a.xyz[s] + ((size_t)b * a.n[s] + i) * 3;
     const size_t g = (size_t)s * a.B + b;
     const double ic = 1.0 / (double)a.cell[g];
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(1024) void nng_build(NgArgs a) {
     if (gated_off(a.gate)) return;
     extern __shared__ int cnt[];  // S + 1: counts -> exclusive starts -> cursors
     const int s = blockIdx.x, b = blockIdx.y, S = a.S, n = a.n[s];
-    if (a.flag[b]) return;  // nng_bbox ran before on this stream
+    if (ref_loop(a, b)) return;  // nng_bbox ran before on this stream
     const size_t g = (size_t)s * a.B + b;
     const float *P = a.xyz[s] + (size_t)b * n * 3;
     const double ic = 1.0 / (double)a.cell[g];
@@ -192,7 +195,8 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
     // the reference-loop clouds (flag) have no grid and go in index order
     int qi = qslot;
     float qx, qy, qz;
-    if (a.flag[b]) {
+    const bool refl = ref_loop(a, b);
+    if (refl) {
         const float *q = a.xyz[qs] + ((size_t)b * a.n[qs] + qi) * 3;
         qx = q[0]; qy = q[1]; qz = q[2];
     } else {
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
             if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
         }
     };
-    if (a.flag[b]) {
+    if (refl) {
         // the reference loop: seed with candidate 0, strict < (my_lib.cpp:11-20)
         if (sub == 0) {
             best = d2f(C[0], C[1], C[2], qx, qy, qz);
@@ -259,12 +263,12 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
     while (S < a.nmax) S <<= 1;
     a.S = S;
     const size_t cells = 2 * (size_t)b, hc = cells * S, stc = cells * (S + 1), pc = cells * a.nmax;
-    char *ws = (char *)workspace(15, 4 * (cells + b + hc + stc) + 16 * pc + 256);
+    char *ws = (char *)workspace(15, 4 * (cells + 2 * (size_t)b + hc + stc) + 16 * pc + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "nnd_forward (grid): %s", pcr_last_error());
     a.pts = (float4 *)ws;
     a.cell = (float *)(a.pts + pc);
     a.flag = (int *)(a.cell + cells);
-    a.hcnt = a.flag + b;
+    a.hcnt = a.flag + 2 * (size_t)b;
     a.start = a.hcnt + hc;
     a.dist[0] = dist1; a.dist[1] = dist2; a.idx[0] = idx1; a.idx[1] = idx2;
     a.gate = current_gate();
@@ -274,7 +278,7 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
         if (v >= 0.1f && v <= 4.0f) a.cf = v;
     }
     const bool lds_build = S <= kLdsSlots;
-    PCR_HIP_CHECK(hipMemsetAsync(a.flag, 0, sizeof(int) * (lds_build ? (size_t)b : b + hc), s));
+    if (!lds_build) PCR_HIP_CHECK(hipMemsetAsync(a.hcnt, 0, sizeof(int) * hc, s));
     hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(1024), 0, s, a);
     PCR_LAUNCH_CHECK();
     if (lds_build) {

@@ -14,8 +14,9 @@ void clear_error();
 
 // Per-device scratch owned by the library.  Grows on demand; superseded buffers
 // stay allocated until process exit so kernels still in flight on another
-// stream never see their scratch freed.  Mutex-guarded.
-void *workspace(int slot, size_t bytes);
+// stream never see their scratch freed.  Mutex-guarded.  *fresh (optional) tells
+// whether the buffer was (re)allocated by this call (contents undefined).
+void *workspace(int slot, size_t bytes, bool *fresh = nullptr);
 
 inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -93,6 +93,8 @@ struct RHeader {
     int n_done, n_cut, n_skip, n_chunks;  // diagnostics (PCR_RANSAC_STATS=1 prints them)
 };
 
+static_assert(2 * sizeof(RHeader) / sizeof(int) <= 256, "ransac_hyp_kernel clears the headers with one thread per word");
+
 struct RArgs {
     const float *src, *tgt;
     const int32_t *n_src, *n_tgt;
@@ -125,6 +127,7 @@ struct RArgs {
     TaskPart *parts;        // (P, hcap, split) when split > 1
     const int *prev_active; // later rounds launched without a host decision: the previous
                             // round's active_count (0: every kernel of this round returns)
+    int clear_hdr;          // ransac_hyp_kernel clears hdr[0..2) (the gated rounds' first launch)
 };
 
 __device__ __forceinline__ bool round_off(const RArgs &a) {
@@ -209,6 +212,10 @@ __device__ bool make_hypothesis(const RArgs &a, int p, int K, uint32_t pid, int 
 template <int RN>
 __global__ __launch_bounds__(kHypThreads) void ransac_hyp_kernel(RArgs a) {
     if (round_off(a)) return;
+    // device-gated rounds: the first round's first block clears both rounds'
+    // headers (every later reader is a later launch on the stream)
+    if (a.clear_hdr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * sizeof(RHeader) / sizeof(int))
+        reinterpret_cast<int *>(a.hdr)[threadIdx.x] = 0;
     const int p = blockIdx.y;
     int lim = min(a.b1, a.max_iter);
     if (a.b0 > 0) {   // later rounds: only pairs still running, below their bound
@@ -833,11 +840,15 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
     prof_begin(s, kProfRansacValidate);
     a.b0 = 0;
     a.b1 = std::min(a.max_iter, kRound0);
+    a.clear_hdr = 0;
     if (gated) {
-        PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, 2 * sizeof(RHeader), s));
         RHeader *h0 = a.hdr;
+        const int nx0 = (a.b1 - a.b0 + kHypThreads - 1) / kHypThreads;
+        if (nx0 > 0) a.clear_hdr = 1;  // the first hypothesis launch clears the headers
+        else PCR_HIP_CHECK(hipMemsetAsync(a.hdr, 0, 2 * sizeof(RHeader), s));
         for (int round = 0; round < (a.max_iter > kRound0 ? 2 : 1); ++round) {
             if (round == 1) {
+                a.clear_hdr = 0;
                 a.b0 = kRound0;
                 a.b1 = a.max_iter;
                 a.hdr = h0 + 1;

@@ -43,7 +43,8 @@ int g_conc = 1;
 std::vector<std::pair<int, void *>> g_retired;
 }  // namespace
 
-void *workspace(int slot, size_t bytes) {
+void *workspace(int slot, size_t bytes, bool *fresh) {
+    if (fresh) *fresh = false;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices || slot < 0 ||
         slot >= kMaxSlots) {
@@ -65,6 +66,7 @@ void *workspace(int slot, size_t bytes) {
     if (s.ptr) g_retired.emplace_back(dev, s.ptr);
     s.ptr = p;
     s.bytes = want;
+    if (fresh) *fresh = true;
     return p;
 }
 
