@@ -1,0 +1,25 @@
+# Round 4 evidence for profiles/r04/ (TAG=vN): the -m gpu suite, smoke, the
+# default bench line (all legs), the 32 / 64-pair shards, the kernel stats of the
+# 256-pair bench, PMC traffic and SQ counters, the C5 / f4 kernel stats.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+V=${TAG:-v1}
+T=gpurun_out/r04final_$V
+mkdir -p $T
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $T/pytest_gpu.txt 2>&1
+echo "pytest rc $?"; tail -2 $T/pytest_gpu.txt
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $T/smoke.txt 2>&1 || { tail -20 $T/smoke.txt; exit 12; }
+tail -2 $T/smoke.txt
+timeout -k 10 600 python bench.py > $T/bench.json 2> $T/bench.err || { tail -20 $T/bench.err; exit 13; }
+python3 -c "import json;d=json.loads(open('$T/bench.json').read().strip().splitlines()[-1]);print('value',round(d['value']),'ms',round(d['ms_per_step'],3))"
+for P in 32 64; do
+  timeout -k 10 300 python bench.py --pairs $P --no-secondary --no-cpu-baseline > $T/bench_${P}pairs.json 2> $T/bench_$P.err || { tail -5 $T/bench_$P.err; exit 14; }
+  python3 -c "import json;d=json.loads(open('$T/bench_${P}pairs.json').read().strip().splitlines()[-1]);print($P,'pairs ms',round(d['ms_per_step'],3))"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-secondary --no-cpu-baseline --no-host-resident > $T/prof.log 2>&1
+echo "rocprof stats rc $?"
+bash tools/pmc_traffic.sh $T/traffic > $T/traffic.txt 2>&1; echo "traffic rc $?"
+bash tools/pmc_sq.sh $T/sq > $T/sq.txt 2>&1; echo "sq rc $?"
+TAG=r04final_${V}_f4 bash tools/gpu_f4_prof.sh > $T/f4.txt 2>&1; echo "f4 prof rc $?"
+tail -3 $T/f4.txt
