@@ -244,6 +244,11 @@ int pcr_icp_batch(const float *src_xyz, const float *tgt_xyz, int32_t P, int32_t
  * of the f32 distances in index order), 37 RANSAC iterations, 38 RANSAC
  * status, 39 correspondences after the mutual filter.
  * pcr_pipeline_records: the records alone, from buffers the stage calls filled.
+ * Streams: the step forks once -- RANSAC's / ICP's target grids and the source
+ * spatial order are built on a library-owned side stream of the calling
+ * thread's (device, workspace context) while the feature stage runs on
+ * `stream`, joined by an event before RANSAC -- and everything else, and the
+ * completion, is on `stream` (a graph capture of the step sees the fork/join).
  * ------------------------------------------------------------------------- */
 typedef struct pcr_pipeline_io {
     const float *src_xyz, *tgt_xyz;    /* (P,N,3), (P,M,3) */
