@@ -234,17 +234,8 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
 #pragma unroll
             for (int u = 0; u < kW; ++u) g.load(sl[u], cx[u], cy[u], cz[u], cw[u]);
             double dd[kW];
-#ifdef PCR_GQ_SPEEDPROBE  // timing probe only (NOT exact): the candidate distance in f32
-            const float fx = (float)px, fy = (float)py, fz = (float)pz;
-#pragma unroll
-            for (int u = 0; u < kW; ++u) {
-                const float ex = cx[u] - fx, ey = cy[u] - fy, ez = cz[u] - fz;
-                dd[u] = (double)((ex * ex + ey * ey) + ez * ez);
-            }
-#else
 #pragma unroll
             for (int u = 0; u < kW; ++u) dd[u] = dist2(px, py, pz, (double)cx[u], (double)cy[u], (double)cz[u]);
-#endif
 #pragma unroll
             for (int u = 0; u < kW; ++u) {
                 if (ok[u] && dd[u] < thr) {
