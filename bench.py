@@ -734,7 +734,11 @@ def _pmc_traffic(kernel, *more):
         return None
     for k, v in ks.items():
         if kernel in k and all(m in k for m in more):
-            return v.get("fetch_size_bytes", 0.0) + v.get("write_size_bytes", 0.0)
+            # the largest launch (RANSAC's gated second round is a near-empty
+            # launch of the same kernel; older summaries have the mean only)
+            f = v.get("fetch_size_bytes_max", v.get("fetch_size_bytes", 0.0))
+            w = v.get("write_size_bytes_max", v.get("write_size_bytes", 0.0))
+            return f + w
     return None
 
 
@@ -956,9 +960,12 @@ def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
                                   "target grid; HBM sees the points once per launch"},
            "traffic": _pmc_traffic(kernel), "frac": None}
     if sq and "SQ_INSTS_VALU" in sq:
-        valu = sq["SQ_INSTS_VALU"]
-        f64 = sum(sq.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
-                                             "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        # the largest launch's counts (`*_max`; RANSAC launches its sweep twice a
+        # step, the gated second round nearly empty: the mean would halve the work)
+        cnt = lambda c: sq.get(c + "_max", sq.get(c, 0.0))  # noqa: E731
+        valu = cnt("SQ_INSTS_VALU")
+        f64 = sum(cnt(c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                     "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
         cyc = 2.0 * (valu - f64) + 4.0 * f64
         floor_ms = cyc / 1024 / (CLOCK_GHZ_PEAK * 1e9) * 1e3
         lane_ops = valu * 64 + f64 * 64   # f32-equivalent lane operations (f64 = 2)
@@ -966,7 +973,7 @@ def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
                     "peak": 1024 * 32 * CLOCK_GHZ_PEAK / 1e3, "unit": "T lane-op/s (f32-equivalent VALU)",
                     "frac": floor_ms / per, "model_floor_ms": floor_ms,
                     "valu_insts_per_launch": valu, "valu_f64_insts_per_launch": f64 if f64 else None,
-                    "lds_insts_per_launch": sq.get("SQ_INSTS_LDS"), "sq_source": src})
+                    "lds_insts_per_launch": cnt("SQ_INSTS_LDS"), "sq_source": src})
     return out
 
 

@@ -1,4 +1,5 @@
-"""Per-kernel SQ counters (mean per launch) from rocprofv3 --pmc pass directories.
+"""Per-kernel SQ counters (mean per launch, and `<counter>_max`: the largest
+launch) from rocprofv3 --pmc pass directories.
 Usage: python3 tools/sq_summary.py OUTDIR [kernel-substring ...]"""
 import csv
 import glob
@@ -19,4 +20,5 @@ for k, cs in acc.items():
     if keys and not any(s in k for s in keys):
         continue
     res[k[:70]] = {c: sum(v) / len(v) for c, v in sorted(cs.items())}
+    res[k[:70]].update({c + "_max": max(v) for c, v in sorted(cs.items())})
 print(json.dumps(res, indent=1))
