@@ -8,7 +8,8 @@ V=${TAG:-v1}
 T=gpurun_out/r04final_$V
 mkdir -p $T
 timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $T/pytest_gpu.txt 2>&1
-echo "pytest rc $?"; tail -2 $T/pytest_gpu.txt
+rc=$?; echo "pytest rc $rc"; tail -2 $T/pytest_gpu.txt
+case $rc in 124|134|137|139) exit 11;; esac
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $T/smoke.txt 2>&1 || { tail -20 $T/smoke.txt; exit 12; }
 tail -2 $T/smoke.txt
 timeout -k 10 600 python bench.py > $T/bench.json 2> $T/bench.err || { tail -20 $T/bench.err; exit 13; }
@@ -18,7 +19,8 @@ for P in 32 64; do
   python3 -c "import json;d=json.loads(open('$T/bench_${P}pairs.json').read().strip().splitlines()[-1]);print($P,'pairs ms',round(d['ms_per_step'],3))"
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-secondary --no-cpu-baseline --no-host-resident > $T/prof.log 2>&1
-echo "rocprof stats rc $?"
+rc=$?; echo "rocprof stats rc $rc"
+case $rc in 124|134|137) exit 15;; esac
 bash tools/pmc_traffic.sh $T/traffic > $T/traffic.txt 2>&1; echo "traffic rc $?"
 bash tools/pmc_sq.sh $T/sq > $T/sq.txt 2>&1; echo "sq rc $?"
 TAG=r04final_${V}_f4 bash tools/gpu_f4_prof.sh > $T/f4.txt 2>&1; echo "f4 prof rc $?"
