@@ -40,6 +40,20 @@
 // Non-finite or out-of-range points (no integer cell coordinates) switch the
 // iteration to the reference loop (seed with candidate 0, strict <) as
 // nnd_grid.hip does.
+//
+// Round 4, the default (PCR_NC_BOX=1): the grid path above is replaced by a
+// box path -- each cloud in a spatial order fixed at prepare, 32-point leaves
+// and 1024-point groups with their bounding boxes; per iteration one launch
+// rewrites the subset's points and boxes (nc_leaves) and one answers both
+// directions (nc_bquery), each query's search bounded by the distance to its
+// previous answer (the level loop moves points a little per iteration, and the
+// level's first iteration starts from the previous level's answers).  A box
+// bound is d2f's own roundings on the axis gaps, so it is a true lower bound of
+// every computed distance inside (monotone rounding): a box above the bound
+// cannot hold the answer or a tie, and the result is the exact lexicographic
+// (d, j) minimum -- the same bits as the grid path and pcr_nnd_forward -- from
+// any starting index.  Four launches and the far-query list (count / scan /
+// scatter, walk, fallback, emit) become two.
 #ifndef PCR_NC_SKIP
 #define PCR_NC_SKIP false  // ring_walk's per-cell bounds (nng.h): off for the level Chamfer
 #endif
@@ -73,6 +87,32 @@ struct NcHdr {
     unsigned amax_s;  // the subset's, this iteration (nc_count; nc_scan consumes and clears)
     int shift;        // this iteration's fixed-point exponent s (nc_scan)
     int pad2;
+    long long nfflag; // box path: a non-finite gradient term this iteration (nc_bquery)
+    unsigned done;    // box path: nc_bquery blocks finished (the last one resets)
+    int pad3;
+};
+
+// ---- the box path (default; PCR_NC_BOX=0 selects the grid path above) ------
+// Each cloud in a fixed spatial (Morton) order, cut into leaves of kLeaf
+// consecutive points and groups of kGrp leaves, each with its f32 bounding box.
+// The target's order and boxes are built once (prepare); the subset keeps the
+// order of its level's starting positions and only its points and boxes are
+// rewritten per iteration (nc_leaves: one launch instead of count / scan /
+// scatter).  A box moving with its points stays exact -- it is recomputed from
+// the current coordinates -- only its tightness depends on the order.
+constexpr int kLeaf = 32, kGrp = 32;  // points per leaf, leaves per group (= one 1024-thread block)
+constexpr int kOrdBits5 = 5, kOrdN = 1 << (3 * kOrdBits5);  // 32^3 Morton buckets of the bounding box
+
+struct NcBox {
+    float4 lo, hi;  // .w unused
+};
+
+struct NcTree {
+    int n, L, G;      // points, leaves, groups
+    int *ord;         // position -> original index (prepare)
+    float4 *pts;      // n points in that order: (x, y, z, index bits)
+    NcBox *leaf;      // L
+    NcBox *grp;       // G
 };
 
 // one cloud's hashed grid (nng.h)
@@ -99,6 +139,8 @@ struct NcArgs {
     int *fb;                // K + M: listed queries (dir 0 at 0, dir 1 at K)
     unsigned long long *fbkey;  // K + M: their (d bits, j) minima
     const double *gate;
+    bool box;               // the box path (PCR_NC_BOX, default on)
+    NcTree bt, bs;          // its target / subset trees
 };
 
 __device__ __forceinline__ bool cell_ok(float x, float y, float z, double ic) {
@@ -203,6 +245,20 @@ __global__ void nc_count(const float *P, int n, const float *cellp, NcCloud g, i
 // strided global reads took ~19 us for 16K slots)
 constexpr int kScanLds = 32768;
 
+// the fixed-point exponent of this iteration (header comment): every finite
+// term <= T = 2 gmax (A_s + A_t), an entry sums <= M + 1 of them
+__device__ inline int nc_shift(const NcHdr *h, float gmax, int Mq, int fshift) {
+    const double T = 2.0 * (double)gmax *
+                     ((double)__uint_as_float(h->amax_s) + (double)__uint_as_float(h->amax_t)) *
+                     (1.0 + 0x1p-20);
+    const double B = (double)(Mq + 2) * T;
+    int sh = 60;
+    if (B > 0.0 && __builtin_isfinite(B)) sh = 59 - ilogb(B);  // B < 2^(ilogb+1): B 2^s < 2^60
+    sh = sh < -900 ? -900 : (sh > 900 ? 900 : sh);
+    if (fshift >= 0) sh = 1000 + fshift;  // marks "hi words only" for fix_add
+    return sh;
+}
+
 __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr *h, long long *gacc,
                                                 float gmax, int Mq, int fshift, const double *gate) {
     if (gated_off(gate)) return;
@@ -243,14 +299,7 @@ __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr
         h->fb_cnt[1] = 0;
         // the fixed-point exponent of this iteration (header comment): every
         // finite term <= T = 2 gmax (A_s + A_t), an entry sums <= M + 1 of them
-        const double T = 2.0 * (double)gmax *
-                         ((double)__uint_as_float(h->amax_s) + (double)__uint_as_float(h->amax_t)) *
-                         (1.0 + 0x1p-20);
-        const double B = (double)(Mq + 2) * T;
-        int sh = 60;
-        if (B > 0.0 && __builtin_isfinite(B)) sh = 59 - ilogb(B);  // B < 2^(ilogb+1): B 2^s < 2^60
-        sh = sh < -900 ? -900 : (sh > 900 ? 900 : sh);
-        if (fshift >= 0) sh = 1000 + fshift;  // marks "hi words only" for fix_add
+        const int sh = nc_shift(h, gmax, Mq, fshift);
         h->shift = sh;
         h->amax_s = 0u;
         gacc[0] = (long long)(sh + 2048) << 8;
@@ -292,7 +341,7 @@ __device__ __forceinline__ void fix_add(long long *hi, long long *lo, float v, i
 // The far target points of a partial overlap share a few boundary answers (up to
 // ~350 terms on one subset point in C5): the terms go to replica q mod kRep, so
 // same-address atomics stay short (integer sums: the replica split changes no bit)
-__device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best, int bj, int sh) {
+__device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best, int bj, int sh, long long *flag) {
     long long *rep = a.gacc + 1 + (size_t)(q & (kRep - 1)) * 3 * a.K;
     const size_t lo = (size_t)3 * kRep * a.K;  // lo words after all hi words
     if (dir == 0) {
@@ -301,8 +350,7 @@ __device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best
         const float g = (!(best >= a.trunc) ? a.g1 : 0.0f) * 2;
         if (bj < 0 || bj >= a.M) return;
         for (int c = 0; c < 3; ++c)
-            fix_add(rep + 3 * q + c, rep + lo + 3 * q + c, g * (a.xs[3 * q + c] - a.tgt[3 * bj + c]), sh,
-                    a.gacc);
+            fix_add(rep + 3 * q + c, rep + lo + 3 * q + c, g * (a.xs[3 * q + c] - a.tgt[3 * bj + c]), sh, flag);
     } else {
         a.d2[q] = best;
         a.i2[q] = bj;
@@ -310,7 +358,7 @@ __device__ __forceinline__ void emit(const NcArgs &a, int dir, int q, float best
         if (bj < 0 || bj >= a.K) return;
         for (int c = 0; c < 3; ++c)
             fix_add(rep + 3 * bj + c, rep + lo + 3 * bj + c, -(g * (a.tgt[3 * q + c] - a.xs[3 * bj + c])), sh,
-                    a.gacc);
+                    flag);
     }
 }
 
@@ -350,7 +398,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
             const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
             if (d < best) { best = d; bj = j; }
         }
-        emit(a, dir, qi, best, bj, sh);
+        emit(a, dir, qi, best, bj, sh, a.gacc);
         return;
     }
     const nng::View v = dir ? nng::View{a.hdr->cell_s, a.cs.S, a.cs.start, a.cs.pts}
@@ -371,7 +419,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
             a.fbkey[e] = ~0ULL;
         }
     }
-    if (sub == 0 && done) emit(a, dir, qi, best, bj, sh);
+    if (sub == 0 && done) emit(a, dir, qi, best, bj, sh, a.gacc);
 }
 
 // the listed queries: work item = (64 listed queries of one direction, a
@@ -477,7 +525,251 @@ __global__ __launch_bounds__(256) void nc_fallback_emit(NcArgs a) {
     const int e = dir ? a.K + (w - c0) : w;
     const unsigned long long k = a.fbkey[e];
     emit(a, dir, a.fb[e], __uint_as_float((unsigned)(k >> 32)), (int)(unsigned)(k & 0xffffffffu),
-         a.hdr->shift);
+         a.hdr->shift, a.gacc);
+}
+
+// ---- box path kernels --------------------------------------------------------
+__device__ __forceinline__ unsigned spread5(unsigned v) {  // 5 bits -> every third bit
+    v &= 31u;
+    v = (v | (v << 8)) & 0x0000F00Fu;
+    v = (v | (v << 4)) & 0x000C30C3u;
+    v = (v | (v << 2)) & 0x00249249u;
+    return v;
+}
+
+// prepare: a spatial order of one cloud (one 1024-thread workgroup): Morton
+// code of the point's bucket in a 32^3 division of the finite bounding box,
+// counting sort in LDS (order inside a bucket: atomic order -- it only changes
+// how tight the boxes are, never an answer)
+__global__ __launch_bounds__(1024) void nc_order(const float *P, int n, int *ord) {
+    extern __shared__ int bk[];  // kOrdN + 1
+    __shared__ float sl[3][16], sh[3][16];
+    __shared__ float lo_s[3], sc_s[3];
+    const int t = threadIdx.x;
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    for (int i = t; i < n; i += 1024)
+        for (int c = 0; c < 3; ++c) {
+            const float v = P[3 * i + c];
+            if (__builtin_isfinite(v)) { lo[c] = fminf(lo[c], v); hi[c] = fmaxf(hi[c], v); }
+        }
+    for (int c = 0; c < 3; ++c) {
+        for (int o = 32; o; o >>= 1) {
+            lo[c] = fminf(lo[c], __shfl_xor(lo[c], o, 64));
+            hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o, 64));
+        }
+        if ((t & 63) == 0) { sl[c][t >> 6] = lo[c]; sh[c][t >> 6] = hi[c]; }
+    }
+    for (int i = t; i < kOrdN; i += 1024) bk[i] = 0;
+    __syncthreads();
+    if (t < 3) {
+        float l = sl[t][0], h = sh[t][0];
+        for (int w = 1; w < 16; ++w) { l = fminf(l, sl[t][w]); h = fmaxf(h, sh[t][w]); }
+        const double e = (double)h - (double)l;
+        lo_s[t] = l;
+        sc_s[t] = (e > 0.0 && e < 1e300) ? (float)(32.0 / e) : 0.0f;
+    }
+    __syncthreads();
+    auto key = [&](int i) -> unsigned {
+        unsigned k = 0;
+        for (int c = 0; c < 3; ++c) {
+            const float v = (P[3 * i + c] - lo_s[c]) * sc_s[c];  // NaN / inf -> bucket 0 / 31
+            const int q = v > 0.0f ? (v < 31.0f ? (int)v : 31) : 0;
+            k |= spread5((unsigned)q) << c;
+        }
+        return k;
+    };
+    for (int i = t; i < n; i += 1024) atomicAdd(&bk[key(i)], 1);
+    __syncthreads();
+    block_exclusive_scan_1024(bk, bk, kOrdN, false);
+    for (int i = t; i < n; i += 1024) ord[atomicAdd(&bk[key(i)], 1)] = i;
+}
+
+// one group per 1024-thread block: position k's point (original index ord[k])
+// into pts[k], the boxes of its leaf (half a wave) and of its group; for the
+// subset also the per-iteration duties of nc_count (zero the gradient words,
+// the non-finite flag, the largest finite |coordinate|)
+__global__ __launch_bounds__(1024) void nc_leaves(const float *P, NcTree g, int *flag, long long *gacc,
+                                                  unsigned *amax, const double *gate) {
+    if (gated_off(gate)) return;
+    __shared__ NcBox lb[kGrp];
+    const int t = threadIdx.x, k = blockIdx.x * 1024 + t;
+    if (gacc) {  // the 6 kRep n gradient words after the header, spread over every block
+        const size_t nw = (size_t)6 * kRep * g.n;
+        for (size_t e = (size_t)k; e < nw; e += (size_t)gridDim.x * 1024) gacc[1 + e] = 0;
+    }
+    if ((int)blockIdx.x >= g.G) return;  // zeroing-only blocks
+    const bool v = k < g.n;
+    float x = 0.f, y = 0.f, z = 0.f, am = 0.0f;
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    bool bad = false;
+    if (v) {
+        const int i = g.ord[k];
+        x = P[3 * i]; y = P[3 * i + 1]; z = P[3 * i + 2];
+        g.pts[k] = make_float4(x, y, z, __int_as_float(i));
+        const float q[3] = {x, y, z};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (__builtin_isfinite(q[c])) {
+                am = fmaxf(am, fabsf(q[c]));
+                lo[c] = q[c];
+                hi[c] = q[c];
+            } else {
+                bad = true;
+            }
+        }
+    }
+    if (flag && __ballot(bad) != 0ull && (t & 63) == 0) atomicOr(flag, 1);
+    if (amax) {
+        for (int o = 32; o; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+        if ((t & 63) == 0 && am > 0.0f) atomicMax(amax, __float_as_uint(am));
+    }
+#pragma unroll
+    for (int o = 16; o; o >>= 1)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = fminf(lo[c], __shfl_xor(lo[c], o, 64));
+            hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o, 64));
+        }
+    const int leaf = k >> 5;
+    if ((t & 31) == 0) {
+        const NcBox b{make_float4(lo[0], lo[1], lo[2], 0.f), make_float4(hi[0], hi[1], hi[2], 0.f)};
+        lb[t >> 5] = b;
+        if (leaf < g.L) g.leaf[leaf] = b;
+    }
+    __syncthreads();
+    if (t < 32) {
+        const NcBox b = lb[t];
+        float l[3] = {b.lo.x, b.lo.y, b.lo.z}, h[3] = {b.hi.x, b.hi.y, b.hi.z};
+#pragma unroll
+        for (int o = 16; o; o >>= 1)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                l[c] = fminf(l[c], __shfl_xor(l[c], o, 64));
+                h[c] = fmaxf(h[c], __shfl_xor(h[c], o, 64));
+            }
+        if (t == 0) g.grp[blockIdx.x] = NcBox{make_float4(l[0], l[1], l[2], 0.f), make_float4(h[0], h[1], h[2], 0.f)};
+    }
+}
+
+// lower bound of d2f over a box: the same roundings as d2f on the per-axis gap
+// (rounding is monotone, so every point c of the box has fl(c - q)^2 terms at
+// least these, and its computed distance is >= the bound; exact, no margin)
+__device__ __forceinline__ float box_lb(const NcBox &b, float qx, float qy, float qz) {
+    const float gx = fmaxf(fmaxf(b.lo.x - qx, qx - b.hi.x), 0.0f);
+    const float gy = fmaxf(fmaxf(b.lo.y - qy, qy - b.hi.y), 0.0f);
+    const float gz = fmaxf(fmaxf(b.lo.z - qz, qz - b.hi.z), 0.0f);
+    return (gx * gx + gy * gy) + gz * gz;
+}
+
+// LPQ lanes per query, 64 / LPQ queries per wave, both directions (blocks
+// [0, nb0): the subset against the target, the rest the target against the
+// subset), queries in their cloud's spatial order.  U = the distance to the
+// query's answer of the previous call (i1 / i2: any index in range is a valid
+// start, so the first call of a level is exact too, only slower) bounds the
+// answer: a group, then a leaf, whose box bound exceeds U is skipped (its
+// points cannot win or tie).  The query's lanes split the groups, OR their
+// selections, split each selected group's leaves, and scan their selected
+// leaves' points themselves; the lanes' (d, j) minima are merged
+// lexicographically.  The last block to finish writes the gradient header word
+// and resets the per-iteration fields.
+template <int LPQ>
+__global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
+    if (gated_off(a.gate)) return;
+    constexpr int QPB = 256 / LPQ;
+    __shared__ bool last;
+    const int sub = threadIdx.x % LPQ;
+    const int dir = blockIdx.x < nb0 ? 0 : 1;
+    const int k = (blockIdx.x - (dir ? nb0 : 0)) * QPB + (int)threadIdx.x / LPQ;
+    const int nq = dir ? a.M : a.K, nc = dir ? a.K : a.M;
+    const NcHdr *h = a.hdr;
+    const int sh = nc_shift(h, a.g1 > a.g2 ? a.g1 : a.g2, a.M, a.fshift);
+    const float *C = dir ? a.xs : a.tgt;
+    if (k < nq) {
+        if ((h->sflag | h->tflag) != 0) {
+            // the reference loop: seed with candidate 0, strict < (my_lib.cpp:11-20)
+            if (sub == 0) {
+                const float *Q = dir ? a.tgt : a.xs;
+                const float qx = Q[3 * k], qy = Q[3 * k + 1], qz = Q[3 * k + 2];
+                float best = d2f(C[0], C[1], C[2], qx, qy, qz);
+                int bj = 0;
+                for (int j = 1; j < nc; ++j) {
+                    const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
+                    if (d < best) { best = d; bj = j; }
+                }
+                emit(a, dir, k, best, bj, sh, &a.hdr->nfflag);
+            }
+        } else {
+            const NcTree &Qt = dir ? a.bt : a.bs;
+            const NcTree &Ct = dir ? a.bs : a.bt;
+            const float4 qp = Qt.pts[k];
+            const float qx = qp.x, qy = qp.y, qz = qp.z;
+            const int qi = __float_as_int(qp.w);
+            int jp = dir ? a.i2[qi] : a.i1[qi];
+            jp = (jp >= 0 && jp < nc) ? jp : 0;
+            const float U = d2f(C[3 * jp], C[3 * jp + 1], C[3 * jp + 2], qx, qy, qz);
+            float best = U;
+            int bj = jp;
+            // groups sub, sub + LPQ, ... (G <= 32)
+            unsigned gm = 0;
+#pragma unroll
+            for (int t = 0; t < kGrp / LPQ; ++t) {
+                const int g = sub + LPQ * t;
+                if (g < Ct.G && box_lb(Ct.grp[g], qx, qy, qz) <= U) gm |= 1u << g;
+            }
+#pragma unroll
+            for (int o = 1; o < LPQ; o <<= 1) gm |= __shfl_xor(gm, o, 64);
+            while (gm) {
+                const int g = __ffs(gm) - 1;
+                gm &= gm - 1;
+                // leaves sub, sub + LPQ, ... of group g
+                unsigned lm = 0;
+#pragma unroll
+                for (int t = 0; t < kGrp / LPQ; ++t) {
+                    const int lf = g * kGrp + sub + LPQ * t;
+                    if (lf < Ct.L && box_lb(Ct.leaf[lf], qx, qy, qz) <= U) lm |= 1u << t;
+                }
+                while (lm) {
+                    const int t = __ffs(lm) - 1;
+                    lm &= lm - 1;
+                    const int p0 = (g * kGrp + sub + LPQ * t) * kLeaf;
+                    const int pn = min(kLeaf, Ct.n - p0);
+                    for (int u = 0; u < pn; u += 8) {
+                        float4 p[8];
+#pragma unroll
+                        for (int v = 0; v < 8; ++v)
+                            if (u + v < pn) p[v] = Ct.pts[p0 + u + v];
+#pragma unroll
+                        for (int v = 0; v < 8; ++v)
+                            if (u + v < pn) take(d2f(p[v].x, p[v].y, p[v].z, qx, qy, qz), __float_as_int(p[v].w), best, bj);
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < LPQ; o <<= 1) {
+                const float ob = __shfl_xor(best, o, 64);
+                const int oj = __shfl_xor(bj, o, 64);
+                take(ob, oj, best, bj);
+            }
+            if (sub == 0) emit(a, dir, qi, best, bj, sh, &a.hdr->nfflag);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&a.hdr->done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    __threadfence();
+    NcHdr *hw = a.hdr;
+    const long long nf = __hip_atomic_load(&hw->nfflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.gacc[0] = ((long long)(sh + 2048) << 8) | (nf & 1);
+    hw->nfflag = 0;
+    hw->sflag = 0;
+    hw->amax_s = 0u;
+    hw->done = 0u;
 }
 
 // the scan's dynamic LDS limit, set once outside any stream capture (prepare
@@ -488,10 +780,18 @@ hipError_t nc_scan_attr() {
     return e;
 }
 
+hipError_t nc_order_attr() {
+    static const hipError_t e = hipFuncSetAttribute((const void *)nc_order, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)(sizeof(int) * (kOrdN + 1)));
+    return e;
+}
+
 struct NcLayout {
     size_t hdr, cnt, fb, fbkey, total;
     size_t start[2], pts[2];  // [0] target, [1] subset
     int S[2];
+    size_t ord[2], bpts[2], leaf[2], grp[2];  // the box path's trees
+    int L[2], G[2];
 };
 
 inline int pow2_at_least(int n, int lo) {
@@ -511,6 +811,14 @@ NcLayout nc_layout(int K, int M) {
         L.S[c] = pow2_at_least(n[c], 256);
         L.start[c] = o; o = up256(o + sizeof(int) * ((size_t)L.S[c] + 1));
         L.pts[c] = o; o = up256(o + sizeof(float4) * (size_t)n[c]);
+    }
+    for (int c = 0; c < 2; ++c) {
+        L.L[c] = (n[c] + kLeaf - 1) / kLeaf;
+        L.G[c] = (L.L[c] + kGrp - 1) / kGrp;
+        L.ord[c] = o; o = up256(o + sizeof(int) * (size_t)n[c]);
+        L.bpts[c] = o; o = up256(o + sizeof(float4) * (size_t)n[c]);
+        L.leaf[c] = o; o = up256(o + sizeof(NcBox) * (size_t)L.L[c]);
+        L.grp[c] = o; o = up256(o + sizeof(NcBox) * (size_t)L.G[c]);
     }
     L.cnt = o; o = up256(o + sizeof(int) * (size_t)std::max(L.S[0], L.S[1]));
     L.fb = o; o = up256(o + sizeof(int) * ((size_t)K + M));
@@ -536,6 +844,18 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
         g.start = (int *)(s + L.start[k]);
         g.pts = (float4 *)(s + L.pts[k]);
     }
+    for (int k = 0; k < 2; ++k) {
+        NcTree &t = k ? a.bs : a.bt;
+        t.n = k ? c->K : c->M;
+        t.L = L.L[k];
+        t.G = L.G[k];
+        t.ord = (int *)(s + L.ord[k]);
+        t.pts = (float4 *)(s + L.bpts[k]);
+        t.leaf = (NcBox *)(s + L.leaf[k]);
+        t.grp = (NcBox *)(s + L.grp[k]);
+    }
+    a.box = true;
+    if (const char *e = getenv("PCR_NC_BOX")) a.box = atoi(e) != 0;
     a.kmax = 1;
     if (const char *e = getenv("PCR_NDP_CHAMFER_RINGS")) {  // test / tuning hook: 0..3
         const int v = atoi(e);
@@ -604,6 +924,20 @@ extern "C" int pcr_ndp_chamfer_prepare(const pcr_ndp_chamfer *c, const float *xs
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, a.tgt, a.M, &a.hdr->cell_t, &a.hdr->tflag,
                        &a.hdr->amax_t);
     PCR_LAUNCH_CHECK();
+    if (a.box) {
+        // both clouds' spatial orders (the subset's from its starting positions xs0),
+        // the target's tree once
+        PCR_HIP_CHECK(pcr::nc_order_attr());
+        const size_t lds = sizeof(int) * (pcr::kOrdN + 1);
+        hipLaunchKernelGGL(pcr::nc_order, dim3(1), dim3(1024), lds, s, a.tgt, a.M, a.bt.ord);
+        PCR_LAUNCH_CHECK();
+        hipLaunchKernelGGL(pcr::nc_order, dim3(1), dim3(1024), lds, s, xs0, a.K, a.bs.ord);
+        PCR_LAUNCH_CHECK();
+        hipLaunchKernelGGL(pcr::nc_leaves, dim3(a.bt.G), dim3(1024), 0, s, a.tgt, a.bt, (int *)nullptr,
+                           (long long *)nullptr, (unsigned *)nullptr, (const double *)nullptr);
+        PCR_LAUNCH_CHECK();
+        return PCR_OK;
+    }
     hipLaunchKernelGGL(pcr::nc_bbox, dim3(1), dim3(1024), 0, s, xs0, a.K, &a.hdr->cell_s, (int *)nullptr,
                        (unsigned *)nullptr);
     PCR_LAUNCH_CHECK();
@@ -617,6 +951,30 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
     int rc = pcr::nc_args(c, a);
     if (rc != PCR_OK) return rc;
     hipStream_t s = pcr::as_stream(stream);
+    if (a.box) {
+        // the leaf blocks, and enough more that each thread zeroes <= 16 gradient words
+        const long long zw = 6LL * pcr::kRep * a.K;
+        const int nbz = (int)std::max<long long>(a.bs.G, (zw + 16 * 1024 - 1) / (16 * 1024));
+        hipLaunchKernelGGL(pcr::nc_leaves, dim3(nbz), dim3(1024), 0, s, a.xs, a.bs, &a.hdr->sflag, a.gacc,
+                           &a.hdr->amax_s, a.gate);
+        PCR_LAUNCH_CHECK();
+        int lpq = 4;
+        if (const char *e = getenv("PCR_NC_LPQ")) {
+            const int v = atoi(e);
+            if (v == 2 || v == 4 || v == 8) lpq = v;
+        }
+        const int qpb = 256 / lpq;
+        const int nb0 = (a.K + qpb - 1) / qpb, nb1 = (a.M + qpb - 1) / qpb;
+        prof_begin(s, pcr::kProfNndGrid);
+        switch (lpq) {
+            case 2: hipLaunchKernelGGL(pcr::nc_bquery<2>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+            case 8: hipLaunchKernelGGL(pcr::nc_bquery<8>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+            default: hipLaunchKernelGGL(pcr::nc_bquery<4>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+        }
+        PCR_LAUNCH_CHECK();
+        prof_end(s, pcr::kProfNndGrid);
+        return PCR_OK;
+    }
     rc = pcr::nc_build(a, a.xs, a.K, &a.hdr->cell_s, a.cs, &a.hdr->sflag, a.gacc, a.gate, s);
     if (rc != PCR_OK) return rc;
     // lanes per query (C5, 30K queries: 4 lanes and a ring cap of 1 measured best,

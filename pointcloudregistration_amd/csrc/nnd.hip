@@ -169,14 +169,26 @@ __global__ __launch_bounds__(kThreads) void nnd_finalize_kernel(NndArgs a) {
     if (qi >= nq) return;
     const float *qp = (dir ? a.xyz2 : a.xyz1) + ((size_t)bat * nq + qi) * 3;
     const float *c0 = (dir ? a.xyz1 : a.xyz2) + (size_t)bat * nc * 3;
-    // slices in order: strict < keeps the earlier slice (lower index) on ties
+    // slices in order: strict < keeps the earlier slice (lower index) on ties;
+    // the partials are loaded 8 at a time (independent loads in flight: C2's 32
+    // slices one round trip each had made this launch the longer of the two)
     const int used = (nc + a.slice_len - 1) / a.slice_len;
+    const size_t ostep = (size_t)2 * a.b * a.nmax;
+    const size_t obase = ((size_t)dir * a.b + bat) * a.nmax + qi;
     float d = __builtin_inff();
     int i = 0;
-    for (int sl = 0; sl < used; ++sl) {
-        const size_t o = (((size_t)sl * 2 + dir) * a.b + bat) * a.nmax + qi;
-        const float v = a.pd[o];
-        if (sl == 0 || v < d) { d = v; i = a.pj[o]; }
+    for (int s0 = 0; s0 < used; s0 += 8) {
+        float v[8];
+        int j[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (s0 + u < used) {
+                v[u] = a.pd[obase + (size_t)(s0 + u) * ostep];
+                j[u] = a.pj[obase + (size_t)(s0 + u) * ostep];
+            }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (s0 + u < used && (s0 + u == 0 || v[u] < d)) { d = v[u]; i = j[u]; }
     }
     const float d0 = sqdist(qp[0], qp[1], qp[2], c0[0], c0[1], c0[2]);
     if (d0 != d0) { d = d0; i = 0; }

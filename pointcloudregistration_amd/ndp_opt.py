@@ -173,14 +173,19 @@ def _bce_to_zero(p):
 class _Level:
     CHECK = 8  # replays between the host's looks at the early-stop flag
 
-    def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig):
+    def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig, shared=None):
         dev = s_sample.device
+        # buffers that do not depend on the level (same N, K, M on every level of a
+        # pyramid) are allocated once per optimize_deformation_pyramid call
+        self.shared = {} if shared is None else shared
         self.layer, self.level, self.cfg = layer, level, cfg
         self.s, self.t, self.inds = s_sample, t_sample, inds
         self.params = [p for p in layer.parameters()]
-        self.grads = [torch.zeros_like(p) for p in self.params]
-        self.m = [torch.zeros_like(p) for p in self.params]
-        self.v = [torch.zeros_like(p) for p in self.params]
+        # gradients and Adam moments: views of one buffer (one fill per reset)
+        sizes = [p.numel() for p in self.params]
+        self._gmv = torch.zeros(3, sum(sizes), dtype=self.params[0].dtype, device=dev)
+        self.grads, self.m, self.v = ([t.view_as(p) for t, p in zip(self._gmv[r].split(sizes), self.params)]
+                                      for r in range(3))
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         self.warped = torch.zeros_like(s_sample)
         self.state = torch.zeros(8, dtype=torch.float64, device=dev)
@@ -197,9 +202,13 @@ class _Level:
 
     def reset(self):
         """Fresh optimizer + early-stop state (registration.py:202-206)."""
-        self.state.copy_(torch.tensor([1.0, 0.0, 1e6, 0.0, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64))
-        for t in self.m + self.v:
-            t.zero_()
+        st0 = self.shared.get("state0")
+        if st0 is None:  # one host -> device copy per pyramid, not per level
+            st0 = torch.tensor([1.0, 0.0, 1e6, 0.0, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64,
+                               device=self.state.device)
+            self.shared["state0"] = st0
+        self.state.copy_(st0)
+        self._gmv[1:].zero_()
         self.ctr.zero_()
 
     def step(self):
@@ -221,27 +230,39 @@ class _Level:
         _lib.call("pcr_adam_masked", _lib.ptr(self.table), len(self.params), self.max_numel,
                   _lib.ptr(self.state), float(cfg.lr), 0.9, 0.999, 1e-8, st)
 
+    def needs_warmup(self):
+        return True  # torch autograd: its allocations must precede the capture
+
     def run(self, use_graph=True):
         iters = self.cfg.iters
         if not use_graph or iters <= 1:
             for _ in range(iters):
                 self.step()
             return
-        # warm-up on a side stream (allocator pools, library handles, libpcr
-        # workspaces) then restore parameters and optimizer state
-        keep = [p.detach().clone() for p in self.params]
         side = torch.cuda.Stream(device=self.s.device)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            self.step()
-        torch.cuda.current_stream().wait_stream(side)
-        with torch.no_grad():
-            for p, k in zip(self.params, keep):
-                p.copy_(k)
-        self.reset()
+        if self.needs_warmup():
+            # warm-up on a side stream (allocator pools, library handles, libpcr
+            # workspaces) then restore parameters and optimizer state
+            keep = [p.detach().clone() for p in self.params]
+            with torch.cuda.stream(side):
+                self.step()
+            torch.cuda.current_stream().wait_stream(side)
+            with torch.no_grad():
+                for p, k in zip(self.params, keep):
+                    p.copy_(k)
+            self.reset()
+            side.wait_stream(torch.cuda.current_stream())
+        # capture on the side stream (torch.cuda.graph would also synchronise the
+        # device and run the garbage collector, ~1 ms per level)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.step()
+        with torch.cuda.stream(side):
+            g.capture_begin()
+            try:
+                self.step()
+            finally:
+                g.capture_end()
+        torch.cuda.current_stream().wait_stream(side)
         self.capture_done = time.perf_counter()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
@@ -289,36 +310,50 @@ class _LevelFused(_Level):
     kernels (csrc/ndp_train.hip) instead of torch autograd; same loss, same
     early-stop rule and Adam (pcr_ndp_control / pcr_adam_masked)."""
 
-    CHUNK = 128
+    # points per weight-gradient partial (split-K chunk; PCR_NDP_CHUNK: a tuning hook)
+    CHUNK = int(os.environ.get("PCR_NDP_CHUNK", "128"))
 
-    def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig):
+    def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig, shared=None):
         sd = dict(layer.named_parameters())
         self.W = sd["input.0.weight"].shape[0]
         self.nhid = sum(1 for k in sd if k.startswith("mlp.pts_linears.") and k.endswith(".weight"))
         if self.W != 128 or self.nhid > 4:
             raise NotImplementedError("fused NDP training: width 128, depth <= 5")
-        super().__init__(layer, s_sample, t_sample, inds, level, cfg)
+        super().__init__(layer, s_sample, t_sample, inds, level, cfg, shared)
         dev, N, W, d = s_sample.device, s_sample.shape[0], self.W, self.nhid + 1
         f32 = dict(dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        # the scratch of the kernels depends on (N, W, depth, K, M) only: shared by
+        # the levels of one pyramid (keyed by those sizes)
+        key = (N, W, d, inds.shape[0], t_sample.shape[0], t_sample.data_ptr(), inds.data_ptr())
+
+        def buf(name, make):
+            k = (name,) + key
+            b = self.shared.get(k)
+            if b is None:
+                b = make()
+                self.shared[k] = b
+            return b
+        self._buf = buf
         self.N = N
-        self.pe = torch.zeros(6, N, **f32)
-        self.H = torch.zeros(d, W, N, **f32)
-        self.aux = torch.zeros(8, N, **f32)
-        self.dO = torch.zeros(8, N, **f32)
-        self.D = torch.zeros(d, W, N, **f32)
-        self.gx = torch.zeros(N, 3, **f32)
+        self.pe = buf("pe", lambda: torch.zeros(6, N, **f32))
+        self.H = buf("H", lambda: torch.zeros(d, W, N, **f32))
+        self.aux = buf("aux", lambda: torch.zeros(8, N, **f32))
+        self.dO = buf("dO", lambda: torch.zeros(8, N, **f32))
+        self.D = buf("D", lambda: torch.zeros(d, W, N, **f32))
+        self.gx = buf("gx", lambda: torch.zeros(N, 3, **f32))
         self.xo = self.warped  # the forward writes the level output in place
         nparts = _lib.load().pcr_ndp_train_partial_floats(N, W, d, self.CHUNK)
-        self.part = torch.zeros(max(int(nparts), 1), **f32)
+        self.part = buf("part", lambda: torch.zeros(max(int(nparts), 1), **f32))
         # gradient buffers in the kernel's order; the Adam table must see the same
         # storage, so the branch parameters' grads are row views of one buffer
-        self.gw_b = torch.zeros(7, W, **f32)
-        self.gb_b = torch.zeros(7, **f32)
+        self.gw_b = buf("gw_b", lambda: torch.zeros(7, W, **f32))
+        self.gb_b = buf("gb_b", lambda: torch.zeros(7, **f32))
         names = [n for n, _ in layer.named_parameters()]
         view = {"rot_brach.weight": self.gw_b[0:3], "rot_brach.bias": self.gb_b[0:3],
                 "trn_branch.weight": self.gw_b[3:6], "trn_branch.bias": self.gb_b[3:6],
                 "nr_branch.weight": self.gw_b[6:7], "nr_branch.bias": self.gb_b[6:7]}
-        own = {n: torch.zeros_like(p) for n, p in layer.named_parameters() if n not in view}
+        own = {n: buf("g:" + n, lambda p=p: torch.zeros_like(p)) for n, p in layer.named_parameters() if n not in view}
         order = ["input.0.weight", "input.0.bias"]
         for k in range(self.nhid):
             order += [f"mlp.pts_linears.{k}.weight", f"mlp.pts_linears.{k}.bias"]
@@ -349,22 +384,27 @@ class _LevelFused(_Level):
         t.dO, t.D = self.dO.data_ptr(), self.D.data_ptr()
         K, M = inds.shape[0], t_sample.shape[0]
         self.K, self.M = K, M
-        self.d1 = torch.zeros(1, K, **f32)
-        self.d2 = torch.zeros(1, M, **f32)
-        self.gd1 = torch.zeros(1, K, **f32)
-        self.gd2 = torch.zeros(1, M, **f32)
-        self.i1 = torch.zeros(1, K, dtype=torch.int32, device=dev)
-        self.i2 = torch.zeros(1, M, dtype=torch.int32, device=dev)
-        self.gsub = torch.zeros(1, K, 3, **f32)
-        self.gt = torch.zeros(1, M, 3, **f32)
-        self.t3 = t_sample[None].contiguous()
+        self.d1 = buf("d1", lambda: torch.zeros(1, K, **f32))
+        self.d2 = buf("d2", lambda: torch.zeros(1, M, **f32))
+        self.gd1 = buf("gd1", lambda: torch.zeros(1, K, **f32))
+        self.gd2 = buf("gd2", lambda: torch.zeros(1, M, **f32))
+        # the level Chamfer's answers: shared by the levels, so each level's
+        # searches start from the previous level's answers (box path, ndp_chamfer.hip)
+        self.i1 = buf("i1", lambda: torch.zeros(1, K, **i32))
+        self.i2 = buf("i2", lambda: torch.zeros(1, M, **i32))
+        self.gsub = buf("gsub", lambda: torch.zeros(1, K, 3, **f32))
+        self.gt = buf("gt", lambda: torch.zeros(1, M, 3, **f32))
+        self.t3 = buf("t3", lambda: t_sample[None].contiguous())
         # duplicate-free subset: the forward writes x'[inds] and the backward reads
         # dL/dx' of the subset through inv (no gather / index_add launches)
-        self.use_inv = int(torch.unique(inds).numel()) == K
+        self.use_inv = buf("use_inv", lambda: int(torch.unique(inds).numel()) == K)
         if self.use_inv:
-            self.inv = torch.full((N,), -1, dtype=torch.int32, device=dev)
-            self.inv[inds] = torch.arange(K, dtype=torch.int32, device=dev)
-            self.xs = torch.zeros(1, K, 3, **f32)
+            def make_inv():
+                inv = torch.full((N,), -1, **i32)
+                inv[inds] = torch.arange(K, **i32)
+                return inv
+            self.inv = buf("inv", make_inv)
+            self.xs = buf("xs", lambda: torch.zeros(1, K, 3, **f32))
             t.inv, t.xs, t.gsub = self.inv.data_ptr(), self.xs.data_ptr(), self.gsub.data_ptr()
         # the level's Chamfer with its gradient in one pass (csrc/ndp_chamfer.hip):
         # the target grid built once here, the subset grid rebuilt per iteration
@@ -378,9 +418,10 @@ class _LevelFused(_Level):
         if self.use_nc:
             lib = _lib.load()
             nbytes = int(lib.pcr_ndp_chamfer_scratch_bytes(K, M))
-            self.nc_raw = torch.empty(nbytes + 256, dtype=torch.uint8, device=dev)
+            self.nc_raw = buf("nc_raw", lambda: torch.empty(nbytes + 256, dtype=torch.uint8, device=dev))
             off = (-self.nc_raw.data_ptr()) % 256
-            self.gacc = torch.zeros(int(lib.pcr_ndp_chamfer_gacc_words(K)), dtype=torch.int64, device=dev)
+            self.gacc = buf("gacc", lambda: torch.zeros(int(lib.pcr_ndp_chamfer_gacc_words(K)), dtype=torch.int64,
+                                                        device=dev))
             c = _ChamferC()
             c.xs, c.tgt, c.K, c.M, c.trunc = self.xs.data_ptr(), self.t3.data_ptr(), K, M, 1e9
             c.d1, c.d2, c.i1, c.i2 = (self.d1.data_ptr(), self.d2.data_ptr(), self.i1.data_ptr(),
@@ -388,11 +429,20 @@ class _LevelFused(_Level):
             c.gacc, c.scratch = self.gacc.data_ptr(), self.nc_raw.data_ptr() + off
             self.nc = c
             t.gacc, t.gacc_k = self.gacc.data_ptr(), K
-            self.loss_scratch = torch.zeros(int(lib.pcr_ndp_loss_scratch_bytes()), dtype=torch.uint8, device=dev)
+            self.loss_scratch = buf("loss_scratch", lambda: torch.zeros(int(lib.pcr_ndp_loss_scratch_bytes()),
+                                                                       dtype=torch.uint8, device=dev))
             self.xs0 = s_sample.index_select(0, inds).contiguous()
             _lib.call("pcr_ndp_chamfer_prepare", ctypes.byref(c), _lib.ptr(self.xs0),
                       _lib.stream_handle(dev))
         self.desc = t
+
+    def needs_warmup(self):
+        # libpcr kernels only (no allocation inside a step): one warm-up per
+        # pyramid loads the code objects before the first capture
+        if self.shared.get("warm"):
+            return False
+        self.shared["warm"] = True
+        return True
 
     def _rebuild_table(self):
         tab = (_AdamTensor * len(self.params))()
@@ -474,12 +524,13 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
     t_sample = (tgt - tgt_mean).contiguous()
     ind = torch.as_tensor(np.asarray(inds), dtype=torch.long, device=dev)
     hist, info = [], []
+    shared = {}  # per-pyramid buffers of the levels (_Level)
     for level in range(NDP.n_hierarchy):
         NDP.gradient_setup(optimized_level=level)
         layer = NDP.pyramid[level]
         use_fused = fused and layer.input[0].weight.shape[0] == 128
         t0 = time.perf_counter()
-        lv = (_LevelFused if use_fused else _Level)(layer, s_sample, t_sample, ind, level, cfg)
+        lv = (_LevelFused if use_fused else _Level)(layer, s_sample, t_sample, ind, level, cfg, shared)
         t1 = time.perf_counter()
         lv.run(use_graph)
         st = lv.state.cpu().numpy()

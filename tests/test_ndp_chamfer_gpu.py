@@ -4,7 +4,8 @@ my_lib.cpp: test_nnd_gpu.py).
 
 * distances and indices: bit-exact vs pcr_nnd_forward, for every ring cap
   (PCR_NDP_CHAMFER_RINGS 0..3: more or fewer queries go to the tiled exact
-  scan), on a partially overlapping pair (a third of the target far from the
+  scan) of the grid path and on the box path (default) from any starting
+  answers, on a partially overlapping pair (a third of the target far from the
   subset), quantised ties, and with a NaN (the reference loop);
 * the gradient (exact two-word fixed-point sums of the f32 terms, the exponent
   taken from the iteration's extents): per entry within 1e-12 relative of the
@@ -119,18 +120,37 @@ def _partial_pair(seed, K=6000, M=12000):
     return (torch.from_numpy(s.astype(np.float32)).cuda(), torch.from_numpy(t.astype(np.float32)).cuda())
 
 
-def _check(xs, tgt, trunc=1e9, rings=None):
-    old = os.environ.get("PCR_NDP_CHAMFER_RINGS")
-    try:
-        if rings is not None:
-            os.environ["PCR_NDP_CHAMFER_RINGS"] = str(rings)
+class _env:
+    """Set environment variables for the duration of a block (None: unset)."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _check(xs, tgt, trunc=1e9, rings=None, seeds=None):
+    """rings given: the grid path (PCR_NC_BOX=0) with that ring cap; else the
+    box path, its searches started from `seeds` (i1, i2) when given."""
+    with _env(PCR_NDP_CHAMFER_RINGS=rings, PCR_NC_BOX=None if rings is None else 0):
         nc = _Nc(xs, tgt, trunc)
+        if seeds is not None:
+            nc.i1.copy_(seeds[0])
+            nc.i2.copy_(seeds[1])
         nc.step()
-    finally:
-        if old is None:
-            os.environ.pop("PCR_NDP_CHAMFER_RINGS", None)
-        else:
-            os.environ["PCR_NDP_CHAMFER_RINGS"] = old
     d1, d2, i1, i2, g1 = _reference(xs, tgt, trunc)
     assert torch.equal(nc.d1, d1) and torch.equal(nc.i1, i1)
     assert torch.equal(nc.d2, d2) and torch.equal(nc.i2, i2)
@@ -152,21 +172,38 @@ def _check_exact(nc, trunc):
     return g, want
 
 
-@pytest.mark.parametrize("rings", [0, 1, 2, 3])
+@pytest.mark.parametrize("rings", [None, 0, 1, 2, 3])
 def test_partial_overlap_bitexact_every_ring_cap(rings):
     xs, tgt = _partial_pair(1)
     _check(xs, tgt, rings=rings)
+
+
+def test_box_path_any_seed():
+    """The box path's searches start from the previous answers (i1 / i2): exact
+    from any start -- out-of-range and negative indices, the worst point, the
+    exact answers themselves."""
+    xs, tgt = _partial_pair(6, K=3000, M=7000)
+    K, M = xs.shape[0], tgt.shape[0]
+    _, _, i1, i2, _ = _reference(xs, tgt, 1e9)
+    far1 = torch.argmax(torch.cdist(xs, tgt), dim=1).int()
+    far2 = torch.argmax(torch.cdist(tgt, xs), dim=1).int()
+    i32 = dict(dtype=torch.int32, device="cuda")
+    for seeds in [(torch.full((K,), -7, **i32), torch.full((M,), 10 ** 9, **i32)),
+                  (far1, far2), (i1, i2),
+                  (torch.randint(0, M, (K,), **i32), torch.randint(0, K, (M,), **i32))]:
+        _check(xs, tgt, seeds=seeds)
 
 
 def test_quantised_ties_and_truncation():
     rng = np.random.default_rng(2)
     xs = torch.from_numpy((rng.integers(0, 20, (3000, 3)) * 0.05).astype(np.float32)).cuda()
     tgt = torch.from_numpy((rng.integers(0, 20, (5000, 3)) * 0.05).astype(np.float32)).cuda()
-    _check(xs, tgt)
-    _check(xs, tgt, trunc=0.0025)  # d >= trunc: no gradient, as the glue's mask
+    for rings in (None, 1):  # the box path, the grid path
+        _check(xs, tgt, rings=rings)
+        _check(xs, tgt, trunc=0.0025, rings=rings)  # d >= trunc: no gradient, as the glue's mask
 
 
-@pytest.mark.parametrize("rings", [0, 1])
+@pytest.mark.parametrize("rings", [None, 0, 1])
 def test_far_clusters_and_duplicates(rings):
     """Two target clusters far apart (one 50 cells from every subset point: the
     coarse-box search walks many empty and colliding slots), duplicated points
@@ -179,11 +216,13 @@ def test_far_clusters_and_duplicates(rings):
     _check(torch.from_numpy(xs).cuda(), torch.from_numpy(tgt).cuda(), rings=rings)
 
 
-def test_nan_switches_to_reference_loop():
+@pytest.mark.parametrize("box", [1, 0])
+def test_nan_switches_to_reference_loop(box):
     xs, tgt = _partial_pair(3, K=2000, M=3000)
     xs[17, 1] = float("nan")
-    nc = _Nc(xs, tgt)
-    nc.step()
+    with _env(PCR_NC_BOX=box):
+        nc = _Nc(xs, tgt)
+        nc.step()
     d1, d2, i1, i2, _ = _reference(xs, tgt, 1e9)
     assert torch.equal(nc.i1, i1) and torch.equal(nc.i2, i2)
     assert torch.equal(torch.nan_to_num(nc.d1, nan=-1.0), torch.nan_to_num(d1, nan=-1.0))
@@ -191,18 +230,21 @@ def test_nan_switches_to_reference_loop():
     assert nc.grad64()[1] != 0  # the NaN term is flagged (the backward returns NaN)
 
 
-def test_repeated_steps_and_moving_subset():
+@pytest.mark.parametrize("box", [1, 0])
+def test_repeated_steps_and_moving_subset(box):
     """Per-iteration resets: a second step on the same input gives the same bits,
-    then a moved subset (the cell fixed at prepare) is still exact."""
+    then a moved subset (the cell / the spatial order fixed at prepare) is still
+    exact."""
     xs, tgt = _partial_pair(4)
-    nc = _Nc(xs, tgt)
-    nc.step()
-    first = [t.clone() for t in (nc.d1, nc.d2, nc.i1, nc.i2, nc.gacc)]
-    nc.step()
-    for a, b in zip(first, (nc.d1, nc.d2, nc.i1, nc.i2, nc.gacc)):
-        assert torch.equal(a, b)
-    nc.xs.mul_(1.3).add_(0.05)  # the level's warp moves the subset
-    nc.step()
+    with _env(PCR_NC_BOX=box):
+        nc = _Nc(xs, tgt)
+        nc.step()
+        first = [t.clone() for t in (nc.d1, nc.d2, nc.i1, nc.i2, nc.gacc)]
+        nc.step()
+        for a, b in zip(first, (nc.d1, nc.d2, nc.i1, nc.i2, nc.gacc)):
+            assert torch.equal(a, b)
+        nc.xs.mul_(1.3).add_(0.05)  # the level's warp moves the subset
+        nc.step()
     d1, d2, i1, i2, g1 = _reference(nc.xs, tgt, 1e9)
     assert torch.equal(nc.d1, d1) and torch.equal(nc.i1, i1)
     assert torch.equal(nc.d2, d2) and torch.equal(nc.i2, i2)
