@@ -1475,11 +1475,25 @@ constexpr int row_tiles(int S) { return S <= 2 ? 2 : 1; }
 // column tiles per LDS group of the row screens (featnn_row7's G)
 constexpr int row_group(int S) { return S <= 2 ? 8 : 4; }
 
+// row tiles per wave of pass 1 / pass 2 at S = 2 (PCR_ROW1_RT / PCR_ROW2_RT = 1:
+// one, for a lower register count and more waves per SIMD, at twice the
+// B-fragment reads per MFMA); other S: row_tiles
+static int pass_tiles(int S, bool pass2) {
+    static const int rt1 = [] { const char *e = getenv("PCR_ROW1_RT"); return e ? atoi(e) : 0; }();
+    static const int rt2 = [] { const char *e = getenv("PCR_ROW2_RT"); return e ? atoi(e) : 0; }();
+    return (S == 2 && (pass2 ? rt2 : rt1) == 1) ? 1 : row_tiles(S);
+}
+
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
-static int launch_row7(const RowArgs5 &r, int S, hipStream_t s) {
+static int launch_row7(const RowArgs5 &r, int S, hipStream_t s, int rt) {
     const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_match: grid too large");
+    if (rt == 1 && row_tiles(S) != 1 && S == 2) {
+        hipLaunchKernelGGL((featnn_row7<2, row_group(2), kIdx, 1>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        PCR_LAUNCH_CHECK();
+        return PCR_OK;
+    }
     switch (S) {
 #define PCR_R7CASE(K)                                                                            \
     case K:                                                                                      \
@@ -1539,14 +1553,15 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     RowArgs5 r;
     r.Ap = v.Ap; r.Bp = v.Bp; r.rnr = v.fnr; r.cmax = v.gmax; r.n_rows = n_src; r.n_cols = n_tgt;
     r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
-    r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * row_tiles(v.S)); r.D = D; r.ctbits = 1;
+    const int rt1 = pass_tiles(v.S, false);
+    r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * rt1); r.D = D; r.ctbits = 1;
     // pass 1 codes the LDS group of column tiles (featnn_row7's G), not the tile
     while ((1 << r.ctbits) < (PCR_ROW_TILECODE ? ntm : cdiv(ntm, row_group(v.S)))) ++r.ctbits;
     r.Fr = F; r.Gc = G;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;
     prof_begin(s, kProfFeatScreen);
-    rc = launch_row7<true>(r, v.S, s);
+    rc = launch_row7<true>(r, v.S, s, rt1);
     if (rc != PCR_OK) return rc;
     prof_end(s, kProfFeatScreen);
     RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
@@ -1563,11 +1578,12 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         RowArgs5 r2 = r;
         r2.Ap = v.Bp; r2.Bp = v.Ap; r2.rnr = v.gnr; r2.cmax = v.fmax; r2.n_rows = n_tgt;
         r2.n_cols = n_src; r2.rlist = ma.jlist; r2.rcount = ma.nj; r2.Rmax = Mmax; r2.Cmax = Nmax;
-        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * row_tiles(v.S));
+        const int rt2 = pass_tiles(v.S, true);
+        r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * rt2);
         r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
         r2.w1 = w1; r2.w2 = w2;
         prof_begin(s, kProfFeatScreen2);
-        rc = launch_row7<false>(r2, v.S, s);
+        rc = launch_row7<false>(r2, v.S, s, rt2);
         if (rc != PCR_OK) return rc;
         prof_end(s, kProfFeatScreen2);
         hipLaunchKernelGGL(featmut_resolve, dim3(cdiv(Nmax, 256), P), dim3(256), 0, s, ma);

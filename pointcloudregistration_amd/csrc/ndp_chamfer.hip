@@ -90,6 +90,7 @@ struct NcHdr {
     long long nfflag; // box path: a non-finite gradient term this iteration (nc_bquery)
     unsigned done;    // box path: nc_bquery blocks finished (the last one resets)
     int pad3;
+    unsigned long long st[3];  // box path diagnostics (PCR_NC_STATS=1): queries, groups, leaves scanned
 };
 
 // ---- the box path (default; PCR_NC_BOX=0 selects the grid path above) ------
@@ -140,6 +141,7 @@ struct NcArgs {
     unsigned long long *fbkey;  // K + M: their (d bits, j) minima
     const double *gate;
     bool box;               // the box path (PCR_NC_BOX, default on)
+    bool stats;             // PCR_NC_STATS: count the groups / leaves the queries scan
     NcTree bt, bs;          // its target / subset trees
 };
 
@@ -711,39 +713,67 @@ __global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
             const float U = d2f(C[3 * jp], C[3 * jp + 1], C[3 * jp + 2], qx, qy, qz);
             float best = U;
             int bj = jp;
-            // groups sub, sub + LPQ, ... (G <= 32)
+            // The query's LPQ lanes share one list: lane sub tests groups (then the
+            // leaves of two selected groups) sub, sub + LPQ, ...; the lanes OR their
+            // bits, then take every selected leaf two at a time, lane sub loading its
+            // points sub, sub + LPQ, ... of both (one round trip per two leaves)
+            constexpr int PL = kGrp / LPQ;
+            auto orq = [](unsigned m) {
+#pragma unroll
+                for (int o = 1; o < LPQ; o <<= 1) m |= __shfl_xor(m, o, 64);
+                return m;
+            };
             unsigned gm = 0;
 #pragma unroll
-            for (int t = 0; t < kGrp / LPQ; ++t) {
+            for (int t = 0; t < PL; ++t) {
                 const int g = sub + LPQ * t;
                 if (g < Ct.G && box_lb(Ct.grp[g], qx, qy, qz) <= U) gm |= 1u << g;
             }
-#pragma unroll
-            for (int o = 1; o < LPQ; o <<= 1) gm |= __shfl_xor(gm, o, 64);
+            gm = orq(gm);
+            if (a.stats && sub == 0) {
+                atomicAdd(&a.hdr->st[0], 1ull);
+                atomicAdd(&a.hdr->st[1], (unsigned long long)__popc(gm));
+            }
             while (gm) {
-                const int g = __ffs(gm) - 1;
+                const int ga = __ffs((int)gm) - 1;
                 gm &= gm - 1;
-                // leaves sub, sub + LPQ, ... of group g
-                unsigned lm = 0;
-#pragma unroll
-                for (int t = 0; t < kGrp / LPQ; ++t) {
-                    const int lf = g * kGrp + sub + LPQ * t;
-                    if (lf < Ct.L && box_lb(Ct.leaf[lf], qx, qy, qz) <= U) lm |= 1u << t;
+                int gb = -1;
+                if (gm) {
+                    gb = __ffs((int)gm) - 1;
+                    gm &= gm - 1;
                 }
+                unsigned la = 0, lb = 0;
+#pragma unroll
+                for (int t = 0; t < PL; ++t) {
+                    const int i = sub + LPQ * t;
+                    const int fa = ga * kGrp + i, fb = gb * kGrp + i;
+                    if (fa < Ct.L && box_lb(Ct.leaf[fa], qx, qy, qz) <= U) la |= 1u << i;
+                    if (gb >= 0 && fb < Ct.L && box_lb(Ct.leaf[fb], qx, qy, qz) <= U) lb |= 1u << i;
+                }
+                unsigned long long lm = (unsigned long long)orq(la) | ((unsigned long long)orq(lb) << 32);
+                if (a.stats && sub == 0) atomicAdd(&a.hdr->st[2], (unsigned long long)__popcll(lm));
                 while (lm) {
-                    const int t = __ffs(lm) - 1;
+                    const int b0 = __ffsll((long long)lm) - 1;
                     lm &= lm - 1;
-                    const int p0 = (g * kGrp + sub + LPQ * t) * kLeaf;
-                    const int pn = min(kLeaf, Ct.n - p0);
-                    for (int u = 0; u < pn; u += 8) {
-                        float4 p[8];
-#pragma unroll
-                        for (int v = 0; v < 8; ++v)
-                            if (u + v < pn) p[v] = Ct.pts[p0 + u + v];
-#pragma unroll
-                        for (int v = 0; v < 8; ++v)
-                            if (u + v < pn) take(d2f(p[v].x, p[v].y, p[v].z, qx, qy, qz), __float_as_int(p[v].w), best, bj);
+                    int b1 = -1;
+                    if (lm) {
+                        b1 = __ffsll((long long)lm) - 1;
+                        lm &= lm - 1;
                     }
+                    const int l0 = (b0 < 32 ? ga : gb) * kGrp + (b0 & 31);
+                    const int l1 = b1 < 0 ? -1 : (b1 < 32 ? ga : gb) * kGrp + (b1 & 31);
+                    float4 p[2 * PL];
+                    bool ok[2 * PL];
+#pragma unroll
+                    for (int v = 0; v < 2 * PL; ++v) {
+                        const int lf = v < PL ? l0 : l1;
+                        const int pos = lf * kLeaf + sub + LPQ * (v % PL);
+                        ok[v] = lf >= 0 && pos < Ct.n;
+                        if (ok[v]) p[v] = Ct.pts[pos];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 2 * PL; ++v)
+                        if (ok[v]) take(d2f(p[v].x, p[v].y, p[v].z, qx, qy, qz), __float_as_int(p[v].w), best, bj);
                 }
             }
 #pragma unroll
@@ -856,6 +886,8 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     }
     a.box = true;
     if (const char *e = getenv("PCR_NC_BOX")) a.box = atoi(e) != 0;
+    a.stats = false;
+    if (const char *e = getenv("PCR_NC_STATS")) a.stats = atoi(e) != 0;
     a.kmax = 1;
     if (const char *e = getenv("PCR_NDP_CHAMFER_RINGS")) {  // test / tuning hook: 0..3
         const int v = atoi(e);
@@ -958,18 +990,18 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
         hipLaunchKernelGGL(pcr::nc_leaves, dim3(nbz), dim3(1024), 0, s, a.xs, a.bs, &a.hdr->sflag, a.gacc,
                            &a.hdr->amax_s, a.gate);
         PCR_LAUNCH_CHECK();
-        int lpq = 4;
+        int lpq = 8;
         if (const char *e = getenv("PCR_NC_LPQ")) {
             const int v = atoi(e);
-            if (v == 2 || v == 4 || v == 8) lpq = v;
+            if (v == 4 || v == 8 || v == 16) lpq = v;
         }
         const int qpb = 256 / lpq;
         const int nb0 = (a.K + qpb - 1) / qpb, nb1 = (a.M + qpb - 1) / qpb;
         prof_begin(s, pcr::kProfNndGrid);
         switch (lpq) {
-            case 2: hipLaunchKernelGGL(pcr::nc_bquery<2>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
-            case 8: hipLaunchKernelGGL(pcr::nc_bquery<8>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
-            default: hipLaunchKernelGGL(pcr::nc_bquery<4>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+            case 4: hipLaunchKernelGGL(pcr::nc_bquery<4>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+            case 16: hipLaunchKernelGGL(pcr::nc_bquery<16>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+            default: hipLaunchKernelGGL(pcr::nc_bquery<8>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
         }
         PCR_LAUNCH_CHECK();
         prof_end(s, pcr::kProfNndGrid);

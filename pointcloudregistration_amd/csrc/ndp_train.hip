@@ -25,7 +25,7 @@
 // level runs 2,500 waves, not the 625 of one wave per 32 points).  The backward
 // products use the transposed weights (A[i][k] = W[k][i], lanes read
 // consecutive columns: coalesced).  Weight gradients are split-K GEMMs over
-// 128-point chunks with per-chunk partials reduced in chunk order
+// 128-point chunks with per-chunk partials reduced in a fixed order
 // (deterministic).
 #include "pcr_internal.h"
 #include "ndp_tile.h"
@@ -394,23 +394,35 @@ struct ReduceArgs {
     const double *gate;
 };
 
+// four lanes per output element: lane q sums the chunks c = q (mod 4) in chunk
+// order, then the four sums are combined as (s0 + s1) + (s2 + s3) by two xor
+// shuffles (f32 addition commutes exactly, so every lane holds the same bits):
+// a fixed order, four times the loads in flight of one lane per element (the
+// single-lane loop was a chain of ~20 dependent load batches per element)
 __global__ __launch_bounds__(256) void ndp_wgrad_reduce(ReduceArgs a) {
     if (gated_off(a.gate)) return;
     const ReduceJob jb = a.job[blockIdx.y];
-    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int e = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
     const int nw = jb.FO * jb.FI;
+    const float *src = nullptr;
+    size_t stride = 0;
     if (e < nw) {
-        float s = 0.0f;
-#pragma unroll 8
-        for (int c = 0; c < a.nchunk; ++c) s += jb.part[(size_t)c * nw + e];
-        jb.gw[e] = s;
+        src = jb.part + e;
+        stride = (size_t)nw;
     } else if (e < nw + jb.FO) {
-        const int o = e - nw;
-        float s = 0.0f;
-#pragma unroll 8
-        for (int c = 0; c < a.nchunk; ++c) s += jb.part[(size_t)a.nchunk * nw + (size_t)c * jb.FO + o];
-        jb.gb[o] = s;
+        src = jb.part + (size_t)a.nchunk * nw + (e - nw);
+        stride = (size_t)jb.FO;
     }
+    float s = 0.0f;
+    if (src) {
+#pragma unroll 8
+        for (int c = q; c < a.nchunk; c += 4) s += src[(size_t)c * stride];
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (q != 0 || !src) return;
+    if (e < nw) jb.gw[e] = s;
+    else jb.gb[e - nw] = s;
 }
 
 // ---- the level loss around the Chamfer pass (registration.py:231-244): the
@@ -625,7 +637,7 @@ extern "C" int pcr_ndp_train_backward(const pcr_ndp_train *t, float *part, int32
     add(a.dO, a.H + (size_t)a.nhid * W * N, 7, W, grads[2 + 2 * a.nhid], grads[3 + 2 * a.nhid]);
     hipLaunchKernelGGL(pcr::ndp_wgrad, dim3(nchunk, nj), dim3(1024), 0, s, wa);
     PCR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(pcr::ndp_wgrad_reduce, dim3((W * W + W + 255) / 256, nj), dim3(256), 0, s, ra);
+    hipLaunchKernelGGL(pcr::ndp_wgrad_reduce, dim3((W * W + W + 63) / 64, nj), dim3(256), 0, s, ra);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }

@@ -547,8 +547,12 @@ def optimize_deformation_pyramid(src_pcd, tgt_pcd, inds, config=None, NDP=None, 
             info[-1]["capture_ms"] = (lv.capture_done - t1) * 1e3
         if getattr(lv, "use_nc", False):
             # listed (uncertified) queries per direction of the last evaluated iteration
-            hdr = lv.nc_raw[(lv.nc.scratch - lv.nc_raw.data_ptr()):][:28].cpu().numpy().view(np.int32)
-            info[-1]["fb_cnt"] = (int(hdr[5]), int(hdr[6]))
+            hdr = lv.nc_raw[(lv.nc.scratch - lv.nc_raw.data_ptr()):][:88].cpu().numpy()
+            h32 = hdr[:28].view(np.int32)
+            info[-1]["fb_cnt"] = (int(h32[5]), int(h32[6]))
+            if os.environ.get("PCR_NC_STATS", "0") != "0":
+                # box path: queries, groups and leaves scanned over the level
+                info[-1]["nc_stats"] = [int(v) for v in hdr[64:88].view(np.uint64)]
         info[-1]["setup_ms"] = (t1 - t0) * 1e3
         info[-1]["level_ms"] = (t2 - t0) * 1e3
         hist.append((lv.warped + tgt_mean).cpu().numpy())

@@ -32,4 +32,5 @@ for rep in range(2):
                                                fused=os.environ.get("FUSED", "1") == "1")
     torch.cuda.synchronize()
     rp = [round(i.get("replay_ms", 0.0), 2) for i in out[3]]
-    print(rep, (time.perf_counter() - t0) * 1e3, "ms; replay ms per level", rp, "sum", round(sum(rp), 2), "fb_cnt", [i.get("fb_cnt") for i in out[3]])
+    print(rep, (time.perf_counter() - t0) * 1e3, "ms; replay ms per level", rp, "sum", round(sum(rp), 2), "fb_cnt", [i.get("fb_cnt") for i in out[3]],
+          "nc_stats", [i.get("nc_stats") for i in out[3]][:3])
