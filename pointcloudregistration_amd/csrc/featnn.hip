@@ -1475,12 +1475,13 @@ constexpr int row_tiles(int S) { return S <= 2 ? 2 : 1; }
 // column tiles per LDS group of the row screens (featnn_row7's G)
 constexpr int row_group(int S) { return S <= 2 ? 8 : 4; }
 
-// row tiles per wave of pass 1 / pass 2 at S = 2 (PCR_ROW1_RT / PCR_ROW2_RT = 1:
-// one, for a lower register count and more waves per SIMD, at twice the
-// B-fragment reads per MFMA); other S: row_tiles
+// row tiles per wave of pass 1 / pass 2 at S = 2: pass 1 two (3.64 ms per
+// 256-pair launch vs 3.80 with one), pass 2 one (128 VGPRs, four waves per SIMD
+// instead of two, at twice the B-fragment reads: 1.58 vs 1.64 ms); PCR_ROW1_RT /
+// PCR_ROW2_RT = 1 or 2 override; other S: row_tiles
 static int pass_tiles(int S, bool pass2) {
-    static const int rt1 = [] { const char *e = getenv("PCR_ROW1_RT"); return e ? atoi(e) : 0; }();
-    static const int rt2 = [] { const char *e = getenv("PCR_ROW2_RT"); return e ? atoi(e) : 0; }();
+    static const int rt1 = [] { const char *e = getenv("PCR_ROW1_RT"); return e ? atoi(e) : 2; }();
+    static const int rt2 = [] { const char *e = getenv("PCR_ROW2_RT"); return e ? atoi(e) : 1; }();
     return (S == 2 && (pass2 ? rt2 : rt1) == 1) ? 1 : row_tiles(S);
 }
 

@@ -87,10 +87,12 @@ struct NcHdr {
     unsigned amax_s;  // the subset's, this iteration (nc_count; nc_scan consumes and clears)
     int shift;        // this iteration's fixed-point exponent s (nc_scan)
     int pad2;
-    long long nfflag; // box path: a non-finite gradient term this iteration (nc_bquery)
-    unsigned done;    // box path: nc_bquery blocks finished (the last one resets)
+    long long reserved0;  // (layout kept: the diagnostics below sit at byte 64)
+    unsigned reserved1;
     int pad3;
     unsigned long long st[3];  // box path diagnostics (PCR_NC_STATS=1): queries, groups, leaves scanned
+    unsigned samax[32];        // box path: per subset group, its largest finite |coordinate| (nc_leaves)
+    int sbad[32];              //   and whether it holds a non-finite coordinate
 };
 
 // ---- the box path (default; PCR_NC_BOX=0 selects the grid path above) ------
@@ -249,16 +251,18 @@ constexpr int kScanLds = 32768;
 
 // the fixed-point exponent of this iteration (header comment): every finite
 // term <= T = 2 gmax (A_s + A_t), an entry sums <= M + 1 of them
-__device__ inline int nc_shift(const NcHdr *h, float gmax, int Mq, int fshift) {
-    const double T = 2.0 * (double)gmax *
-                     ((double)__uint_as_float(h->amax_s) + (double)__uint_as_float(h->amax_t)) *
-                     (1.0 + 0x1p-20);
+__device__ inline int nc_shift_of(float amax_s, float amax_t, float gmax, int Mq, int fshift) {
+    const double T = 2.0 * (double)gmax * ((double)amax_s + (double)amax_t) * (1.0 + 0x1p-20);
     const double B = (double)(Mq + 2) * T;
     int sh = 60;
     if (B > 0.0 && __builtin_isfinite(B)) sh = 59 - ilogb(B);  // B < 2^(ilogb+1): B 2^s < 2^60
     sh = sh < -900 ? -900 : (sh > 900 ? 900 : sh);
     if (fshift >= 0) sh = 1000 + fshift;  // marks "hi words only" for fix_add
     return sh;
+}
+
+__device__ inline int nc_shift(const NcHdr *h, float gmax, int Mq, int fshift) {
+    return nc_shift_of(__uint_as_float(h->amax_s), __uint_as_float(h->amax_t), gmax, Mq, fshift);
 }
 
 __global__ __launch_bounds__(1024) void nc_scan(const int *cnt, NcCloud g, NcHdr *h, long long *gacc,
@@ -595,10 +599,12 @@ __global__ __launch_bounds__(1024) void nc_leaves(const float *P, NcTree g, int 
                                                   unsigned *amax, const double *gate) {
     if (gated_off(gate)) return;
     __shared__ NcBox lb[kGrp];
+    __shared__ unsigned s_am[16];
+    __shared__ int s_bad[16];
     const int t = threadIdx.x, k = blockIdx.x * 1024 + t;
-    if (gacc) {  // the 6 kRep n gradient words after the header, spread over every block
-        const size_t nw = (size_t)6 * kRep * g.n;
-        for (size_t e = (size_t)k; e < nw; e += (size_t)gridDim.x * 1024) gacc[1 + e] = 0;
+    if (gacc) {  // the header word and the 6 kRep n gradient words, spread over every block
+        const size_t nw = (size_t)6 * kRep * g.n + 1;
+        for (size_t e = (size_t)k; e < nw; e += (size_t)gridDim.x * 1024) gacc[e] = 0;
     }
     if ((int)blockIdx.x >= g.G) return;  // zeroing-only blocks
     const bool v = k < g.n;
@@ -622,10 +628,13 @@ __global__ __launch_bounds__(1024) void nc_leaves(const float *P, NcTree g, int 
             }
         }
     }
-    if (flag && __ballot(bad) != 0ull && (t & 63) == 0) atomicOr(flag, 1);
-    if (amax) {
+    // per group: its largest finite |coordinate| and a non-finite flag, plain
+    // stores into flag[b] / amax[b] (the query kernel reduces the G of them: no
+    // atomics, nothing to reset between iterations)
+    if (amax || flag) {
         for (int o = 32; o; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
-        if ((t & 63) == 0 && am > 0.0f) atomicMax(amax, __float_as_uint(am));
+        const bool wbad = __ballot(bad) != 0ull;
+        if ((t & 63) == 0) { s_am[t >> 6] = __float_as_uint(am); s_bad[t >> 6] = wbad ? 1 : 0; }
     }
 #pragma unroll
     for (int o = 16; o; o >>= 1)
@@ -652,6 +661,13 @@ __global__ __launch_bounds__(1024) void nc_leaves(const float *P, NcTree g, int 
                 h[c] = fmaxf(h[c], __shfl_xor(h[c], o, 64));
             }
         if (t == 0) g.grp[blockIdx.x] = NcBox{make_float4(l[0], l[1], l[2], 0.f), make_float4(h[0], h[1], h[2], 0.f)};
+        if (t == 0 && (amax || flag)) {
+            unsigned m = 0u;
+            int b = 0;
+            for (int w = 0; w < 16; ++w) { m = max(m, s_am[w]); b |= s_bad[w]; }  // >= 0: bits order as values
+            if (amax) amax[blockIdx.x] = m;
+            if (flag) flag[blockIdx.x] = b;
+        }
     }
 }
 
@@ -674,22 +690,46 @@ __device__ __forceinline__ float box_lb(const NcBox &b, float qx, float qy, floa
 // points cannot win or tie).  The query's lanes split the groups, OR their
 // selections, split each selected group's leaves, and scan their selected
 // leaves' points themselves; the lanes' (d, j) minima are merged
-// lexicographically.  The last block to finish writes the gradient header word
-// and resets the per-iteration fields.
+// lexicographically.  Nothing is reset between iterations: the subset's extent
+// and non-finite flag arrive as nc_leaves' per-group partials (every block
+// reduces them alike), nc_leaves zeroes the gradient header word, block 0 ORs
+// the exponent into it and a non-finite term ORs bit 0.
 template <int LPQ>
 __global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
     if (gated_off(a.gate)) return;
     constexpr int QPB = 256 / LPQ;
-    __shared__ bool last;
+    // the candidate tree's group and leaf boxes, staged once per block (<= 33 KiB):
+    // the box tests read LDS, so a query's chain of dependent global loads is its
+    // start point and its leaves' points only
+    extern __shared__ NcBox sbox[];  // [0, 32): groups, [32, 32 + L): leaves
     const int sub = threadIdx.x % LPQ;
     const int dir = blockIdx.x < nb0 ? 0 : 1;
+    {
+        const NcTree &Ct = dir ? a.bs : a.bt;
+        const float4 *gsrc = reinterpret_cast<const float4 *>(Ct.grp);
+        const float4 *lsrc = reinterpret_cast<const float4 *>(Ct.leaf);
+        float4 *dst = reinterpret_cast<float4 *>(sbox);
+        for (int i = threadIdx.x; i < 2 * Ct.G; i += 256) dst[i] = gsrc[i];
+        for (int i = threadIdx.x; i < 2 * Ct.L; i += 256) dst[2 * kGrp + i] = lsrc[i];
+        __syncthreads();
+    }
     const int k = (blockIdx.x - (dir ? nb0 : 0)) * QPB + (int)threadIdx.x / LPQ;
     const int nq = dir ? a.M : a.K, nc = dir ? a.K : a.M;
     const NcHdr *h = a.hdr;
-    const int sh = nc_shift(h, a.g1 > a.g2 ? a.g1 : a.g2, a.M, a.fshift);
+    // the subset's extent and non-finite flag from nc_leaves' per-group partials
+    // (every block reduces the same values in the same order)
+    unsigned amx = 0u;
+    int sbad = 0;
+    for (int b = 0; b < a.bs.G; ++b) { amx = max(amx, h->samax[b]); sbad |= h->sbad[b]; }
+    const int sh = nc_shift_of(__uint_as_float(amx), __uint_as_float(h->amax_t), a.g1 > a.g2 ? a.g1 : a.g2, a.M,
+                               a.fshift);
+    // the gradient header word (nc_leaves zeroed it): the exponent, once; a
+    // non-finite term ORs bit 0 into the same word (fix_add)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_or(a.gacc, (long long)(sh + 2048) << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float *C = dir ? a.xs : a.tgt;
     if (k < nq) {
-        if ((h->sflag | h->tflag) != 0) {
+        if ((sbad | h->tflag) != 0) {
             // the reference loop: seed with candidate 0, strict < (my_lib.cpp:11-20)
             if (sub == 0) {
                 const float *Q = dir ? a.tgt : a.xs;
@@ -700,7 +740,7 @@ __global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
                     const float d = d2f(C[3 * j], C[3 * j + 1], C[3 * j + 2], qx, qy, qz);
                     if (d < best) { best = d; bj = j; }
                 }
-                emit(a, dir, k, best, bj, sh, &a.hdr->nfflag);
+                emit(a, dir, k, best, bj, sh, a.gacc);
             }
         } else {
             const NcTree &Qt = dir ? a.bt : a.bs;
@@ -727,7 +767,7 @@ __global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
 #pragma unroll
             for (int t = 0; t < PL; ++t) {
                 const int g = sub + LPQ * t;
-                if (g < Ct.G && box_lb(Ct.grp[g], qx, qy, qz) <= U) gm |= 1u << g;
+                if (g < Ct.G && box_lb(sbox[g], qx, qy, qz) <= U) gm |= 1u << g;
             }
             gm = orq(gm);
             if (a.stats && sub == 0) {
@@ -747,8 +787,8 @@ __global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
                 for (int t = 0; t < PL; ++t) {
                     const int i = sub + LPQ * t;
                     const int fa = ga * kGrp + i, fb = gb * kGrp + i;
-                    if (fa < Ct.L && box_lb(Ct.leaf[fa], qx, qy, qz) <= U) la |= 1u << i;
-                    if (gb >= 0 && fb < Ct.L && box_lb(Ct.leaf[fb], qx, qy, qz) <= U) lb |= 1u << i;
+                    if (fa < Ct.L && box_lb(sbox[kGrp + fa], qx, qy, qz) <= U) la |= 1u << i;
+                    if (gb >= 0 && fb < Ct.L && box_lb(sbox[kGrp + fb], qx, qy, qz) <= U) lb |= 1u << i;
                 }
                 unsigned long long lm = (unsigned long long)orq(la) | ((unsigned long long)orq(lb) << 32);
                 if (a.stats && sub == 0) atomicAdd(&a.hdr->st[2], (unsigned long long)__popcll(lm));
@@ -782,24 +822,9 @@ __global__ __launch_bounds__(256) void nc_bquery(NcArgs a, int nb0) {
                 const int oj = __shfl_xor(bj, o, 64);
                 take(ob, oj, best, bj);
             }
-            if (sub == 0) emit(a, dir, qi, best, bj, sh, &a.hdr->nfflag);
+            if (sub == 0) emit(a, dir, qi, best, bj, sh, a.gacc);
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(&a.hdr->done, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last || threadIdx.x != 0) return;
-    __threadfence();
-    NcHdr *hw = a.hdr;
-    const long long nf = __hip_atomic_load(&hw->nfflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.gacc[0] = ((long long)(sh + 2048) << 8) | (nf & 1);
-    hw->nfflag = 0;
-    hw->sflag = 0;
-    hw->amax_s = 0u;
-    hw->done = 0u;
 }
 
 // the scan's dynamic LDS limit, set once outside any stream capture (prepare
@@ -987,8 +1012,8 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
         // the leaf blocks, and enough more that each thread zeroes <= 16 gradient words
         const long long zw = 6LL * pcr::kRep * a.K;
         const int nbz = (int)std::max<long long>(a.bs.G, (zw + 16 * 1024 - 1) / (16 * 1024));
-        hipLaunchKernelGGL(pcr::nc_leaves, dim3(nbz), dim3(1024), 0, s, a.xs, a.bs, &a.hdr->sflag, a.gacc,
-                           &a.hdr->amax_s, a.gate);
+        hipLaunchKernelGGL(pcr::nc_leaves, dim3(nbz), dim3(1024), 0, s, a.xs, a.bs, a.hdr->sbad, a.gacc,
+                           a.hdr->samax, a.gate);
         PCR_LAUNCH_CHECK();
         int lpq = 8;
         if (const char *e = getenv("PCR_NC_LPQ")) {
@@ -997,11 +1022,12 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
         }
         const int qpb = 256 / lpq;
         const int nb0 = (a.K + qpb - 1) / qpb, nb1 = (a.M + qpb - 1) / qpb;
+        const size_t lds = sizeof(pcr::NcBox) * (size_t)(pcr::kGrp + std::max(a.bt.L, a.bs.L));  // <= 33 KiB
         prof_begin(s, pcr::kProfNndGrid);
         switch (lpq) {
-            case 4: hipLaunchKernelGGL(pcr::nc_bquery<4>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
-            case 16: hipLaunchKernelGGL(pcr::nc_bquery<16>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
-            default: hipLaunchKernelGGL(pcr::nc_bquery<8>, dim3(nb0 + nb1), dim3(256), 0, s, a, nb0); break;
+            case 4: hipLaunchKernelGGL(pcr::nc_bquery<4>, dim3(nb0 + nb1), dim3(256), lds, s, a, nb0); break;
+            case 16: hipLaunchKernelGGL(pcr::nc_bquery<16>, dim3(nb0 + nb1), dim3(256), lds, s, a, nb0); break;
+            default: hipLaunchKernelGGL(pcr::nc_bquery<8>, dim3(nb0 + nb1), dim3(256), lds, s, a, nb0); break;
         }
         PCR_LAUNCH_CHECK();
         prof_end(s, pcr::kProfNndGrid);

@@ -189,15 +189,19 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
     const bool valid = pt < a.N;
     const int N = a.N;
     const bool has_nr = a.w_nr != nullptr;
-    // per-point branch gradients (every lane of every wave computes them)
+    // per-point branch gradients: computed once per workgroup by wave 0 (its two
+    // half-waves split the gradient replicas) and broadcast through LDS to the
+    // four waves (each had recomputed them, 96 gradient words per lane)
+    __shared__ float sdO[8][32];
     float dO[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (valid) {
-        const float x[3] = {a.x[3 * pt], a.x[3 * pt + 1], a.x[3 * pt + 2]};
-        float g[3];
+    if (w == 0) {
+        const float x[3] = {valid ? a.x[3 * pt] : 0.f, valid ? a.x[3 * pt + 1] : 0.f, valid ? a.x[3 * pt + 2] : 0.f};
+        float g[3] = {0.f, 0.f, 0.f};
         if (a.inv && a.gacc) {
             // the two-word fixed point of ndp_chamfer.hip: header word = flag bit 0,
-            // (s + 2048) << 8; hi words at 2^-s, lo words (after all hi) at 2^-(s+40)
-            const int k = a.inv[pt];
+            // (s + 2048) << 8; hi words at 2^-s, lo words (after all hi) at 2^-(s+40);
+            // half h sums replicas h, h + 2, ... (integer sums: exact, any order)
+            const int k = valid ? a.inv[pt] : -1;
             const long long hw = a.gacc[0];
             const float bad = (hw & 1) ? __builtin_nanf("") : 0.0f;
             int sh = (int)(hw >> 8) - 2048;
@@ -208,14 +212,17 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
                 long long vh = 0, vl = 0;
                 if (k >= 0)
 #pragma unroll
-                    for (int r = 0; r < PCR_NDP_GACC_REPLICAS; ++r) {
+                    for (int r = h; r < PCR_NDP_GACC_REPLICAS; r += 2) {
                         const size_t o = 1 + 3 * ((size_t)r * a.gacc_k + k) + c;
                         vh += a.gacc[o];
                         vl += a.gacc[o + lo];
                     }
+                vh += __shfl_xor(vh, 32, 64);
+                vl += __shfl_xor(vl, 32, 64);
                 const double v = __builtin_ldexp((double)vh, -sh) + __builtin_ldexp((double)vl, -sh - 40);
                 g[c] = k >= 0 ? (float)v + bad : 0.0f;
             }
+        } else if (!valid) {
         } else if (a.inv) {
             const int k = a.inv[pt];
             g[0] = k >= 0 ? a.gsub[3 * k] : 0.0f;
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
         }
         float aux[7];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) aux[k] = a.aux[(size_t)k * N + pt];
+        for (int k = 0; k < 7; ++k) aux[k] = valid ? a.aux[(size_t)k * N + pt] : 0.f;
         const float r0 = aux[0], r1 = aux[1], r2 = aux[2];
         const float y[3] = {aux[3], aux[4], aux[5]};
         if (has_nr) {
@@ -272,9 +279,19 @@ __global__ __launch_bounds__(64 * kNT) void ndp_train_bwd(TrainArgs a) {
         const float gww = (gw[0] * w[0] + gw[1] * w[1]) + gw[2] * w[2];
 #pragma unroll
         for (int c = 0; c < 3; ++c) dO[c] = 0.001f * ((gw[c] - gww * w[c]) / th + dth * w[c]);
-        if (h == 0 && threadIdx.x < 64)  // wave 0 (w is the rotation axis here)
-            for (int k = 0; k < 8; ++k) a.dO[(size_t)k * N + pt] = dO[k];
+        if (!valid)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dO[k] = 0.0f;
+        if (h == 0) {  // (w is the rotation axis here)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sdO[k][j] = dO[k];
+            if (valid)
+                for (int k = 0; k < 8; ++k) a.dO[(size_t)k * N + pt] = dO[k];
+        }
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dO[k] = sdO[k][j];
     // delta of the last hidden activation: W_b^T dO (K = 8 branch rows, 4 k-steps)
     const int L = a.nhid;
     auto load_act = [&](int layer, int r) -> float {

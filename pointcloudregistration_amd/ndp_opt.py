@@ -171,7 +171,10 @@ def _bce_to_zero(p):
 
 
 class _Level:
-    CHECK = 8  # replays between the host's looks at the early-stop flag
+    CHECK = 8  # iterations between the host's looks at the early-stop flag
+    # iterations per captured graph (PCR_NDP_GRAPH_STEPS): each graph launch costs
+    # a gap of ~8 us on the device; more steps per graph cost capture time
+    GRAPH_STEPS = int(os.environ.get("PCR_NDP_GRAPH_STEPS", "2"))
 
     def __init__(self, layer, s_sample, t_sample, inds, level, cfg: NDPConfig, shared=None):
         dev = s_sample.device
@@ -255,24 +258,37 @@ class _Level:
             side.wait_stream(torch.cuda.current_stream())
         # capture on the side stream (torch.cuda.graph would also synchronise the
         # device and run the garbage collector, ~1 ms per level)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(side):
-            g.capture_begin()
-            try:
-                self.step()
-            finally:
-                g.capture_end()
+        # a graph of `spg` iterations (the iterations are gated on the rule, so a
+        # graph that runs past the stop is a no-op from there on), and one of
+        # the remainder
+        spg = max(1, min(self.GRAPH_STEPS, iters))
+        graphs = {}
+        for n in {spg, iters % spg} - {0}:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                g.capture_begin()
+                try:
+                    for _ in range(n):
+                        self.step()
+                finally:
+                    g.capture_end()
+            graphs[n] = g
         torch.cuda.current_stream().wait_stream(side)
         self.capture_done = time.perf_counter()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
-        for k in range(iters):
-            g.replay()
+        done, seen = 0, 0
+        while done < iters:
+            n = spg if iters - done >= spg else iters - done
+            graphs[n].replay()
+            done += n
             # the replays after the rule fired are no-ops (gated kernels); every
-            # CHECK replays the host looks whether the level has stopped and
+            # CHECK iterations the host looks whether the level has stopped and
             # skips the rest (one 8-byte read; the results do not depend on it)
-            if (k + 1) % self.CHECK == 0 and k + 1 < iters and self.state[0].item() == 0.0:
-                break
+            if done - seen >= self.CHECK and done < iters:
+                seen = done
+                if self.state[0].item() == 0.0:
+                    break
         ev[1].record()
         self.replay_events = ev
 
