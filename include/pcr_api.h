@@ -583,8 +583,15 @@ int pcr_ndp_chamfer_glue(const float *d1, int32_t K, const float *d2, int32_t M,
  *   scratch: pcr_ndp_chamfer_scratch_bytes(K, M) bytes, 256-byte aligned,
  *   owned by the caller for the level.
  * pcr_ndp_chamfer_prepare: the target grid and the subset cell (from xs0, the
- *   level's input subset); once per level, outside the captured graph.
- * pcr_ndp_chamfer_step: one iteration (gated like the other f4 launches). */
+ *   level's input subset) -- with the box path (default; PCR_NC_BOX=0: the grid
+ *   path), both clouds' spatial orders and the target's leaf / group boxes;
+ *   once per level, outside the captured graph.  The path is read from the
+ *   environment by prepare and step alike: keep it unchanged between them.
+ * pcr_ndp_chamfer_step: one iteration (gated like the other f4 launches).  The
+ *   box path starts each query's search from its answer of the previous call,
+ *   read from i1 / i2 before they are overwritten: any value is a valid start
+ *   (out-of-range ones count as 0), the results are exact from every start,
+ *   only the time depends on it. */
 /* pcr_ndp_chamfer_loss: pcr_ndp_chamfer_glue's loss (no dist gradients: the
  *   Chamfer step made them) over 32 workgroups (fixed ranges, partials summed in
  *   block order), then -- when state is given -- pcr_ndp_control's rule on it,
