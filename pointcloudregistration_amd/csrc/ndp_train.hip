@@ -30,6 +30,7 @@
 #include "pcr_internal.h"
 #include "ndp_tile.h"
 #include "ndp_ctl.h"
+#include <cstdlib>
 
 namespace pcr {
 namespace {
