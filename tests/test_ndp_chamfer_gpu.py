@@ -194,6 +194,17 @@ def test_box_path_any_seed():
         _check(xs, tgt, seeds=seeds)
 
 
+@pytest.mark.parametrize("K,M", [(1, 1), (1, 37), (33, 1), (31, 1025), (1025, 33), (2049, 4097)])
+def test_small_and_ragged_sizes(K, M):
+    """Partial leaves and groups (n not a multiple of 32 / 1024), single points,
+    both paths."""
+    rng = np.random.default_rng(K * 7919 + M)
+    xs = torch.from_numpy(rng.normal(0, 1, (K, 3)).astype(np.float32)).cuda()
+    tgt = torch.from_numpy(rng.normal(0, 1, (M, 3)).astype(np.float32)).cuda()
+    _check(xs, tgt)
+    _check(xs, tgt, rings=1)
+
+
 def test_quantised_ties_and_truncation():
     rng = np.random.default_rng(2)
     xs = torch.from_numpy((rng.integers(0, 20, (3000, 3)) * 0.05).astype(np.float32)).cuda()
