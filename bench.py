@@ -53,6 +53,9 @@ def parse():
                     help="skip the PCIe-inclusive (host-resident inputs) measurement")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the C2 / a4 / a10 / f1 / f4 side measurements")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured HIP graph (measured: no gain at 256 pairs, "
+                         "slower at 32 / 64 where the cooperative launches are recorded)")
     ap.add_argument("--streams", type=int, default=1,
                     help="split the rank's shard into this many sub-batches run concurrently on "
                          "their own HIP streams (1..4)")
@@ -1149,8 +1152,10 @@ def main():
     rank, world, local = dist_setup()
     from pointcloudregistration_amd import _lib
     from pointcloudregistration_amd.pipeline import PairPipeline
+    # --graph: the headline replays the step as one captured HIP graph (eager if
+    # the runtime refuses to record a launch); the profiled steps run eagerly
     pipe = PairPipeline(batch.src, batch.tgt, batch.src_feat, batch.tgt_feat, params,
-                        pair_ids=pair_ids)
+                        pair_ids=pair_ids, graph=args.graph)
 
     rows = -(-args.pairs // world)   # equal-size record blocks for the all-gather
     S = max(1, min(args.streams, 4, P))
@@ -1188,6 +1193,8 @@ def main():
     # the per-kernel split from K more steps with libpcr's HIP events around the
     # named kernels (the events add their own packets, so these steps are not
     # the headline's)
+    graphed = pipe._graph is not None
+    pipe.use_graph = False
     _lib.profile_enable(True)
     for pid in range(_lib.PROF_SLOTS):
         _lib.profile_read(pid, reset=True)
@@ -1306,6 +1313,7 @@ def main():
         "roofline_icp": _sweep_roofline("a8 ICP", "icp_kernel", prof["icp"], icp_sweeps, N, cb_i),
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
         "profiled_ms_per_step": pwall / args.steps * 1e3,  # the steps kernels_ms_per_step came from
+        "step_graph": graphed,  # the headline steps were replays of the captured step
         "featnn_rescan_rows_per_step": [r / args.steps for r in rescan_rows],
         "stages_ms": stages,
         "accuracy": {"rre_deg_median": float(np.median(rre)), "rre_deg_max": float(np.max(rre)),

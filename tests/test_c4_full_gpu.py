@@ -122,3 +122,33 @@ def test_sampled_pairs_bitexact_vs_oracle(c4, oracle, p):
     d1, d2, _, _ = oracle.nnd_forward(aligned[None], b.tgt[p][None])
     ch = d1.astype(np.float64).mean() + d2.astype(np.float64).mean()
     assert np.isclose(c4["rec"][p, 36], ch, rtol=1e-6)
+
+
+def test_graph_replay_equals_eager(c4):
+    """bench.py's headline replays the step as one captured HIP graph: the same
+    records bit for bit as the eager step, replay after replay."""
+    b = c4["batch"]
+    pipe = PairPipeline(b.src, b.tgt, b.src_feat, b.tgt_feat, c4["params"],
+                        pair_ids=np.arange(P, dtype=np.int32), graph=True)
+    for _ in range(3):
+        pipe.run()
+        torch.cuda.synchronize()
+        assert _bits(pipe.records().cpu().numpy(), c4["rec"])
+    assert pipe._graph is not None  # 256 pairs: no cooperative launch, capturable
+
+
+def test_graph_small_shard_equals_eager():
+    """The 32-pair shard (cooperative ICP launch): captured or, if the runtime
+    refuses to record it, eager -- the same records either way."""
+    Ps = 32
+    b = synth.make_batch(Ps, n=4096, m=4096, d=D, base_seed=1000, feat_noise=1.0)
+    prm = default_params(seed=0)
+    ids = np.arange(Ps, dtype=np.int32)
+    eager = PairPipeline(b.src, b.tgt, b.src_feat, b.tgt_feat, prm, pair_ids=ids)
+    eager.run()
+    want = eager.records(copy=True).cpu().numpy()
+    pipe = PairPipeline(b.src, b.tgt, b.src_feat, b.tgt_feat, prm, pair_ids=ids, graph=True)
+    for _ in range(2):
+        pipe.run()
+        torch.cuda.synchronize()
+        assert _bits(pipe.records().cpu().numpy(), want)
