@@ -60,12 +60,23 @@ struct IArgs {
     int32_t *stats;
     int32_t *corr_tgt;   // optional (P, Nmax): final correspondence per source point
     const int32_t *order;  // (P, Nmax) spatial order of the source points, or null
-    int G;
+    int G;               // workgroups per pair (phase 2: computed on the device)
+    // tail rebalancing (phase 1 / 2; phase 0 = one launch as before): phase 1 runs
+    // every pair on one workgroup and, once at most thr_active pairs are still
+    // iterating, the rest save their state and list themselves; phase 2 spreads
+    // the listed pairs over all CUs (G = grid / listed) and finishes them
+    int phase, thr_active, gmax2;
+    int *ctl;            // [0] pairs still iterating in phase 1, [1] listed pairs
+    int *list;           // (P) listed pairs
+    double *save;        // (P, kSave) the listed pairs' state
     XPart *part;         // (P, 2, G) when G > 1
     unsigned *bar;       // (P, 2) when G > 1
     int *chunk;          // (P, 2) sweep chunk counters by sweep parity, when G > 1
     unsigned long long *timing;  // debug (PCR_ICP_TIMING): per pair, phase clocks
 };
+
+// a listed pair's state: T (16), C (9), ms (3), mt (3), fit, rmse, count, it
+constexpr int kSave = 36;
 
 __device__ __forceinline__ int cnt_of(const int32_t *n, int p, int mx) {
     return n ? min(max(n[p], 0), mx) : mx;
@@ -87,6 +98,7 @@ struct IShared {  // LDS header; the grid copy (if any) follows
     double U[12];     // this iteration's update
     int nred;         // reductions done (parity of the HBM partial slots)
     int chunk[2];     // next 64-position chunk of the current sweep, by parity (G = 1)
+    int handoff;      // phase 1: this pair is listed for phase 2
 };
 
 // wave-level sums of NQ exact f64 values (integer multiples of the quantum:
@@ -106,7 +118,7 @@ __device__ __forceinline__ void wave_park(IShared &sh, double *v) {
 // sum the NV parked values + (cnt, acc) over the pair's workgroups; result in
 // sh.tot / sh.cnt / sh.acc (all threads call; ends with a barrier)
 template <int NV>
-__device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int cnt,
+__device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int G, int cnt,
                             unsigned long long acc) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #pragma unroll
@@ -128,8 +140,8 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int cnt,
             else if (tid == NV) C += sh.wcnt[w];
             else A += sh.wacc[w];
         }
-        if (a.G > 1) {
-            XPart &me = a.part[((size_t)p * 2 + (sh.nred & 1)) * a.G + g];
+        if (G > 1) {
+            XPart &me = a.part[((size_t)p * 2 + (sh.nred & 1)) * G + g];
             if (tid < NV) me.s[tid] = s;
             else if (tid == NV) me.cnt = C;
             else me.acc = A;
@@ -139,14 +151,14 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int cnt,
             else sh.acc = A;
         }
     }
-    if (a.G > 1) {
-        pair_barrier(a.bar + 2 * (size_t)p, a.G);
+    if (G > 1) {
+        pair_barrier(a.bar + 2 * (size_t)p, G);
         if (tid < NV + 2) {
-            const XPart *all = a.part + ((size_t)p * 2 + (sh.nred & 1)) * a.G;
+            const XPart *all = a.part + ((size_t)p * 2 + (sh.nred & 1)) * G;
             double s = 0.0;
             unsigned long long A = 0;
             int C = 0;
-            for (int h = 0; h < a.G; ++h) {
+            for (int h = 0; h < G; ++h) {
                 if (tid < NV) s += all[h].s[tid];
                 else if (tid == NV) C += all[h].cnt;
                 else A += all[h].acc;
@@ -164,8 +176,20 @@ template <bool kLds>
 __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     IShared &sh = *reinterpret_cast<IShared *>(dsm);
-    const int G = a.G;
-    const int p = blockIdx.x / G, g = blockIdx.x - p * G;
+    int G = a.G, p, g;
+    if (a.phase == 2) {
+        // the listed pairs over the whole grid (uniform in every workgroup)
+        const int R = __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (R <= 0) return;
+        G = max(1, min(a.gmax2, (int)gridDim.x / R));
+        if ((int)blockIdx.x >= R * G) return;  // whole workgroup, before any barrier
+        p = a.list[blockIdx.x / G];
+        g = blockIdx.x - (blockIdx.x / G) * G;
+    } else {
+        p = blockIdx.x / G;
+        g = blockIdx.x - p * G;
+    }
+    const bool resume = a.phase == 2;
     const int n = cnt_of(a.n_src, p, a.Nmax);
     const int m = cnt_of(a.n_tgt, p, a.Mmax);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -174,8 +198,9 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     // working copy (f64 xyz) by source INDEX, AoS
     double *P3 = a.P3 + (size_t)p * a.Nmax * 3;
     int32_t *CT = a.corr_tgt ? a.corr_tgt + (size_t)p * a.Nmax : nullptr;
-    if (tid < 16) sh.T[tid] = a.init[(size_t)p * 16 + tid];
-    if (tid == 0) { sh.nred = 0; sh.chunk[0] = 0; sh.chunk[1] = 0; }
+    const double *sv = resume ? a.save + (size_t)p * kSave : nullptr;
+    if (tid < 16) sh.T[tid] = resume ? sv[tid] : a.init[(size_t)p * 16 + tid];
+    if (tid == 0) { sh.nred = 0; sh.chunk[0] = 0; sh.chunk[1] = 0; sh.handoff = 0; }
     __syncthreads();
     const bool valid = a.d > 0.0 && n > 0 && m > 0;
     bool ident = true;
@@ -207,7 +232,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         const int k = min(200, max(-200, 52 - en - emax));
         if (tid == 0) { sh.sk = ldexp(1.0, k); sh.isk = ldexp(1.0, -k); }
     }
-    if (valid) {  // working copy = init applied to the f32 input (Open3D's Transform)
+    if (valid && !resume) {  // working copy = init applied to the f32 input (Open3D's Transform)
         double T0[12];
         for (int q = 0; q < 12; ++q) T0[q] = sh.T[q];
         const float *Sp = (a.srcp && ord) ? a.srcp + (size_t)p * a.Nmax * 3 : nullptr;
@@ -326,7 +351,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         }
         mark(0);
         wave_park<kQ>(sh, v);
-        pair_reduce<kQ>(a, sh, p, g, cnt, acc);
+        pair_reduce<kQ>(a, sh, p, g, G, cnt, acc);
         // every workgroup has left this sweep (pair_reduce's barrier): re-arm its
         // counter for the sweep after next (the next sweep uses the other one,
         // re-armed one reduction ago)
@@ -359,9 +384,20 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         __syncthreads();  // sh.tot is rewritten by the next reduction
     };
     int it = 0;
+    bool handed = false;
     if (valid) {
-        evaluate(false);
-        for (it = 0; it < a.max_iter;) {
+        if (resume) {  // the state phase 1 left: the last sweep's sums, fit, rmse
+            if (tid < 9) sh.C[tid] = sv[16 + tid];
+            if (tid < 3) { sh.ms[tid] = sv[25 + tid]; sh.mt[tid] = sv[28 + tid]; }
+            fit = sv[31];
+            rmse = sv[32];
+            count = (int)sv[33];
+            it = (int)sv[34];
+            __syncthreads();
+        } else {
+            evaluate(false);
+        }
+        for (; it < a.max_iter;) {
             if (count == 0) break;
             mark(2);
             if (tid == 0) {
@@ -389,8 +425,33 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             evaluate(true);
             ++it;
             if (__builtin_fabs(pf - fit) < a.rel_fit && __builtin_fabs(pr - rmse) < a.rel_rmse) break;
+            if (a.phase == 1 && it < a.max_iter && count > 0) {
+                // few pairs still iterating: hand this one to phase 2 (G = 1 here)
+                if (tid == 0)
+                    sh.handoff = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
+                                 a.thr_active;
+                __syncthreads();
+                if (sh.handoff) {
+                    if (tid == 0) {
+                        double *o = a.save + (size_t)p * kSave;
+                        for (int k = 0; k < 16; ++k) o[k] = sh.T[k];
+                        for (int k = 0; k < 9; ++k) o[16 + k] = sh.C[k];
+                        for (int k = 0; k < 3; ++k) { o[25 + k] = sh.ms[k]; o[28 + k] = sh.mt[k]; }
+                        o[31] = fit;
+                        o[32] = rmse;
+                        o[33] = (double)count;
+                        o[34] = (double)it;
+                        a.list[atomicAdd(&a.ctl[1], 1)] = p;
+                    }
+                    handed = true;
+                    break;
+                }
+            }
         }
     }
+    if (a.phase == 1 && !handed && tid == 0)  // this pair is done: one fewer iterating
+        __hip_atomic_fetch_add(&a.ctl[0], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (handed) return;  // phase 2 writes its outputs
     if (CT) {  // the last sweep wrote CT[0, n) when valid
         for (int i = valid ? n + base : base; i < a.Nmax; i += stride) CT[i] = -1;
     }
@@ -467,16 +528,43 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     // workgroups their cost outgrows the split sweep (32-pair shard: G = 4
     // 0.80 ms, G = 8 0.97 ms; RANSAC, two barriers per sweep, is best at 8)
     a.G = coop_groups(P, per_cu, 4);
+    a.phase = 0;
+    a.thr_active = 0;
+    a.gmax2 = 8;
+    a.ctl = nullptr;
+    a.list = nullptr;
+    a.save = nullptr;
+    // tail rebalancing: a batch that fills the chip with one workgroup per pair
+    // (G = 1) ends on a few slow pairs -- C4: 4.6 iterations per pair on average,
+    // 8 at most, so ~40 % of the CU-time of the launch sat idle.  Phase 1 hands
+    // the last thr_active pairs still iterating to a second, cooperative launch
+    // that gives each of them G = CUs / listed workgroups (PCR_ICP_TAIL=0: one
+    // launch).  The sums are exact, so G changes no bit.
+    const char *tail_env = getenv("PCR_ICP_TAIL");
+    const bool tail_on = !(tail_env && atoi(tail_env) == 0);
+    int ncu = kCUs;
+    {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            ncu = v;
+        else
+            (void)hipGetLastError();
+    }
+    const int grid2 = per_cu > 0 ? per_cu * ncu : 0;
+    const bool two_phase = tail_on && a.G == 1 && a.d > 0.0 && Nmax > 0 && grid2 >= 4 && P >= grid2 / 2;
+    if (two_phase) a.thr_active = grid2 / 4;  // phase 2: >= 4 workgroups per listed pair
     // working copy, by position
     const size_t nm = (size_t)(Nmax > 0 ? Nmax : 1);
     char *ws = (char *)workspace(8, sizeof(double) * 3 * (size_t)P * nm + 64);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
     a.P3 = (double *)ws;
-    if (a.G > 1) {
-        char *cw = (char *)workspace(10, (sizeof(XPart) * 2 * (size_t)a.G + sizeof(unsigned) * 4) * (size_t)P + 64);
+    if (a.G > 1 || two_phase) {
+        const int gp = two_phase ? a.gmax2 : a.G;  // partial slots per pair
+        char *cw = (char *)workspace(10, (sizeof(XPart) * 2 * (size_t)gp + sizeof(unsigned) * 4) * (size_t)P + 64);
         PCR_REQUIRE(cw, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
         a.part = (XPart *)cw;
-        a.bar = (unsigned *)(cw + sizeof(XPart) * 2 * (size_t)a.G * (size_t)P);
+        a.bar = (unsigned *)(cw + sizeof(XPart) * 2 * (size_t)gp * (size_t)P);
         a.chunk = (int *)(a.bar + 2 * (size_t)P);
         PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 4 * (size_t)P, s));
     } else {
@@ -491,12 +579,33 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         PCR_REQUIRE(a.timing, PCR_ERR_NOMEM, "icp timing: %s", pcr_last_error());
         PCR_HIP_CHECK(hipMemsetAsync(a.timing, 0, sizeof(unsigned long long) * 8 * (size_t)P, s));
     }
+    if (two_phase) {
+        char *tw = (char *)workspace(37, sizeof(int) * (2 + (size_t)P) + sizeof(double) * kSave * (size_t)P + 64);
+        PCR_REQUIRE(tw, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
+        a.save = (double *)tw;
+        a.ctl = (int *)(a.save + kSave * (size_t)P);
+        a.list = a.ctl + 2;
+        PCR_HIP_CHECK(hipMemsetD32Async(a.ctl, P, 1, s));       // pairs iterating
+        PCR_HIP_CHECK(hipMemsetAsync(a.ctl + 1, 0, sizeof(int), s));  // none listed
+    }
     prof_begin(s, kProfIcp);
-    {
+    if (!two_phase) {
         void *args[] = {&a};
         PCR_HIP_CHECK(coop_launch(fn, P, a.G, kThreads, args, sm, s));
+        PCR_LAUNCH_CHECK();
+    } else {
+        a.phase = 1;
+        {
+            void *args[] = {&a};
+            PCR_HIP_CHECK(coop_launch(fn, P, 1, kThreads, args, sm, s));  // one workgroup per pair
+            PCR_LAUNCH_CHECK();
+        }
+        a.phase = 2;
+        a.G = 0;  // from the listed count, on the device
+        void *args[] = {&a};
+        PCR_HIP_CHECK(hipLaunchCooperativeKernel(fn, dim3(grid2), dim3(kThreads), args, (unsigned)sm, s));
+        PCR_LAUNCH_CHECK();
     }
-    PCR_LAUNCH_CHECK();
     prof_end(s, kProfIcp);
     if (want_timing) {  // debug: phase split in shader clocks, mean over pairs, to stderr
         std::vector<unsigned long long> h(8 * (size_t)P);

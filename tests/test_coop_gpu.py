@@ -200,3 +200,42 @@ def test_ransac_speculative_mixed_batch(oracle, ransac_sched, wgs, slots, split)
         cs = r["correspondence_set"]
         got = np.nonzero(ct[p] >= 0)[0]
         assert np.array_equal(got, cs[:, 0]) and np.array_equal(ct[p, got], cs[:, 1])
+
+
+@pytest.mark.parametrize("relf", [1e-6, 0.0])
+def test_icp_tail_rebalance_bitexact(oracle, coop_g, relf):
+    """A batch that fills the chip (G = 1) hands its last iterating pairs to a
+    second, cooperative launch with several workgroups per pair (icp.hip's tail
+    rebalancing): the same bits as one launch (PCR_ICP_TAIL=0) and as the
+    oracle, with uneven iteration counts (per-pair init noise; relf = 0: all 30
+    iterations, every pair listed)."""
+    os.environ.pop("PCR_COOP_G", None)
+    P, n = 200, 2000
+    B = synth.make_batch(P, n=n, m=n, d=8, base_seed=4200, feat_noise=1.0)
+    rng = np.random.default_rng(42)
+    init = np.zeros((P, 4, 4))
+    for p in range(P):
+        s = 0.002 + 0.05 * rng.random()
+        init[p, :3, :3] = synth.rotation_xyz(*rng.normal(0, s, 3)) @ B.R[p]
+        init[p, :3, 3] = B.t[p] + rng.normal(0, s, 3)
+        init[p, 3, 3] = 1
+    prm = reg.IcpParams(0.05, relative_fitness=relf, relative_rmse=relf)
+    old = os.environ.get("PCR_ICP_TAIL")
+    try:
+        os.environ["PCR_ICP_TAIL"] = "0"
+        one = reg.icp_batch(B.src, B.tgt, init, prm)
+        one = [_np(t).copy() for t in (one.transformation, one.fitness, one.inlier_rmse, one.stats, one.corr_tgt)]
+        os.environ.pop("PCR_ICP_TAIL")
+        two = reg.icp_batch(B.src, B.tgt, init, prm)
+        two = [_np(t) for t in (two.transformation, two.fitness, two.inlier_rmse, two.stats, two.corr_tgt)]
+    finally:
+        if old is not None:
+            os.environ["PCR_ICP_TAIL"] = old
+    for a, b in zip(one, two):
+        assert _bits(a, b)
+    its = two[3][:, 0]
+    assert its.max() > its.min()  or relf == 0.0
+    for p in (0, int(np.argmax(its)), P - 1):
+        o = oracle.icp(B.src[p], B.tgt[p], 0.05, init=init[p], relative_fitness=relf, relative_rmse=relf)
+        assert _bits(two[0][p], o["T"]), p
+        assert tuple(two[3][p]) == (o["iters"], o["n_corr"])

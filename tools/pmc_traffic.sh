@@ -7,6 +7,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+# one ICP launch (the tail hand-off's cooperative launch faults at exit under
+# the profiler)
+export PCR_ICP_TAIL=0
 OUT=${1:-gpurun_out/pmc_traffic}
 mkdir -p "$OUT"
 for c in FETCH_SIZE WRITE_SIZE; do

@@ -1,4 +1,6 @@
-# Round 4 evidence for profiles/r04/ (TAG=vN): the -m gpu suite, smoke, the
+# Round 4 evidence for profiles/r04/ (TAG=vN; the profiled runs with
+# PCR_ICP_TAIL=0: ICP's second, cooperative launch makes the process fault at
+# exit under rocprofv3): the -m gpu suite, smoke, the
 # default bench line (all legs), the 32 / 64-pair shards, the kernel stats of the
 # 256-pair bench, PMC traffic and SQ counters, the C5 / f4 kernel stats.
 set -o pipefail
@@ -18,7 +20,7 @@ for P in 32 64; do
   timeout -k 10 300 python bench.py --pairs $P --no-secondary --no-cpu-baseline > $T/bench_${P}pairs.json 2> $T/bench_$P.err || { tail -5 $T/bench_$P.err; exit 14; }
   python3 -c "import json;d=json.loads(open('$T/bench_${P}pairs.json').read().strip().splitlines()[-1]);print($P,'pairs ms',round(d['ms_per_step'],3))"
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-secondary --no-cpu-baseline --no-host-resident > $T/prof.log 2>&1
+PCR_ICP_TAIL=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-secondary --no-cpu-baseline --no-host-resident > $T/prof.log 2>&1
 rc=$?; echo "rocprof stats rc $rc"
 case $rc in 124|134|137) exit 15;; esac
 bash tools/pmc_traffic.sh $T/traffic > $T/traffic.txt 2>&1; echo "traffic rc $?"
