@@ -21,6 +21,8 @@
 #include "scan.h"
 #include <stdlib.h>
 #include <algorithm>
+#include <cstdio>
+#include <vector>
 
 namespace pcr {
 namespace {
@@ -1394,8 +1396,16 @@ static RescanArgs5 rescan_args(const float *F, const float *G, const int32_t *n_
 // zero count costs its empty blocks only)
 static int run_rescan(RescanArgs5 &ra, int P, int D, hipStream_t s) {
     const bool v4 = (D % 4) == 0 && ((uintptr_t)ra.F & 15) == 0 && ((uintptr_t)ra.G & 15) == 0;
-    // candidate slices per (pair, direction): ~2048 blocks whatever the batch
-    const int S = std::max(1, std::min(16, 1024 / std::max(P, 1)));
+    // candidate slices per (pair, direction): ~8192 blocks whatever the batch --
+    // a pair's list is short (C4: 27 rows on average, 45 at most, one or two
+    // 32-row batches), so a block is a short chain of dependent candidate
+    // loads and more, shorter slices finish sooner (256 pairs: 4 / 8 / 16
+    // slices 0.575 / 0.489 / 0.471 ms per step); PCR_RESCAN_S (1..16) overrides
+    int S = std::max(1, std::min(16, 4096 / std::max(P, 1)));
+    if (const char *e = getenv("PCR_RESCAN_S")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 16) S = v;
+    }
     if (S > 1) {
         char *rw = (char *)workspace(6, (sizeof(double) + sizeof(int)) * (size_t)P * 2 * ra.cap * S + 64);
         PCR_REQUIRE(rw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
@@ -1403,6 +1413,21 @@ static int run_rescan(RescanArgs5 &ra, int P, int D, hipStream_t s) {
         ra.sj = (int *)(ra.sd + (size_t)P * 2 * ra.cap * S);
     }
     const dim3 rg(P, 2, S);
+    if (getenv("PCR_RESCAN_DEBUG")) {  // diagnostic: the per-pair list lengths (host sync)
+        for (int d = 0; d < 2; ++d) {
+            const int *c = d ? ra.cnt21 : ra.cnt12;
+            if (!c) continue;
+            std::vector<int> h((size_t)P);
+            PCR_HIP_CHECK(hipMemcpyAsync(h.data(), c, sizeof(int) * (size_t)P, hipMemcpyDeviceToHost, s));
+            PCR_HIP_CHECK(hipStreamSynchronize(s));
+            long long tot = 0;
+            int mx = 0, over = 0;
+            for (int v : h) { tot += v; mx = std::max(mx, v); over += v > ra.cap ? 1 : 0; }
+            std::sort(h.begin(), h.end());
+            fprintf(stderr, "rescan dir %d: rows %lld, max %d, p50 %d, p90 %d, p99 %d, pairs over cap %d\n", d, tot,
+                    mx, h[P / 2], h[(P * 9) / 10], h[(P * 99) / 100], over);
+        }
+    }
     prof_begin(s, kProfFeatRescan);
     const int dv = cdiv(D, 16) * 16;
 #define PCR_R3(DVV)                                                                    \
