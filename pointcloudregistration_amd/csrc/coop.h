@@ -13,7 +13,8 @@
 
 namespace pcr {
 
-// bar[0] = arrivals, bar[1] = generation (zeroed before the launch).
+// bar[0] = arrivals (zero before the first arrival; the last arrival resets
+// it, so a completed launch leaves it zero), bar[1] = generation (any start).
 // Cost matters (a split sweep meets here several times per iteration): each
 // thread only waits for its own stores (vmcnt), thread 0 alone makes them
 // device-visible (one release fence = one L2 write-back), arrives and spins with

@@ -70,8 +70,10 @@ struct IArgs {
     int *list;           // (P) listed pairs
     double *save;        // (P, kSave) the listed pairs' state
     XPart *part;         // (P, 2, G) when G > 1
-    unsigned *bar;       // (P, 2) when G > 1
-    int *chunk;          // (P, 2) sweep chunk counters by sweep parity, when G > 1
+    // when G > 1: per pair 4 words at bar + 4 p -- the pair barrier (arrivals,
+    // generation) and, at chunk + 4 p, the sweep chunk counters by sweep parity
+    unsigned *bar;
+    int *chunk;
     unsigned long long *timing;  // debug (PCR_ICP_TIMING): per pair, phase clocks
 };
 
@@ -152,7 +154,7 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int G, in
         }
     }
     if (G > 1) {
-        pair_barrier(a.bar + 2 * (size_t)p, G);
+        pair_barrier(a.bar + 4 * (size_t)p, G);
         if (tid < NV + 2) {
             const XPart *all = a.part + ((size_t)p * 2 + (sh.nred & 1)) * G;
             double s = 0.0;
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             }
             P3[3 * k] = x; P3[3 * k + 1] = y; P3[3 * k + 2] = z;
         }
-        if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);  // (G = 1: the barrier below)
+        if (G > 1) pair_barrier(a.bar + 4 * (size_t)p, G);  // (G = 1: the barrier below)
     }
     GridP4 gl{};
     GridView gg{};
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         }
     };
     auto sync_pair = [&]() {
-        if (G > 1) pair_barrier(a.bar + 2 * (size_t)p, G);
+        if (G > 1) pair_barrier(a.bar + 4 * (size_t)p, G);
         else __syncthreads();
     };
     double fit = 0.0, rmse = 0.0;
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         {  // 64-query chunks of the spatial order taken from a counter (dense and
            // sparse regions cost different time); the counter of this sweep's
            // parity was re-armed after the previous sweep's reduction
-            int *ctr = G > 1 ? a.chunk + 2 * p + (nsweep & 1) : &sh.chunk[nsweep & 1];
+            int *ctr = G > 1 ? a.chunk + 4 * p + (nsweep & 1) : &sh.chunk[nsweep & 1];
             const int nch = (n + 63) >> 6;
             const double c0x = sh.c0[0], c0y = sh.c0[1], c0z = sh.c0[2];
             for (;;) {
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         // counter for the sweep after next (the next sweep uses the other one,
         // re-armed one reduction ago)
         if (tid == 0 && g == 0) {
-            if (G > 1) __hip_atomic_store(a.chunk + 2 * p + (nsweep & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (G > 1) __hip_atomic_store(a.chunk + 4 * p + (nsweep & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else sh.chunk[nsweep & 1] = 0;
         }
         ++nsweep;
@@ -561,12 +563,22 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     a.P3 = (double *)ws;
     if (a.G > 1 || two_phase) {
         const int gp = two_phase ? a.gmax2 : a.G;  // partial slots per pair
-        char *cw = (char *)workspace(10, (sizeof(XPart) * 2 * (size_t)gp + sizeof(unsigned) * 4) * (size_t)P + 64);
+        char *cw = (char *)workspace(10, sizeof(XPart) * 2 * (size_t)gp * (size_t)P + 64);
         PCR_REQUIRE(cw, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
         a.part = (XPart *)cw;
-        a.bar = (unsigned *)(cw + sizeof(XPart) * 2 * (size_t)gp * (size_t)P);
-        a.chunk = (int *)(a.bar + 2 * (size_t)P);
-        PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 4 * (size_t)P, s));
+        // barriers and chunk counters in a slot of their own, zeroed when
+        // allocated: every launch leaves the arrivals and the counters zero (a
+        // barrier resets its arrivals, a sweep re-arms its counter) and the
+        // barrier works from any generation, so no memset per call; the
+        // (pair, 4) layout does not move with P, and a power-of-two size either
+        // fits the zeroed range or outgrows the slot's headroom (fresh, zeroed)
+        size_t nb = 16384;
+        while (nb < 4 * (size_t)P) nb <<= 1;
+        bool fresh = false;
+        a.bar = (unsigned *)workspace(39, sizeof(unsigned) * nb, &fresh);
+        PCR_REQUIRE(a.bar, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
+        if (fresh) PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * nb, s));
+        a.chunk = (int *)(a.bar + 2);
     } else {
         a.part = nullptr;
         a.bar = nullptr;

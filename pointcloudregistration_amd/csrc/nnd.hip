@@ -344,9 +344,17 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 }  // namespace
 
 namespace pcr {
-int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
-                     float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s);
+// large clouds: exact certified grid search (nnd_grid.hip), identical results;
+// PCR_NND_ALGO=brute|grid overrides the size rule.  The grid's builds cost tens
+// of microseconds of launches; below ~2^27 pair evaluations the brute force
+// finishes first (C2: 2 x 4096^2)
+bool nnd_uses_grid(int b, int n, int m) {
+    const char *e = getenv("PCR_NND_ALGO");
+    const bool force_brute = e && e[0] == 'b', force_grid = e && e[0] == 'g';
+    const bool big = (long long)b * n * m > (1LL << 27);
+    return force_grid || (!force_brute && n >= 1024 && m >= 1024 && big);
 }
+}  // namespace pcr
 
 extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, int32_t n,
                                int32_t m, float *dist1, float *dist2, int32_t *idx1,
@@ -369,17 +377,7 @@ extern "C" int pcr_nnd_forward(const float *xyz1, const float *xyz2, int32_t b, 
         }
         return PCR_OK;
     }
-    // large clouds: exact certified grid search (nnd_grid.hip), identical results;
-    // PCR_NND_ALGO=brute|grid overrides the size rule
-    {
-        const char *e = getenv("PCR_NND_ALGO");
-        const bool force_brute = e && e[0] == 'b', force_grid = e && e[0] == 'g';
-        // the grid's builds cost tens of microseconds of launches; below ~2^27
-        // pair evaluations the brute force finishes first (C2: 2 x 4096^2)
-        const bool big = (long long)b * n * m > (1LL << 27);
-        if (force_grid || (!force_brute && n >= 1024 && m >= 1024 && big))
-            return pcr::nnd_forward_grid(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, s);
-    }
+    if (pcr::nnd_uses_grid(b, n, m)) return pcr::nnd_forward_grid(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, s);
     const int nmax = n > m ? n : m;
     // 8 queries per lane (4 packed pairs) and 512-candidate tiles, or -- when that
     // cannot give the launch ~4 workgroups per CU (C2: one pair) -- 2 queries

@@ -23,6 +23,7 @@
 #include "pcr_internal.h"
 #include "scan.h"
 #include "nng.h"
+#include "geom.h"
 #include <cstdlib>
 
 namespace pcr {
@@ -43,6 +44,11 @@ struct NgArgs {
     float *dist[2];       // dist[0] = dist1: queries of set 0 against the grid of set 1
     int32_t *idx[2];
     const double *gate;   // f4 early stop (pcr_internal.h), or null
+    // set 0 as T (x) src, written to xyz[0] by the box pass (nnd_forward_grid_xf;
+    // null: set 0 is read as given)
+    const float *xsrc;
+    const double *xT;
+    float *xout;
 };
 
 // the pair's clouds go to the reference loop (either set flagged by nng_bbox)
@@ -52,21 +58,34 @@ using nng::ccoord;
 using nng::d2f;
 using nng::nhash;
 
-__global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
-    if (gated_off(a.gate)) return;
+// one cloud's box -> its cell size and flag (thread 0 writes both, to global
+// and to *cell_out / *bad_out in LDS); every thread of the block calls it
+__device__ __forceinline__ void bbox_block(const NgArgs &a, float *cell_out, int *bad_out) {
     const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x, n = a.n[s];
     const float *P = a.xyz[s] + (size_t)b * n * 3;
     float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
     int bad = 0;
+    const bool xf = a.xsrc && s == 0;
 #pragma unroll 4
-    for (int i = t; i < n; i += 1024)
-        for (int c = 0; c < 3; ++c) {
-            const float v = P[3 * i + c];
-            bad |= !__builtin_isfinite(v);
-            lo[c] = fminf(lo[c], v);
-            hi[c] = fmaxf(hi[c], v);
+    for (int i = t; i < n; i += 1024) {
+        float v[3];
+        if (xf) {  // transform_kernel's rounding (procrustes.hip): f64 xform12, then f32
+            const float *q = a.xsrc + ((size_t)b * n + i) * 3;
+            double x, y, z;
+            xform12(a.xT + (size_t)b * 16, (double)q[0], (double)q[1], (double)q[2], x, y, z);
+            v[0] = (float)x; v[1] = (float)y; v[2] = (float)z;
+            float *o = a.xout + ((size_t)b * n + i) * 3;
+            o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+        } else {
+            v[0] = P[3 * i]; v[1] = P[3 * i + 1]; v[2] = P[3 * i + 2];
         }
+        for (int c = 0; c < 3; ++c) {
+            bad |= !__builtin_isfinite(v[c]);
+            lo[c] = fminf(lo[c], v[c]);
+            hi[c] = fmaxf(hi[c], v[c]);
+        }
+    }
     __shared__ float sl[3][16], sh[3][16];
     __shared__ int sb[16];
     for (int c = 0; c < 3; ++c)
@@ -80,7 +99,7 @@ __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
         sb[t >> 6] = bad;
     }
     __syncthreads();
-    if (t != 0) return;
+    if (t != 0) return;  // (the callers synchronise after the call)
     double e[3], m = 0.0, amax = 0.0;
     for (int c = 0; c < 3; ++c) {
         float l = sl[c][0], h = sh[c][0];
@@ -101,6 +120,15 @@ __global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
     if (!(amax / cell < 1e9)) bad = 1;
     a.cell[s * a.B + b] = (float)cell;
     a.flag[s * a.B + b] = bad ? 1 : 0;  // every launch writes both sets' flags: no clearing
+    *cell_out = (float)cell;
+    *bad_out = bad;
+}
+
+__global__ __launch_bounds__(1024) void nng_bbox(NgArgs a) {
+    if (gated_off(a.gate)) return;
+    __shared__ float sc;
+    __shared__ int sbad;
+    bbox_block(a, &sc, &sbad);
 }
 
 __global__ void nng_count(NgArgs a) {
@@ -139,14 +167,12 @@ __global__ void nng_scatter(NgArgs a) {
 // cell is atomic order, as before; the (d, j) minimum does not depend on it.
 constexpr int kLdsSlots = 32768;
 
-__global__ __launch_bounds__(1024) void nng_build(NgArgs a) {
-    if (gated_off(a.gate)) return;
+__device__ __forceinline__ void build_block(const NgArgs &a, float cell) {
     extern __shared__ int cnt[];  // S + 1: counts -> exclusive starts -> cursors
     const int s = blockIdx.x, b = blockIdx.y, S = a.S, n = a.n[s];
-    if (ref_loop(a, b)) return;  // nng_bbox ran before on this stream
     const size_t g = (size_t)s * a.B + b;
     const float *P = a.xyz[s] + (size_t)b * n * 3;
-    const double ic = 1.0 / (double)a.cell[g];
+    const double ic = 1.0 / (double)cell;
     for (int i = threadIdx.x; i < S; i += 1024) cnt[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += 1024)
@@ -161,6 +187,20 @@ __global__ __launch_bounds__(1024) void nng_build(NgArgs a) {
         const unsigned h = nhash(ccoord(x, ic), ccoord(y, ic), ccoord(z, ic), S);
         a.pts[g * a.nmax + atomicAdd(&cnt[h], 1)] = make_float4(x, y, z, __int_as_float(i));
     }
+}
+
+// the box and the grid of one cloud in one workgroup (one launch fewer per
+// call).  A cloud flagged by its own box is not built; one flagged only by the
+// other set's box is built and never read (nng_query, launched after both,
+// tests both flags).
+__global__ __launch_bounds__(1024) void nng_bbox_build(NgArgs a) {
+    if (gated_off(a.gate)) return;
+    __shared__ float sc;
+    __shared__ int sbad;
+    bbox_block(a, &sc, &sbad);
+    __syncthreads();
+    if (sbad) return;
+    build_block(a, sc);
 }
 
 // XCD-aware block order: the hardware deals linear block ids round-robin over
@@ -256,8 +296,14 @@ __global__ __launch_bounds__(256) void nng_query(NgArgs a, int nchunk) {
 
 int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
                      float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s) {
+    return nnd_forward_grid_xf(xyz1, nullptr, nullptr, xyz2, b, n, m, dist1, dist2, idx1, idx2, s);
+}
+
+int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, const float *xyz2, int b, int n,
+                        int m, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s) {
     NgArgs a;
     a.xyz[0] = xyz1; a.xyz[1] = xyz2; a.n[0] = n; a.n[1] = m; a.B = b;
+    a.xsrc = src; a.xT = T; a.xout = src ? const_cast<float *>(xyz1) : nullptr;
     a.nmax = n > m ? n : m;
     int S = 256;
     while (S < a.nmax) S <<= 1;
@@ -278,18 +324,20 @@ int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, 
         if (v >= 0.1f && v <= 4.0f) a.cf = v;
     }
     const bool lds_build = S <= kLdsSlots;
+    PCR_REQUIRE(lds_build || !src, PCR_ERR_ARG, "nnd_forward (grid): fused transform needs the LDS build");
     if (!lds_build) PCR_HIP_CHECK(hipMemsetAsync(a.hcnt, 0, sizeof(int) * hc, s));
-    hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(1024), 0, s, a);
-    PCR_LAUNCH_CHECK();
     if (lds_build) {
         // the attribute is set once, outside any stream capture (the NDP level
         // graphs capture this call after an eager warm-up step)
-        static const hipError_t attr = hipFuncSetAttribute(
-            (const void *)nng_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(int) * (kLdsSlots + 1)));
+        static const hipError_t attr = hipFuncSetAttribute((const void *)nng_bbox_build,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)(sizeof(int) * (kLdsSlots + 1)));
         PCR_HIP_CHECK(attr);
-        hipLaunchKernelGGL(nng_build, dim3(2, b), dim3(1024), sizeof(int) * (size_t)(S + 1), s, a);
+        hipLaunchKernelGGL(nng_bbox_build, dim3(2, b), dim3(1024), sizeof(int) * (size_t)(S + 1), s, a);
         PCR_LAUNCH_CHECK();
     } else {
+        hipLaunchKernelGGL(nng_bbox, dim3(2, b), dim3(1024), 0, s, a);
+        PCR_LAUNCH_CHECK();
         const dim3 pg((a.nmax + 255) / 256, b, 2);
         hipLaunchKernelGGL(nng_count, pg, dim3(256), 0, s, a);
         PCR_LAUNCH_CHECK();

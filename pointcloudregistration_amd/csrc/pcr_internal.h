@@ -18,6 +18,15 @@ void clear_error();
 // whether the buffer was (re)allocated by this call (contents undefined).
 void *workspace(int slot, size_t bytes, bool *fresh = nullptr);
 
+// Chamfer NN (nnd.hip / nnd_grid.hip): the size rule of pcr_nnd_forward, and
+// its grid path; _xf forms set 0 as T (x) src (transform_kernel's rounding),
+// writing it to xyz1, inside the grid's box pass (max(n, m) <= 32768)
+bool nnd_uses_grid(int b, int n, int m);
+int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
+                     float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s);
+int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, const float *xyz2, int b, int n,
+                        int m, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s);
+
 inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 // A second stream of the calling thread's (device, workspace context) and two

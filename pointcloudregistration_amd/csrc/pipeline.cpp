@@ -143,9 +143,15 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
                        io->fit_icp, io->stats_icp, nullptr, s, order, gi ? &grid_i : nullptr, perm);
     if (rc != PCR_OK) return rc;
     lap("icp");
-    rc = pcr_transform_batch(io->src_xyz, P, N, io->T_icp, io->aligned, stream);
-    if (rc != PCR_OK) return rc;
-    rc = pcr_nnd_forward(io->aligned, io->tgt_xyz, P, N, M, io->d1, io->d2, io->i1, io->i2, stream);
+    if (pcr::nnd_uses_grid(P, N, M) && N <= 32768 && M <= 32768) {
+        // the aligned sources formed inside the Chamfer's box pass (one launch fewer)
+        rc = pcr::nnd_forward_grid_xf(io->aligned, io->src_xyz, io->T_icp, io->tgt_xyz, P, N, M, io->d1, io->d2,
+                                      io->i1, io->i2, s);
+    } else {
+        rc = pcr_transform_batch(io->src_xyz, P, N, io->T_icp, io->aligned, stream);
+        if (rc != PCR_OK) return rc;
+        rc = pcr_nnd_forward(io->aligned, io->tgt_xyz, P, N, M, io->d1, io->d2, io->i1, io->i2, stream);
+    }
     if (rc != PCR_OK) return rc;
     rc = pcr::pipeline_records(io, s);
     lap("chamfer");
