@@ -1032,8 +1032,12 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 #ifndef PCR_ROW_KV1
 #define PCR_ROW_KV1 0  // pass 1's VALU per MFMA slot (0: the epilogue's VALU spread evenly)
 #endif
-    constexpr int kV = (kIdx && PCR_ROW_KV1 > 0) ? PCR_ROW_KV1
-                                                  : ((kIdx && PCR_ROW_TILECODE) ? 48 : 32) * RT / NX + 1;  // VALU per MFMA slot below
+#ifndef PCR_ROW_KV2
+#define PCR_ROW_KV2 0  // the same for pass 2
+#endif
+    constexpr int kV = (kIdx && PCR_ROW_KV1 > 0)    ? PCR_ROW_KV1
+                       : (!kIdx && PCR_ROW_KV2 > 0) ? PCR_ROW_KV2
+                                                    : ((kIdx && PCR_ROW_TILECODE) ? 48 : 32) * RT / NX + 1;  // VALU per MFMA slot below
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
