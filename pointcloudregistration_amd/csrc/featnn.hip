@@ -1594,10 +1594,12 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.Fr = F; r.Gc = G;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.w1 = nullptr; r.w2 = nullptr;
+    if (prep_event && prep_at == 2) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
     prof_begin(s, kProfFeatScreen);
     rc = launch_row7<true>(r, v.S, s, rt1);
     if (rc != PCR_OK) return rc;
     prof_end(s, kProfFeatScreen);
+    if (prep_event && prep_at == 1) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
     RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
     ra.list12 = v.list12; ra.list21 = v.list21; ra.cnt12 = v.cnt12; ra.cnt21 = zero;
     ra.nn12 = nn12; ra.nn21 = nn21x;

@@ -22,6 +22,12 @@ void *workspace(int slot, size_t bytes, bool *fresh = nullptr);
 // its grid path; _xf forms set 0 as T (x) src (transform_kernel's rounding),
 // writing it to xyz1, inside the grid's box pass (max(n, m) <= 32768)
 bool nnd_uses_grid(int b, int n, int m);
+
+// pcr_pipeline_step's hook into the feature stage (tuning, PCR_PREP_AT): when
+// set, feature_corres_v5 records prep_event on its stream before (at = 2) or
+// after (at = 1) the pass-1 launch, so the side stream's grid builds start there
+extern thread_local hipEvent_t prep_event;
+extern thread_local int prep_at;
 int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
                      float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s);
 int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, const float *xyz2, int b, int n,

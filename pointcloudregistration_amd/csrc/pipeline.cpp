@@ -111,27 +111,51 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     hipEvent_t ev_in = nullptr, ev_prep = nullptr;
     rc = pcr::side_stream(&side, &ev_in, &ev_prep);
     if (rc != PCR_OK) return rc;
-    PCR_HIP_CHECK(hipEventRecord(ev_in, s));
-    PCR_HIP_CHECK(hipStreamWaitEvent(side, ev_in, 0));
+    // when the prep starts: 0 with the step (it then competes with the
+    // bandwidth-bound descriptor pack), 1 / 2 once pass 1 of the feature screen
+    // is done / launched (an event recorded inside the feature stage).  Measured
+    // (tools/r04_check35.sh): 256 pairs 9.47 / 9.36 / 9.48 ms, 32 pairs 1.84 /
+    // 1.83 / 1.81 ms -- 1 for large batches, 2 for small shards; PCR_PREP_AT
+    // overrides.  D > 64 (no hook in that screen): 0
+    int at = P >= 128 ? 1 : 2;
+    if (const char *e = getenv("PCR_PREP_AT")) at = atoi(e) == 1 || atoi(e) == 2 ? atoi(e) : 0;
+    if (io->D > 64) at = 0;
     pcr::GridBatch grid_r{}, grid_i{};
     const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP
     const float *perm = nullptr;     // the sources in that order
     const bool gr = rp->max_correspondence_distance > 0.0, gi = ip->max_correspondence_distance > 0.0;
-    if (gr) {
-        rc = pcr::build_grids(io->tgt_xyz, nullptr, P, M, rp->max_correspondence_distance, side, 4, grid_r);
-        if (rc != PCR_OK) return rc;
-        rc = pcr::spatial_order(io->src_xyz, nullptr, P, N, grid_r.cell, side, 13, &order, &perm, 36);
+    auto prep = [&]() -> int {
+        PCR_HIP_CHECK(hipStreamWaitEvent(side, ev_in, 0));
+        if (gr) {
+            int r = pcr::build_grids(io->tgt_xyz, nullptr, P, M, rp->max_correspondence_distance, side, 4, grid_r);
+            if (r != PCR_OK) return r;
+            r = pcr::spatial_order(io->src_xyz, nullptr, P, N, grid_r.cell, side, 13, &order, &perm, 36);
+            if (r != PCR_OK) return r;
+        }
+        if (gi) {
+            int r = pcr::build_grids(io->tgt_xyz, nullptr, P, M, ip->max_correspondence_distance, side, 7, grid_i);
+            if (r != PCR_OK) return r;
+        }
+        PCR_HIP_CHECK(hipEventRecord(ev_prep, side));
+        return PCR_OK;
+    };
+    if (at == 0) {
+        PCR_HIP_CHECK(hipEventRecord(ev_in, s));
+        rc = prep();
         if (rc != PCR_OK) return rc;
     }
-    if (gi) {
-        rc = pcr::build_grids(io->tgt_xyz, nullptr, P, M, ip->max_correspondence_distance, side, 7, grid_i);
-        if (rc != PCR_OK) return rc;
-    }
-    PCR_HIP_CHECK(hipEventRecord(ev_prep, side));
     lap("prep");
+    pcr::prep_event = at ? ev_in : nullptr;
+    pcr::prep_at = at;
     rc = pcr::feature_corres_impl(io->src_feat, io->tgt_feat, P, N, M, io->D, nullptr, nullptr,
                                   rp->mutual_filter, rp->ransac_n, io->nn12, io->corres, io->n_corres, s);
+    pcr::prep_event = nullptr;
+    pcr::prep_at = 0;
     if (rc != PCR_OK) return rc;
+    if (at) {
+        rc = prep();
+        if (rc != PCR_OK) return rc;
+    }
     lap("features");
     PCR_HIP_CHECK(hipStreamWaitEvent(s, ev_prep, 0));
     rc = pcr::ransac_impl(io->src_xyz, io->tgt_xyz, P, N, M, nullptr, nullptr, io->corres, io->n_corres, N,

@@ -70,6 +70,9 @@ void *workspace(int slot, size_t bytes, bool *fresh) {
     return p;
 }
 
+thread_local hipEvent_t prep_event = nullptr;
+thread_local int prep_at = 0;
+
 // ---- side stream of a (device, workspace context) -------------------------
 namespace {
 struct Side {
