@@ -44,14 +44,16 @@ int pcr_version(void);
 int pcr_workspace_release(void);
 /* end of process: synchronise every device the library used and free its
  * workspace, retired buffers and pooled profiling events (idempotent; the
- * library stays usable).  The Python layer runs it from atexit. */
+ * library stays usable; a device that cannot be synchronised keeps its
+ * buffers).  A HIP graph captured before it records freed buffers and must not
+ * be replayed after it.  The Python layer runs it from atexit. */
 int pcr_shutdown(void);
 /* Concurrent sub-batches.  pcr_set_workspace_context(ctx) (thread-local, 0..3)
  * selects which copy of the library's scratch the calling thread's next calls
  * use: calls that run concurrently on different streams must use different
  * contexts.  pcr_set_concurrency(k) (1..4): k launches share the device, so
- * cooperative grids (ICP's workgroups per pair) are sized to CUs / k and k of
- * them can be resident at once. */
+ * cooperative grids (ICP's workgroups per pair and its tail launch) are sized
+ * to CUs / k and k of them can be resident at once. */
 int pcr_set_workspace_context(int32_t ctx);
 int pcr_set_concurrency(int32_t k);
 

@@ -166,11 +166,24 @@ PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID, PROF_FEAT_SCREEN2 = 5, 6, 7, 8
 PROF_SLOTS = 9   # pcr_internal.h kProfSlots
 
 
+# bumped by every shutdown(): a HIP graph captured before it points at freed
+# workspace buffers and must not be replayed (pipeline.PairPipeline re-captures)
+_generation = 0
+
+
+def generation():
+    return _generation
+
+
 def shutdown():
     """pcr_shutdown(): synchronise and free the library's per-device workspace and
     profiling events (idempotent; the library stays usable and re-allocates on
-    the next call).  Registered with atexit when the library is loaded."""
+    the next call).  Graphs captured before it must not be replayed: the
+    generation counter tells their owners.  Registered with atexit when the
+    library is loaded."""
+    global _generation
     if _lib is not None:
+        _generation += 1
         _lib.pcr_shutdown()
 
 

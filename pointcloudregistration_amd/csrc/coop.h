@@ -56,6 +56,11 @@ __device__ __forceinline__ int coop_load(const int *p) {
 // pairs alone fill it
 int coop_groups(int P, int per_cu, int gmax = 8);
 
+// host: workgroups a cooperative launch may use when it fits `per_cu` per CU:
+// the chip's share of one of the pcr_set_concurrency(k) launches sharing the
+// device (CUs * per_cu / k), so k such launches are co-resident; 0 = cannot tell
+int coop_capacity(int per_cu);
+
 // host: launch `fn` with P*G workgroups (cooperative when G > 1)
 hipError_t coop_launch(const void *fn, int P, int G, int threads, void **args, size_t lds,
                        hipStream_t s);

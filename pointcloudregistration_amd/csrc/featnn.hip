@@ -68,8 +68,9 @@ __global__ __launch_bounds__(1024) void corres_build(const int32_t *nn12, const 
 //   split: x = hi + lo + e_x, hi = f16(x), lo = f16(x - hi): |e_x| <= 2^-22|x|
 //          + 2^-14 (the 2^-14 covers f16 subnormals even if flushed).
 //   operands (k order, each D-segment padded to S = ceil(D/16) chunks of 16):
-//          A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c]
-//          B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo]
+//          A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c | 0]
+//          B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo | 2^15]
+//          (k = 6 of the norm chunk: featnn_row8 sets the row's to 2.0)
 //          nx = |x|^2 / c split into three f16 parts, c = 2^cs fits f16.
 //          Executed: NX = 3S + 1 k-chunks (one MFMA each).  Stored: NM = 2S + 1
 //          -- A as [-2hi | -2lo | norms], B as [hi | lo | norms]; the MFMA of
@@ -106,53 +107,116 @@ inline Split5 split5_params(int D) {
     return s;
 }
 
-// max |element| of each pair's clouds (f32 bits; both clouds -> same slot):
-// gridDim.z 1024-thread blocks per (pair, cloud), each a contiguous slice of
-// float4 loads (several in flight per thread), one atomic per block -- with few
-// pairs one block per cloud was a chain of ~64 dependent load round trips
-// Partial maxima, one plain store per block (mxp[(p * 2 + which) * Z + z]): the
-// packs reduce them, so nothing has to be cleared before this launch.  Block
-// (p, 0, 0) also clears the pair's counters that the later launches of the
-// stage accumulate into (the packs' norm maxima, the rescan list counts).
-__global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_t *nf, int Nmax,
-                                                    const float *G, const int32_t *ng, int Mmax,
-                                                    int D, unsigned *mxp, unsigned *clr, int P) {
-    const int p = blockIdx.x, which = blockIdx.y, t = threadIdx.x, z = blockIdx.z, Z = gridDim.z;
-    const float *X = which ? G : F;
-    const int cnt = which ? count_of(ng, p, Mmax) : count_of(nf, p, Nmax);
-    const size_t tot = (size_t)cnt * D;
-    const float *x = X + (size_t)p * (which ? Mmax : Nmax) * D;
-    float m = 0.0f;
-    if (((uintptr_t)x & 15) == 0) {
-        const float4 *x4 = reinterpret_cast<const float4 *>(x);
-        const size_t t4 = tot >> 2;
-        const size_t per = (t4 + Z - 1) / Z, lo = min(t4, per * z), hi = min(t4, lo + per);
-#pragma unroll 4
-        for (size_t i = lo + t; i < hi; i += 1024) {
-            const float4 v = x4[i];
-            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+// Round 5: the pair's scale without a separate pass over the descriptors.
+// The split needs every |x s| below 2^T (f16 range of hi / lo and of the norm
+// parts); round 4 read both clouds once for their max (feat_maxabs, 537 MB per
+// 256-pair step) before the packs read them again.  Now:
+//   feat_sample  -- per pair, the max |x| of the first kSampleRows rows of each cloud;
+//   the packs    -- scale s = 2^(T - kSpecMargin - 1 - e) for the sample max in
+//                   [2^e, 2^(e+1)), i.e. kSpecMargin binades of headroom; a row
+//                   with an element at or above 2^T after scaling (or not
+//                   finite) flags its pair;
+//   repair       -- feat_maxabs and the packs again, for the flagged pairs only
+//                   (the round-4 path: s from the full max), launched every
+//                   call on a small grid that walks the flags (empty in the
+//                   common case).
+// The screens' bounds are in the units of the scale actually used (the packs
+// store it per pair), so a smaller-than-optimal scale only loosens the
+// certification by its absolute (f16 subnormal, norm-split) terms: one binade
+// of headroom (any element up to 2-4x the sample's max stays in range) cost
+// ~2 % of the bound at the bench's magnitudes; three binades cost 25 % (27 %
+// more rows rescanned, measured).
+constexpr int kSpecMargin = 1;
+constexpr int kSampleRows = 64;  // rows of each cloud in the sample
+constexpr int kRepairR = 8;  // repair launches' grid.y (flagged pairs by rank mod R)
+
+// the flagged pairs of rank y, y + R, ... (every wave walks the same flags, so
+// control flow stays uniform across the block)
+template <class Fn>
+__device__ __forceinline__ void for_flagged(const int *bad, int P, int y, int R, Fn fn) {
+    const int l = threadIdx.x & 63;
+    int rank = 0;
+    for (int b = 0; b < P; b += 64) {
+        unsigned long long f = __ballot(b + l < P && bad[b + l] != 0);
+        while (f) {
+            const int q = b + __builtin_ctzll(f);
+            f &= f - 1;
+            if (rank % R == y) fn(q);
+            ++rank;
         }
-        if (z == Z - 1)
-            for (size_t i = (t4 << 2) + t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
-    } else {
-        for (size_t i = (size_t)z * 1024 + t; i < tot; i += (size_t)Z * 1024) m = fmaxf(m, fabsf(x[i]));
+    }
+}
+
+// sample max bits per pair; clears the pair's counters that the stage's later
+// launches accumulate into (norm maxima, rescan list counts) and its flag
+__global__ __launch_bounds__(256) void feat_sample(const float *F, const int32_t *nf, int Nmax,
+                                                   const float *G, const int32_t *ng, int Mmax, int D,
+                                                   unsigned *smax, unsigned *clr, int *bad, int P) {
+    const int p = blockIdx.x, t = threadIdx.x;
+    float m = 0.0f;
+    for (int which = 0; which < 2; ++which) {
+        const float *x = (which ? G + (size_t)p * Mmax * D : F + (size_t)p * Nmax * D);
+        const int rows = min(which ? count_of(ng, p, Mmax) : count_of(nf, p, Nmax), kSampleRows);
+        for (int i = t; i < rows * D; i += 256) m = fmaxf(m, fabsf(x[i]));
     }
 #pragma unroll
     for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    __shared__ float wm[16];
+    __shared__ float wm[4];
     if ((t & 63) == 0) wm[t >> 6] = m;
     __syncthreads();
     if (t == 0) {
-        float r = wm[0];
-        for (int w = 1; w < 16; ++w) r = fmaxf(r, wm[w]);
-        mxp[((size_t)p * 2 + which) * Z + z] = __float_as_uint(r);  // r >= 0, never NaN
-        if (which == 0 && z == 0) {  // gmax, fmax, (mx: written by the packs), cnt12, cnt21
-            clr[p] = 0u;
-            clr[P + p] = 0u;
-            clr[3 * P + p] = 0u;
-            clr[4 * P + p] = 0u;
-        }
+        smax[p] = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));  // >= 0, never NaN
+        clr[p] = 0u;          // gmax
+        clr[P + p] = 0u;      // fmax
+        clr[3 * P + p] = 0u;  // cnt12
+        clr[4 * P + p] = 0u;  // cnt21
+        bad[p] = 0;
     }
+}
+
+// repair: max |element| of each FLAGGED pair's clouds, gridDim.z 1024-thread
+// blocks per (pair, cloud), each a contiguous slice of float4 loads; partial
+// maxima, one plain store per block (mxp[(p * 2 + which) * Z + z]); block
+// (., 0, 0) also clears the pair's norm maxima for the repair packs
+__global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_t *nf, int Nmax,
+                                                    const float *G, const int32_t *ng, int Mmax,
+                                                    int D, unsigned *mxp, unsigned *clr, const int *bad, int P) {
+    const int which = blockIdx.y, t = threadIdx.x, z = blockIdx.z, Z = gridDim.z;
+    for_flagged(bad, P, blockIdx.x, gridDim.x, [&](int p) {
+        const float *X = which ? G : F;
+        const int cnt = which ? count_of(ng, p, Mmax) : count_of(nf, p, Nmax);
+        const size_t tot = (size_t)cnt * D;
+        const float *x = X + (size_t)p * (which ? Mmax : Nmax) * D;
+        float m = 0.0f;
+        if (((uintptr_t)x & 15) == 0) {
+            const float4 *x4 = reinterpret_cast<const float4 *>(x);
+            const size_t t4 = tot >> 2;
+            const size_t per = (t4 + Z - 1) / Z, lo = min(t4, per * z), hi = min(t4, lo + per);
+            for (size_t i = lo + t; i < hi; i += 1024) {
+                const float4 v = x4[i];
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            }
+            if (z == Z - 1)
+                for (size_t i = (t4 << 2) + t; i < tot; i += 1024) m = fmaxf(m, fabsf(x[i]));
+        } else {
+            for (size_t i = (size_t)z * 1024 + t; i < tot; i += (size_t)Z * 1024) m = fmaxf(m, fabsf(x[i]));
+        }
+#pragma unroll
+        for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        __shared__ float wm[16];
+        if ((t & 63) == 0) wm[t >> 6] = m;
+        __syncthreads();
+        if (t == 0) {
+            float r = wm[0];
+            for (int w = 1; w < 16; ++w) r = fmaxf(r, wm[w]);
+            mxp[((size_t)p * 2 + which) * Z + z] = __float_as_uint(r);  // r >= 0, never NaN
+            if (which == 0 && z == 0) {  // gmax, fmax: the repair packs max into them again
+                clr[p] = 0u;
+                clr[P + p] = 0u;
+            }
+        }
+        __syncthreads();
+    });
 }
 
 // the pair's max |element| from feat_maxabs' 2 Z partials (bits of non-negative
@@ -173,95 +237,128 @@ __device__ __forceinline__ float pair_scale5(unsigned mbits, int T) {
     return __int_as_float((e + 127) << 23);
 }
 
+// Where a pack launch takes its pairs and their scale (see feat_sample):
+// normal: grid.y = P, the pair's sample max with kSpecMargin binades of
+// headroom, rows outside the split's range flag the pair; repair: grid.y =
+// kRepairR, the flagged pairs by rank, the full max from feat_maxabs.
+struct PackCtl {
+    const unsigned *smax;  // [P] sample max bits (normal)
+    const unsigned *mxp;   // [P][2][Z] full partial maxima (repair)
+    int Z, P, repair;
+    int *bad;              // [P] flags
+    unsigned *sc;          // [P] the scale used (f32 bits), for the rescans
+};
+
+template <class Body>
+__device__ __forceinline__ void pack_pairs(const PackCtl &c, int T, Body body) {
+    if (!c.repair) {
+        const int p = blockIdx.y;
+        const float s = pair_scale5(c.smax[p], T - kSpecMargin);
+        if (blockIdx.x == 0 && threadIdx.x == 0) c.sc[p] = __float_as_uint(s);
+        body(p, s, true);
+    } else {
+        for_flagged(c.bad, c.P, blockIdx.y, gridDim.y, [&](int p) {
+            const float s = pair_scale5(pair_max_bits(c.mxp, c.Z, p), T);
+            if (blockIdx.x == 0 && threadIdx.x == 0) c.sc[p] = __float_as_uint(s);
+            body(p, s, false);
+            __syncthreads();  // the block's LDS is reused by the next pair
+        });
+    }
+}
+
 // role 0: rows (A), role 1: columns (B).  256-thread blocks, one wave per
 // 32-row tile; each tile is staged through LDS with coalesced loads (scaled,
 // exact) and every lane emits its 2S + 1 stored 16-byte operand fragments.
 __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t *n, int Nmax, int D,
-                                                  int S, int ntiles, int role, Split5 sp,
-                                                  const unsigned *mxp, int Z, unsigned *mx, f16x8 *Xp,
-                                                  float *nrm, unsigned *nmax) {
+                                                  int S, int ntiles, int role, Split5 sp, PackCtl pc,
+                                                  f16x8 *Xp, float *nrm, unsigned *nmax) {
     __shared__ float xs[4][32][65];  // D <= 64 (+1 pad: conflict-free row reads)
-    const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
-    const int cnt = count_of(n, p, Nmax);
-    const int nrows = min(max(cnt - t * 32, 0), 32);
-    const unsigned mb = pair_max_bits(mxp, Z, p);
-    if (blockIdx.x == 0 && threadIdx.x == 0) mx[p] = mb;  // for the rescans (later launches)
-    const float s = pair_scale5(mb, sp.T);
-    const float *base = X + ((size_t)p * Nmax + (size_t)t * 32) * D;
-    float (*x)[65] = xs[w];
-    // e / D by a 64-bit reciprocal (exact for e < 2^16; 2^32/D + 1 needs 33 bits at D = 1)
-    const unsigned long long invD = 0xFFFFFFFFull / (unsigned long long)D + 1ull;
-    for (int e = l; e < 32 * D; e += 64) {
-        const int r = (int)(((unsigned long long)e * invD) >> 32), k = e - r * D;
-        x[r][k] = r < nrows ? base[e] * s : 0.0f;
-    }
-    __syncthreads();
-    const int rr = l & 31, h = l >> 5;
-    const bool valid = rr < nrows;
-    double acc = 0.0;
-    for (int k = 0; k < D; ++k) {
-        const double v = (double)x[rr][k];
-        acc = acc + v * v;
-    }
-    // norm parts of acc / c (exact power-of-two division)
-    _Float16 np[3];
-    if (valid) {
-        double wv = acc * __builtin_ldexp(1.0, -sp.cs);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            np[q] = (_Float16)(float)wv;  // |wv| < 2^15: double->float->half may round twice;
-            wv = wv - (double)np[q];      // the bound charges 2^-11 per part regardless
-        }
-    } else {
-        // finite sentinel 3 * 65504 * c > any real distance (<= 4 D 2^2T):
-        // index bits are OR-ed into screen values, which must not be inf
-        np[0] = (_Float16)65504.0f;
-        np[1] = (_Float16)65504.0f;
-        np[2] = (_Float16)65504.0f;
-    }
-    const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
-    const int NM = 2 * S + 1;
-    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NM * 64 + l;
-    for (int c = 0; c < NM; ++c) {
-        f16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int seg = c < S ? 0 : (c < 2 * S ? 1 : 2);   // hi | lo | norms
-            const int k = 16 * (c - seg * S) + 8 * h + j;      // index inside the segment
-            _Float16 v = (_Float16)0.0f;
-            if (seg < 2) {
-                if (k < D) {
-                    const float xv = x[rr][k];
-                    const _Float16 hi = (_Float16)xv;
-                    const _Float16 lo = (_Float16)(xv - (float)hi);
-                    const _Float16 part = seg == 0 ? hi : lo;
-                    v = role == 0 ? (_Float16)(-2.0f * (float)part) : part;
-                }
-            } else {
-                if (k < 3) v = role == 0 ? np[k] : cval;
-                else if (k < 6) v = role == 0 ? cval : np[k - 3];
-            }
-            o[j] = v;
-        }
-        dst[(size_t)c * 64] = o;
-    }
-    // the pair's max norm: one atomic per WORKGROUP.  The P words share a few
-    // cache lines, and one atomic per wave (256 per cloud) serialised at the
-    // L2: ~80 us per launch whatever the batch.  Max of the bit patterns: the
-    // same word per-lane atomics would leave, NaN included.
-    const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
-    if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
-    unsigned rb = __float_as_uint(r);
-#pragma unroll
-    for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
     __shared__ unsigned wmax[4];
-    if (l == 0) wmax[w] = rb;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-        if (m != 0u) atomicMax(nmax + p, m);
-    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
+    const float lim = __builtin_ldexpf(1.0f, sp.T);
+    pack_pairs(pc, sp.T, [&](int p, float s, bool check) {
+        const int cnt = count_of(n, p, Nmax);
+        const int nrows = min(max(cnt - t * 32, 0), 32);
+        const float *base = X + ((size_t)p * Nmax + (size_t)t * 32) * D;
+        float (*x)[65] = xs[w];
+        // e / D by a 64-bit reciprocal (exact for e < 2^16; 2^32/D + 1 needs 33 bits at D = 1)
+        const unsigned long long invD = 0xFFFFFFFFull / (unsigned long long)D + 1ull;
+        bool ok = true;
+        for (int e = l; e < 32 * D; e += 64) {
+            const int r = (int)(((unsigned long long)e * invD) >> 32), k = e - r * D;
+            const float v = r < nrows ? base[e] * s : 0.0f;
+            ok = ok && __builtin_fabsf(v) < lim;  // NaN / inf: not ok
+            x[r][k] = v;
+        }
+        if (check && !ok) pc.bad[p] = 1;
+        __syncthreads();
+        const int rr = l & 31, h = l >> 5;
+        const bool valid = rr < nrows;
+        double acc = 0.0;
+        for (int k = 0; k < D; ++k) {
+            const double v = (double)x[rr][k];
+            acc = acc + v * v;
+        }
+        // norm parts of acc / c (exact power-of-two division)
+        _Float16 np[3];
+        if (valid) {
+            double wv = acc * __builtin_ldexp(1.0, -sp.cs);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                np[q] = (_Float16)(float)wv;  // |wv| < 2^15: double->float->half may round twice;
+                wv = wv - (double)np[q];      // the bound charges 2^-11 per part regardless
+            }
+        } else {
+            // finite sentinel 3 * 65504 * c > any real distance (<= 4 D 2^2T):
+            // index bits are OR-ed into screen values, which must not be inf
+            np[0] = (_Float16)65504.0f;
+            np[1] = (_Float16)65504.0f;
+            np[2] = (_Float16)65504.0f;
+        }
+        const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
+        const int NM = 2 * S + 1;
+        f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NM * 64 + l;
+        for (int c = 0; c < NM; ++c) {
+            f16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int seg = c < S ? 0 : (c < 2 * S ? 1 : 2);   // hi | lo | norms
+                const int k = 16 * (c - seg * S) + 8 * h + j;      // index inside the segment
+                _Float16 v = (_Float16)0.0f;
+                if (seg < 2) {
+                    if (k < D) {
+                        const float xv = x[rr][k];
+                        const _Float16 hi = (_Float16)xv;
+                        const _Float16 lo = (_Float16)(xv - (float)hi);
+                        const _Float16 part = seg == 0 ? hi : lo;
+                        v = role == 0 ? (_Float16)(-2.0f * (float)part) : part;
+                    }
+                } else {
+                    if (k < 3) v = role == 0 ? np[k] : cval;
+                    else if (k < 6) v = role == 0 ? cval : np[k - 3];
+                    else if (k == 6 && role == 1) v = (_Float16)32768.0f;  // featnn_row8's bias
+                }
+                o[j] = v;
+            }
+            dst[(size_t)c * 64] = o;
+        }
+        // the pair's max norm: one atomic per WORKGROUP.  The P words share a few
+        // cache lines, and one atomic per wave (256 per cloud) serialised at the
+        // L2: ~80 us per launch whatever the batch.  Max of the bit patterns: the
+        // same word per-lane atomics would leave, NaN included.
+        const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
+        if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+        unsigned rb = __float_as_uint(r);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
+        if (l == 0) wmax[w] = rb;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            if (m != 0u) atomicMax(nmax + p, m);
+        }
+    });
 }
 
 // Register-resident pack for a compile-time D (the hot D = 32): one lane per
@@ -272,104 +369,107 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
 // feat_pack5 (same operations, same order).
 template <int D>
 __global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t *n, int Nmax,
-                                                   int ntiles, int role, Split5 sp,
-                                                   const unsigned *mxp, int Z, unsigned *mx, f16x8 *Xp,
-                                                   float *nrm, unsigned *nmax) {
+                                                   int ntiles, int role, Split5 sp, PackCtl pc,
+                                                   f16x8 *Xp, float *nrm, unsigned *nmax) {
     constexpr int S = (D + 15) / 16;  // chunks per segment
     constexpr int NM = 2 * S + 1;     // stored chunks
     constexpr int G = 2 * S;          // 8-half fragments per segment
-    const int p = blockIdx.y, w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
-    const int cnt = count_of(n, p, Nmax);
-    const int nrows = min(max(cnt - t * 32, 0), 32);
-    const unsigned mb = pair_max_bits(mxp, Z, p);
-    if (blockIdx.x == 0 && threadIdx.x == 0) mx[p] = mb;  // for the rescans (later launches)
-    const float s = pair_scale5(mb, sp.T);
-    const int rr = l & 31, h = l >> 5;
-    const bool valid = rr < nrows;
-    float x[D];
-    if (valid) {
-        const float4 *row = reinterpret_cast<const float4 *>(X + ((size_t)p * Nmax + (size_t)t * 32 + rr) * D);
-#pragma unroll
-        for (int q = 0; q < D / 4; ++q) {
-            const float4 v = row[q];
-            x[4 * q] = v.x * s; x[4 * q + 1] = v.y * s; x[4 * q + 2] = v.z * s; x[4 * q + 3] = v.w * s;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < D; ++k) x[k] = 0.0f;
-    }
-    double acc = 0.0;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-        const double v = (double)x[k];
-        acc = acc + v * v;
-    }
-    _Float16 np[3];
-    if (valid) {
-        double wv = acc * __builtin_ldexp(1.0, -sp.cs);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            np[q] = (_Float16)(float)wv;
-            wv = wv - (double)np[q];
-        }
-    } else {
-        np[0] = (_Float16)65504.0f;
-        np[1] = (_Float16)65504.0f;
-        np[2] = (_Float16)65504.0f;
-    }
-    const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
-    _Float16 s0[D], s1[D];  // the two stored segments of this role: hi | lo
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-        const _Float16 hi = (_Float16)x[k];
-        const _Float16 lo = (_Float16)(x[k] - (float)hi);
-        if (role == 0) {
-            s0[k] = (_Float16)(-2.0f * (float)hi);
-            s1[k] = (_Float16)(-2.0f * (float)lo);
-        } else {
-            s0[k] = hi;
-            s1[k] = lo;
-        }
-    }
-    auto frag = [&](int g) {  // compile-time g after unrolling
-        f16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            _Float16 v = (_Float16)0.0f;
-            const int k0 = 8 * (g % G) + j;
-            if (g < G) v = k0 < D ? s0[k0 < D ? k0 : 0] : (_Float16)0.0f;
-            else if (g < 2 * G) v = k0 < D ? s1[k0 < D ? k0 : 0] : (_Float16)0.0f;
-            else if (g == 2 * G) {
-                if (j < 3) v = role == 0 ? np[j] : cval;
-                else if (j < 6) v = role == 0 ? cval : np[j - 3];
-            }
-            o[j] = v;
-        }
-        return o;
-    };
-    f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NM * 64 + l;
-#pragma unroll
-    for (int c = 0; c < NM; ++c) {
-        const f16x8 a = frag(2 * c), b = frag(2 * c + 1);
-        dst[(size_t)c * 64] = h ? b : a;
-    }
-    // the pair's max norm: one atomic per WORKGROUP.  The P words share a few
-    // cache lines, and one atomic per wave (256 per cloud) serialised at the
-    // L2: ~80 us per launch whatever the batch.  Max of the bit patterns: the
-    // same word per-lane atomics would leave, NaN included.
-    const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
-    if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
-    unsigned rb = __float_as_uint(r);
-#pragma unroll
-    for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
     __shared__ unsigned wmax[4];
-    if (l == 0) wmax[w] = rb;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-        if (m != 0u) atomicMax(nmax + p, m);
-    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + w;  // ntiles is a multiple of 8 (host pads)
+    const float lim = __builtin_ldexpf(1.0f, sp.T);
+    pack_pairs(pc, sp.T, [&](int p, float s, bool check) {
+        const int cnt = count_of(n, p, Nmax);
+        const int nrows = min(max(cnt - t * 32, 0), 32);
+        const int rr = l & 31, h = l >> 5;
+        const bool valid = rr < nrows;
+        float x[D];
+        if (valid) {
+            const float4 *row = reinterpret_cast<const float4 *>(X + ((size_t)p * Nmax + (size_t)t * 32 + rr) * D);
+#pragma unroll
+            for (int q = 0; q < D / 4; ++q) {
+                const float4 v = row[q];
+                x[4 * q] = v.x * s; x[4 * q + 1] = v.y * s; x[4 * q + 2] = v.z * s; x[4 * q + 3] = v.w * s;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) x[k] = 0.0f;
+        }
+        if (check) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < D; ++k) ok = ok && __builtin_fabsf(x[k]) < lim;  // NaN / inf: not ok
+            if (!ok) pc.bad[p] = 1;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const double v = (double)x[k];
+            acc = acc + v * v;
+        }
+        _Float16 np[3];
+        if (valid) {
+            double wv = acc * __builtin_ldexp(1.0, -sp.cs);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                np[q] = (_Float16)(float)wv;
+                wv = wv - (double)np[q];
+            }
+        } else {
+            np[0] = (_Float16)65504.0f;
+            np[1] = (_Float16)65504.0f;
+            np[2] = (_Float16)65504.0f;
+        }
+        const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, sp.cs);
+        _Float16 s0[D], s1[D];  // the two stored segments of this role: hi | lo
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const _Float16 hi = (_Float16)x[k];
+            const _Float16 lo = (_Float16)(x[k] - (float)hi);
+            if (role == 0) {
+                s0[k] = (_Float16)(-2.0f * (float)hi);
+                s1[k] = (_Float16)(-2.0f * (float)lo);
+            } else {
+                s0[k] = hi;
+                s1[k] = lo;
+            }
+        }
+        auto frag = [&](int g) {  // compile-time g after unrolling
+            f16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                _Float16 v = (_Float16)0.0f;
+                const int k0 = 8 * (g % G) + j;
+                if (g < G) v = k0 < D ? s0[k0 < D ? k0 : 0] : (_Float16)0.0f;
+                else if (g < 2 * G) v = k0 < D ? s1[k0 < D ? k0 : 0] : (_Float16)0.0f;
+                else if (g == 2 * G) {
+                    if (j < 3) v = role == 0 ? np[j] : cval;
+                    else if (j < 6) v = role == 0 ? cval : np[j - 3];
+                    else if (j == 6 && role == 1) v = (_Float16)32768.0f;  // featnn_row8's bias
+                }
+                o[j] = v;
+            }
+            return o;
+        };
+        f16x8 *dst = Xp + ((size_t)p * ntiles + t) * NM * 64 + l;
+#pragma unroll
+        for (int c = 0; c < NM; ++c) {
+            const f16x8 a = frag(2 * c), b = frag(2 * c + 1);
+            dst[(size_t)c * 64] = h ? b : a;
+        }
+        // the pair's max norm: one atomic per WORKGROUP (see feat_pack5)
+        const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
+        if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+        unsigned rb = __float_as_uint(r);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
+        if (l == 0) wmax[w] = rb;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            if (m != 0u) atomicMax(nmax + p, m);
+        }
+    });
 }
 
 // certification threshold for a top-2 gap in scaled units (see header)
@@ -680,7 +780,7 @@ __device__ __forceinline__ void rescan_out(const RescanArgs5 &a, int dir, int p,
                                            int bj, int32_t *nn) {
     nn[row] = (bj == 0x7fffffff) ? 0 : bj;
     if (dir == 0 && a.v12) {
-        const double sc = (double)pair_scale5(a.mx[p], a.T);
+        const double sc = (double)__uint_as_float(a.mx[p]);  // the scale the packs used
         a.v12[(size_t)p * a.Nmax + row] = best * sc * sc;
         a.e12[(size_t)p * a.Nmax + row] = 0.0f;
     }
@@ -1212,6 +1312,249 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     }
 }
 
+// Pass 1, round 5 (S <= 2): the row top-2 of TWO column tiles at a time.
+//
+// featnn_row7 spends 3 VALU per distance (code, med3, min) against 7 MFMAs per
+// 32x32 tile: 262 issue cycles per tile beside 224 of MFMA pipe, so the screen
+// was bound by SIMD issue.  Here a wave holds RT = 2 row tiles and walks the
+// LDS group in steps of two column tiles (c0, c1): each slot (row, column lane)
+// takes its pair of values (x, y) at once --
+//     t = med3(b1, x, y);  b2 = min(b2, t);  b1 = min3(b1, x, y)
+// (the second smallest of {b1, b2, x, y} is min(b2, med3(b1, x, y)) for
+// b1 <= b2) -- 2.5 VALU per distance with the tile code, 40 per tile: 226
+// issue cycles, i.e. the kernel becomes MFMA-pipe bound.  The top-2 runs on
+// the f32 BIT PATTERNS as unsigned integers (v_med3_u32 / v_min3_u32 /
+// v_min_u32: no NaN canonicalisation, no inline asm next to the accumulators):
+// that order is the float order for non-negative values, so every value is
+// shifted up by a bias B = 2^15 -- the row operand's norm chunk carries 1.0 at
+// k = 6 (patched in registers) against 2^15 in the column image's (the other
+// screens multiply it by 0) -- larger than any screen error (bound5 at the
+// split's range |x| < 2^T, D <= 32: < 29,000 in scaled units), so no screened
+// value is negative; NaN patterns sort above +inf, so NaN distances never win (as
+// in the oracle's strict <), and a pair with a non-finite value is uncertified
+// by its bound anyway.  The certification charges the bias's rounding.
+// Schedule per step, two phases of 14 MFMAs (accumulators acc[t][c]: 64 VGPRs):
+//   A: row tile 0's MFMAs | row tile 1's epilogue of the previous step
+//   B: row tile 1's MFMAs | row tile 0's epilogue of this step
+// so each phase is 14 MFMAs beside 80 VALU (5.7 per 32-cycle MFMA slot) and no
+// accumulator is double-buffered.  The step's B fragments (10 ds_read_b128)
+// open phase A, their latency covered by the epilogue's first VALU.
+// ---------------------------------------------------------------------------
+#ifndef PCR_ROW8_PIN
+#define PCR_ROW8_PIN 1
+#endif
+#ifndef PCR_ROW8_HEAD
+#define PCR_ROW8_HEAD 24  // epilogue VALU in front of phase A's first MFMA (the B reads' latency)
+#endif
+#ifndef PCR_ROW8_G
+#define PCR_ROW8_G 8      // column tiles per LDS group
+#endif
+#ifndef PCR_ROW8_PRIO
+#define PCR_ROW8_PRIO 0
+#endif
+constexpr double kRowBias = 32768.0;  // B: 1.0 (row k = 6) x 2^15 (column image k = 6)
+
+__device__ __forceinline__ unsigned umin2(unsigned a, unsigned b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned umax2(unsigned a, unsigned b) { return a > b ? a : b; }
+
+template <int S, int G>
+__global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
+    constexpr int W = 8, RT = 2;                   // waves per workgroup, row tiles per wave
+    constexpr int NX = 3 * S + 1, NM = 2 * S + 1;  // executed / stored k-chunks
+    constexpr int kB = G * NM * 64;                // f16x8 per B buffer
+    static_assert(G % 2 == 0 && S <= 2, "column tiles in pairs; two row tiles fit up to S = 2");
+    __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
+    if (p >= a.P) return;  // whole block
+    const int nr = count_of(a.n_rows, p, a.Rmax);
+    if (rb * W * RT * 32 >= nr) return;  // whole block: no rows here
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int m = count_of(a.n_cols, p, a.Cmax);
+    const int qt0 = (rb * W + wid) * RT;  // this wave's first row tile
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    const unsigned ctmask = (1u << a.ctbits) - 1u;
+    unsigned keep = ~ctmask;
+    asm("" : "+v"(keep));  // a VGPR operand: one v_and_or_b32 per code with the SGPR tile number
+    f16x8 A[RT][NM];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {  // padded row tiles (qt < ntr) hold sentinel rows
+        const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt0 + t) * NM * 64 + l;
+#pragma unroll
+        for (int c = 0; c < NM; ++c) A[t][c] = qp[(size_t)c * 64];
+        if (h == 0) A[t][NM - 1][6] = (_Float16)1.0f;  // the bias (see above)
+    }
+    unsigned b1[RT][16], b2[RT][16];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { b1[t][r] = 0x7f800000u; b2[t][r] = 0x7f800000u; }
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * NM; c += W) {
+            const f16x8 *src = bsrc + ((size_t)grp * G * NM + c) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
+        }
+    };
+    // row tile t's slots take the values of column tiles ct (x) and ct + 1 (y)
+    auto epilogue = [&](const f32x16 (&x)[2], int t, unsigned ct) {
+        asm("" : "+s"(ct));
+        const unsigned ct1 = ct + 1u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const unsigned cx = (__float_as_uint(x[0][r]) & keep) | ct;
+            const unsigned cy = (__float_as_uint(x[1][r]) & keep) | ct1;
+            // the median as v_med3_f32 (the same order on these non-negative
+            // patterns; an integer median shares min(b1, cx) with the min3
+            // below and costs a v_min more)
+            const unsigned md = __float_as_uint(
+                __builtin_amdgcn_fmed3f(__uint_as_float(b1[t][r]), __uint_as_float(cx), __uint_as_float(cy)));
+            b2[t][r] = umin2(b2[t][r], md);
+            b1[t][r] = umin2(b1[t][r], umin2(cx, cy));
+#if PCR_ROW8_PIN
+            asm("" : "+v"(b2[t][r]));  // no b2 min chain across steps (registers)
+#endif
+        }
+    };
+    f32x16 acc[RT][2];
+    // the first phase A finds a harmless pending epilogue: +inf with code 0
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[1][c][r] = __builtin_inff();
+    unsigned pend = 0u;
+    const f32x16 zero = {};
+#if PCR_ROW8_PRIO
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // the SIMD partners' later half (MI355X guide, two waves per SIMD)
+#endif
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = grp & 1;
+        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        const f16x8 *Bb = Bs + buf * kB + l;
+        // the step's B fragments, read in MFMA order (the first MFMAs wait for
+        // the first reads only): the group's first step reads them at its
+        // start, every later step at the end of the previous step's phase B
+        f16x8 Bf[2][NM];
+#pragma unroll
+        for (int c = 0; c < NM; ++c)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[(u * NM + c) * 64];
+#pragma unroll
+        for (int st = 0; st < G / 2; ++st) {
+            const unsigned ct = (unsigned)(grp * G + 2 * st);
+            // phase A
+#pragma unroll
+            for (int c = 0; c < NX; ++c)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0][amap(c, S)], Bf[u][bmap(c, S)],
+                                                                       c == 0 ? zero : acc[0][u], 0, 0, 0);
+            epilogue(acc[1], 1, pend);
+            if (st == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NM, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, PCR_ROW8_HEAD, 0);
+#pragma unroll
+            for (int i = 0; i < 2 * NX; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, (80 - PCR_ROW8_HEAD + 2 * NX - 1) / (2 * NX), 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // phase B
+#pragma unroll
+            for (int c = 0; c < NX; ++c)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[1][amap(c, S)], Bf[u][bmap(c, S)],
+                                                                       c == 0 ? zero : acc[1][u], 0, 0, 0);
+            epilogue(acc[0], 0, ct);
+            if (st + 1 < G / 2) {  // the next step's fragments, behind this phase's last MFMA
+#pragma unroll
+                for (int c = 0; c < NM; ++c)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[((2 * st + 2 + u) * NM + c) * 64];
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+            for (int i = 0; i < 2 * NX - 2; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            if (st + 1 < G / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NM, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            pend = ct;
+        }
+        // the next group's DMA has landed for every wave, and every wave is done
+        // reading this buffer before the group after next overwrites it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    epilogue(acc[1], 1, pend);
+    // Row merge through LDS (the B buffers are free): each lane stores its 16
+    // slots (b1, b2), then lane L takes row L & 31 and half of its 32 column
+    // lanes (16 entries in column order: on equal patterns -- same value, same
+    // tile code -- the lower column lane stays), and the two halves combine by
+    // one exchange.  Unsigned order = the screen's order (all values >= 0 or
+    // +inf).  Stride 17: the stores and the row reads spread over the banks.
+    uint2 *tl = reinterpret_cast<uint2 *>(Bs) + (size_t)wid * 64 * 17;
+    const int R = l & 31, hR = (R >> 2) & 1, rR = (R & 3) + 4 * (R >> 3), j0 = 16 * h;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {  // every wave runs both (the barriers), rows past nr write nothing
+        const int qt = qt0 + t;
+        __syncthreads();  // (t = 0: every wave is past its last B read; t = 1: the row reads)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tl[l * 17 + r] = make_uint2(b1[t][r], b2[t][r]);
+        __syncthreads();
+        unsigned B1 = 0x7f800000u, B2 = 0x7f800000u;
+        int jw = j0;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const uint2 e = tl[(hR * 32 + j0 + jj) * 17 + rR];
+            B2 = umin2(umin2(B2, e.y), umax2(B1, e.x));
+            const bool take = e.x < B1;
+            B1 = take ? e.x : B1;
+            jw = take ? j0 + jj : jw;
+        }
+        {   // lanes L < 32 hold column lanes 0..15: the partner's (16..31) win strictly below
+            const unsigned o1 = (unsigned)__shfl_xor((int)B1, 32, 64), o2 = (unsigned)__shfl_xor((int)B2, 32, 64);
+            const int oj = __shfl_xor(jw, 32, 64);
+            B2 = umin2(umin2(B2, o2), umax2(B1, o1));
+            const bool take = o1 < B1;
+            B1 = take ? o1 : B1;
+            jw = take ? oj : jw;
+        }
+        const float mb1 = __uint_as_float(B1), mb2 = __uint_as_float(B2);
+        const int mi1 = (int)(B1 & ctmask) * 32 + jw;
+        const int row = qt * 32 + R;
+        if (h != 0 || row >= nr) continue;
+        const size_t o = (size_t)p * a.Rmax + row;
+        if (m == 0) {
+            a.nn[o] = 0;
+            a.v[o] = __builtin_inf();
+            a.e[o] = 0.0f;
+            continue;
+        }
+        const double Gm = (double)__uint_as_float(a.cmax[p]);
+        const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+        // bound5 plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled like bound5
+        const double bnd = bound5(qn, Gm, 16 * NX, a.D) + 4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kRowBias;
+        const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
+        a.v[o] = (double)mb1 - kRowBias;  // exact (both multiples of mb1's ulp)
+        a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
+        if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)))) {
+            a.nn[o] = 0;  // the exact rescan writes it
+            a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
+        } else {
+            a.nn[o] = mi1;
+        }
+    }
+}
+
 struct MutArgs {
     const int32_t *nn12, *n_src, *n_tgt;
     int Nmax, Mmax, mutual, ransac_n, Kt, D, ntm;
@@ -1334,7 +1677,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     // row tiles, padded to whole blocks of the dual screen (8 tiles) and of the
     // row screens (8 waves x row_tiles(S) tiles; the sentinel rows are valid encodings)
     v.ntn = cdiv(cdiv(Nmax, 32), 16) * 16;
-    v.ntm = cdiv(cdiv(Mmax, 32), 8) * 8;              // column tiles, padded to whole groups (G | 8)
+    v.ntm = cdiv(cdiv(Mmax, 32), PCR_ROW8_G) * PCR_ROW8_G;  // column tiles, padded to whole groups (G | 8)
     v.ctbits = 1;
     while ((1 << v.ctbits) < std::max(v.ntm, v.ntn)) ++v.ctbits;
     PCR_REQUIRE(v.ctbits <= 16, PCR_ERR_ARG, "feature_match: N=%d / M=%d too large", Nmax, Mmax);
@@ -1342,14 +1685,14 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     const size_t ap = (size_t)P * ntn * NM * 64, bp = (size_t)P * ntm * NM * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
-        16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax) + 128 * (size_t)P);
+        16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax) + 18 * (size_t)P);
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     v.Ap = (f16x8 *)ws;
     v.Bp = v.Ap + ap;
     v.fnr = (float *)(v.Bp + bp);
     v.gnr = v.fnr + nn_n;
-    // [0,P): max|y|  [P,2P): max|x|  [2P,3P): max|elem|  [3P,4P): cnt12  [4P,5P): cnt21
+    // [0,P): max|y|  [P,2P): max|x|  [2P,3P): the scale used  [3P,4P): cnt12  [4P,5P): cnt21
     v.gmax = (unsigned *)(v.gnr + nn_m);
     v.fmax = v.gmax + P;
     v.mx = v.gmax + 2 * P;
@@ -1357,29 +1700,38 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.cnt21 = v.cnt12 + P;
     v.list12 = v.cnt21 + P;                    // per pair, stride Nmax
     v.list21 = v.list12 + (size_t)P * Nmax;    // per pair, stride Mmax
-    unsigned *mxp = (unsigned *)(v.list21 + (size_t)P * Mmax);  // [P][2][zsl <= 64] partial maxima
+    unsigned *mxp = (unsigned *)(v.list21 + (size_t)P * Mmax);  // [P][2][zr] partial maxima (repair)
+    unsigned *smax = mxp + 2 * (size_t)P * 8;                     // [P] sample maxima
+    int *bad = (int *)(smax + P);                                  // [P] repair flags
     prof_begin(s, kProfFeatPack);
-    // ~1024 blocks whatever the batch (each >= 16 KB of a cloud)
-    const long long cloud_f4 = ((long long)std::max(Nmax, Mmax) * D + 3) / 4;
-    const int zsl = (int)std::max(1LL, std::min(std::min(64LL, (cloud_f4 + 1023) / 1024),
-                                                (long long)cdiv(1024, 2 * P)));
-    hipLaunchKernelGGL(feat_maxabs, dim3(P, 2, zsl), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax,
-                       D, mxp, v.gmax, P);
+    hipLaunchKernelGGL(feat_sample, dim3(P), dim3(256), 0, s, F, n_src, Nmax, G, n_tgt, Mmax, D, smax, v.gmax,
+                       bad, P);
     PCR_LAUNCH_CHECK();
-    if (D == 32) {  // the hot shape: register-resident pack
-        hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax,
-                           ntn, 0, v.sp, mxp, zsl, v.mx, v.Ap, v.fnr, v.fmax);
-        PCR_LAUNCH_CHECK();
-        hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax,
-                           ntm, 1, v.sp, mxp, zsl, v.mx, v.Bp, v.gnr, v.gmax);
-        PCR_LAUNCH_CHECK();
-    } else {
-        hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), P), dim3(256), 0, s, F, n_src, Nmax, D,
-                           v.S, ntn, 0, v.sp, mxp, zsl, v.mx, v.Ap, v.fnr, v.fmax);
-        PCR_LAUNCH_CHECK();
-        hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), P), dim3(256), 0, s, G, n_tgt, Mmax, D,
-                           v.S, ntm, 1, v.sp, mxp, zsl, v.mx, v.Bp, v.gnr, v.gmax);
-        PCR_LAUNCH_CHECK();
+    // the repair passes: few blocks walking the flags (empty in the common case)
+    const int R = std::min(P, kRepairR), zr = 8;
+    for (int rep = 0; rep < 2; ++rep) {
+        PackCtl pc{smax, mxp, zr, P, rep, bad, v.mx};
+        if (rep) {
+            hipLaunchKernelGGL(feat_maxabs, dim3(R, 2, zr), dim3(1024), 0, s, F, n_src, Nmax, G, n_tgt, Mmax, D,
+                               mxp, v.gmax, bad, P);
+            PCR_LAUNCH_CHECK();
+        }
+        const int gy = rep ? R : P;
+        if (D == 32) {  // the hot shape: register-resident pack
+            hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntn, 4), gy), dim3(256), 0, s, F, n_src, Nmax,
+                               ntn, 0, v.sp, pc, v.Ap, v.fnr, v.fmax);
+            PCR_LAUNCH_CHECK();
+            hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntm, 4), gy), dim3(256), 0, s, G, n_tgt, Mmax,
+                               ntm, 1, v.sp, pc, v.Bp, v.gnr, v.gmax);
+            PCR_LAUNCH_CHECK();
+        } else {
+            hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), gy), dim3(256), 0, s, F, n_src, Nmax, D,
+                               v.S, ntn, 0, v.sp, pc, v.Ap, v.fnr, v.fmax);
+            PCR_LAUNCH_CHECK();
+            hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), gy), dim3(256), 0, s, G, n_tgt, Mmax, D,
+                               v.S, ntm, 1, v.sp, pc, v.Bp, v.gnr, v.gmax);
+            PCR_LAUNCH_CHECK();
+        }
     }
     prof_end(s, kProfFeatPack);
     return PCR_OK;
@@ -1596,8 +1948,17 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.w1 = nullptr; r.w2 = nullptr;
     if (prep_event && prep_at == 2) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
     prof_begin(s, kProfFeatScreen);
-    rc = launch_row7<true>(r, v.S, s, rt1);
-    if (rc != PCR_OK) return rc;
+    if (v.S <= 2) {  // two column tiles per step (featnn_row8)
+        r.nrb = cdiv(cdiv(Nmax, 32), v.W * 2);
+        const long long nblk = 8LL * r.nrb * cdiv(P, 8);  // XCD-aware 1-D grid
+        PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
+        if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, PCR_ROW8_G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        else hipLaunchKernelGGL((featnn_row8<2, PCR_ROW8_G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        PCR_LAUNCH_CHECK();
+    } else {
+        rc = launch_row7<true>(r, v.S, s, rt1);
+        if (rc != PCR_OK) return rc;
+    }
     prof_end(s, kProfFeatScreen);
     if (prep_event && prep_at == 1) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
     RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);

@@ -472,6 +472,10 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     }
 }
 
+// set while an ICP call's launches are being issued: a call that returned an
+// error in between leaves it set, and the next call re-zeroes the barrier slot
+thread_local bool t_icp_failed = false;
+
 const void *icp_fn(bool lds) {
     return lds ? (const void *)icp_kernel<true> : (const void *)icp_kernel<false>;
 }
@@ -544,16 +548,10 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     // launch).  The sums are exact, so G changes no bit.
     const char *tail_env = getenv("PCR_ICP_TAIL");
     const bool tail_on = !(tail_env && atoi(tail_env) == 0);
-    int ncu = kCUs;
-    {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-            ncu = v;
-        else
-            (void)hipGetLastError();
-    }
-    const int grid2 = per_cu > 0 ? per_cu * ncu : 0;
+    // phase 2 is sized like coop_groups' grids: this launch's share of the chip
+    // when pcr_set_concurrency(k) lets k launches run at once, so concurrent
+    // phase-2 grids are all resident together (their pair barriers spin)
+    const int grid2 = coop_capacity(per_cu);
     const bool two_phase = tail_on && a.G == 1 && a.d > 0.0 && Nmax > 0 && grid2 >= 4 && P >= grid2 / 2;
     if (two_phase) a.thr_active = grid2 / 4;  // phase 2: >= 4 workgroups per listed pair
     // working copy, by position
@@ -574,10 +572,13 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         // fits the zeroed range or outgrows the slot's headroom (fresh, zeroed)
         size_t nb = 16384;
         while (nb < 4 * (size_t)P) nb <<= 1;
+        // A launch that failed after some of its workgroups arrived could leave
+        // arrivals or counters behind: the call after any failed one re-zeroes.
         bool fresh = false;
         a.bar = (unsigned *)workspace(39, sizeof(unsigned) * nb, &fresh);
         PCR_REQUIRE(a.bar, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
-        if (fresh) PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * nb, s));
+        if (fresh || t_icp_failed) PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * nb, s));
+        t_icp_failed = false;
         a.chunk = (int *)(a.bar + 2);
     } else {
         a.part = nullptr;
@@ -601,6 +602,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         PCR_HIP_CHECK(hipMemsetAsync(a.ctl + 1, 0, sizeof(int), s));  // none listed
     }
     prof_begin(s, kProfIcp);
+    t_icp_failed = true;  // until every launch below went in
     if (!two_phase) {
         void *args[] = {&a};
         PCR_HIP_CHECK(coop_launch(fn, P, a.G, kThreads, args, sm, s));
@@ -618,6 +620,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         PCR_HIP_CHECK(hipLaunchCooperativeKernel(fn, dim3(grid2), dim3(kThreads), args, (unsigned)sm, s));
         PCR_LAUNCH_CHECK();
     }
+    t_icp_failed = false;
     prof_end(s, kProfIcp);
     if (want_timing) {  // debug: phase split in shader clocks, mean over pairs, to stderr
         std::vector<unsigned long long> h(8 * (size_t)P);

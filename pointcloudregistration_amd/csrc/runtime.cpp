@@ -124,6 +124,16 @@ int coop_groups(int P, int per_cu, int gmax) {
     return (int)(g > gmax ? gmax : g);
 }
 
+int coop_capacity(int per_cu) {
+    int dev = 0, cus = 0;
+    if (per_cu <= 0 || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return per_cu * cus / (g_conc > 1 ? g_conc : 1);
+}
+
 hipError_t coop_launch(const void *fn, int P, int G, int threads, void **args, size_t lds,
                        hipStream_t s) {
     if (G <= 1) return hipLaunchKernel(fn, dim3(P), dim3(threads), args, lds, s);
@@ -279,6 +289,9 @@ extern "C" int pcr_shutdown(void) {
     }
     {
         std::lock_guard<std::mutex> lk(pcr::g_mu);
+        // a device that cannot be synchronised may still run work on its
+        // buffers: its slots and retired buffers are kept
+        bool unsynced[pcr::kMaxDevices] = {};
         for (int dev = 0; dev < pcr::kMaxDevices; ++dev) {
             bool any = false;
             for (auto &ctx : pcr::g_slots[dev])
@@ -289,6 +302,7 @@ extern "C" int pcr_shutdown(void) {
                 (void)hipGetLastError();
                 pcr::set_error("shutdown: device %d not synchronisable", dev);
                 rc = PCR_ERR_HIP;
+                unsynced[dev] = true;
                 continue;
             }
             for (auto &ctx : pcr::g_slots[dev])
@@ -311,7 +325,7 @@ extern "C" int pcr_shutdown(void) {
             }
         std::vector<std::pair<int, void *>> keep;
         for (auto &r : pcr::g_retired) {
-            if (hipSetDevice(r.first) == hipSuccess) (void)hipFree(r.second);
+            if (!unsynced[r.first] && hipSetDevice(r.first) == hipSuccess) (void)hipFree(r.second);
             else keep.push_back(r);
         }
         pcr::g_retired.swap(keep);

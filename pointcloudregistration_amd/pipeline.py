@@ -69,6 +69,7 @@ class PairPipeline:
         # cooperative launches run slower -- off by default
         self.use_graph = bool(graph)
         self._graph = None
+        self._graph_gen = -1
         self._graph_failed = False
         # libpcr workspace context (pcr_set_workspace_context): pipelines whose
         # steps run concurrently on different streams need different ones
@@ -146,6 +147,7 @@ class PairPipeline:
             return
         cur.wait_stream(side)
         self._graph = g
+        self._graph_gen = _lib.generation()
 
     def _publish(self, rr, ir, ncor, corres, nn12):
         chamfer = self.rec[:, 36]
@@ -160,6 +162,8 @@ class PairPipeline:
         if not time_stages:
             # the whole step in one host call, no round trip (csrc/pipeline.cpp)
             with torch.cuda.device(self.device):
+                if self._graph is not None and self._graph_gen != _lib.generation():
+                    self._graph = None  # pcr_shutdown freed the buffers it recorded
                 if self.use_graph and self._graph is None and not self._graph_failed:
                     self._capture()
                 if self.use_graph and self._graph is not None:

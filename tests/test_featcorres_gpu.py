@@ -54,6 +54,23 @@ def _cases():
     c["nan_rows"] = (a, b)
     c["subnormal"] = ((rng.standard_normal((300, 16)) * 1e-39).astype(np.float32),
                       (rng.standard_normal((280, 16)) * 1e-39).astype(np.float32))
+    # the packs' speculative scale (feat_sample: the first 64 rows' max with one
+    # binade of headroom): a tail far above the sample takes the repair path,
+    # one far below it only loses precision; NaN / inf past the sample
+    a = rng.standard_normal((700, 32)).astype(np.float32)
+    b = rng.standard_normal((650, 32)).astype(np.float32)
+    a[:80] *= np.float32(1e-3)
+    b[:65] *= np.float32(1e-3)
+    c["tail_above_sample"] = (a, b)
+    a = rng.standard_normal((700, 32)).astype(np.float32)
+    b = rng.standard_normal((650, 32)).astype(np.float32)
+    a[:32] *= np.float32(1e4)
+    c["tail_below_sample"] = (a, b)
+    a = rng.standard_normal((600, 32)).astype(np.float32)
+    b = rng.standard_normal((500, 32)).astype(np.float32)
+    a[400, 7] = np.nan
+    b[300, 1] = np.inf
+    c["nonfinite_past_sample"] = (a, b)
     c["d1"] = (rng.standard_normal((513, 1)).astype(np.float32),
                rng.standard_normal((300, 1)).astype(np.float32))
     c["d33_small"] = (rng.standard_normal((40, 33)).astype(np.float32),
@@ -103,5 +120,28 @@ def test_feature_correspondences_ragged_many_pairs(oracle):
         e12 = oracle.featnn(f, g)
         exp = oracle.corres(e12, oracle.featnn(g, f), True, 3)
         assert np.array_equal(_np(nn12)[p, :ns[p]], e12), p
+        assert int(_np(nc)[p]) == len(exp), p
+        assert np.array_equal(_np(co)[p, :len(exp)], exp), p
+
+
+@pytest.mark.parametrize("d", [32, 24])
+def test_feature_correspondences_repair_mixed_batch(oracle, d):
+    """20 pairs, 11 of them with rows far above their sample's range (the packs'
+    repair path: flagged pairs by rank over kRepairR blocks, ranks past 8
+    included), D = 32 (register pack) and 24 (LDS pack): every pair equals the
+    oracle."""
+    P, N, M = 20, 400, 380
+    rng = np.random.default_rng(9)
+    fs = rng.standard_normal((P, N, d)).astype(np.float32)
+    ft = rng.standard_normal((P, M, d)).astype(np.float32)
+    flagged = [0, 2, 3, 5, 8, 9, 11, 13, 16, 18, 19]
+    for p in flagged:
+        fs[p, 64 + p:] *= np.float32(200.0) if p % 2 else np.float32(1.0)
+        ft[p, 100:] *= np.float32(300.0)
+    co, nc, nn12 = reg.feature_correspondences(fs, ft)
+    for p in range(P):
+        e12 = oracle.featnn(fs[p], ft[p])
+        exp = oracle.corres(e12, oracle.featnn(ft[p], fs[p]), True, 3)
+        assert np.array_equal(_np(nn12)[p], e12), p
         assert int(_np(nc)[p]) == len(exp), p
         assert np.array_equal(_np(co)[p, :len(exp)], exp), p

@@ -1,4 +1,4 @@
-# Round 4 evidence for profiles/r04/ (TAG=vN; the profiled runs with
+# Round evidence for profiles/rNN/ (ROUND=r05 TAG=vN; the profiled runs with
 # PCR_ICP_TAIL=0: ICP's second, cooperative launch makes the process fault at
 # exit under rocprofv3): the -m gpu suite, smoke, the
 # default bench line (all legs), the 32 / 64-pair shards, the kernel stats of the
@@ -6,8 +6,8 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-V=${TAG:-v1}
-T=gpurun_out/r04final_$V
+V=${TAG:-v1}; R=${ROUND:-r05}
+T=gpurun_out/${R}final_$V
 mkdir -p $T
 timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $T/pytest_gpu.txt 2>&1
 rc=$?; echo "pytest rc $rc"; tail -2 $T/pytest_gpu.txt
@@ -25,5 +25,5 @@ rc=$?; echo "rocprof stats rc $rc"
 case $rc in 124|134|137) exit 15;; esac
 bash tools/pmc_traffic.sh $T/traffic > $T/traffic.txt 2>&1; echo "traffic rc $?"
 bash tools/pmc_sq.sh $T/sq > $T/sq.txt 2>&1; echo "sq rc $?"
-TAG=r04final_${V}_f4 bash tools/gpu_f4_prof.sh > $T/f4.txt 2>&1; echo "f4 prof rc $?"
+TAG=${R}final_${V}_f4 bash tools/gpu_f4_prof.sh > $T/f4.txt 2>&1; echo "f4 prof rc $?"
 tail -3 $T/f4.txt
