@@ -1008,9 +1008,65 @@ struct RowArgs5 {
     double *v;
     float *e;
     int *list, *count;
-    float *w1, *w2;             // pass 2: top-2 values by original row index
+    float4 *wq;                 // pass 2: (top-2 values, the screen's error bound, -) by original row index
     const float *Fr, *Gc;       // pass 1: the f32 rows / columns (the winner's tile in its group)
+    // pass 2: the gathered rows built in registers from the f32 cloud (one
+    // 128-byte row per lane instead of ten 16-byte pieces in ten lines of the
+    // packed image), with the scale the packs used and the image's role
+    const float *Xr;
+    const unsigned *sc;
+    int role, cs;
 };
+
+// One row's operand fragments exactly as feat_pack5 / feat_pack5r store them
+// (same scale, same operations in the same order), for lane half h: x the
+// row's f32 values (DV >= D, zero beyond D).
+template <int S>
+__device__ __forceinline__ void row_frags(const float *x, int D, int h, int role, int cs,
+                                          f16x8 (&out)[2 * S + 1]) {
+    constexpr int DV = 16 * S;
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < DV; ++k)
+        if (k < D) {
+            const double v = (double)x[k];
+            acc = acc + v * v;
+        }
+    _Float16 np[3];
+    double wv = acc * __builtin_ldexp(1.0, -cs);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        np[q] = (_Float16)(float)wv;
+        wv = wv - (double)np[q];
+    }
+    const _Float16 cval = (_Float16)__builtin_ldexpf(1.0f, cs);
+    _Float16 s0[DV], s1[DV];
+#pragma unroll
+    for (int k = 0; k < DV; ++k) {
+        const _Float16 hi = (_Float16)x[k];
+        const _Float16 lo = (_Float16)(x[k] - (float)hi);
+        s0[k] = role == 0 ? (_Float16)(-2.0f * (float)hi) : hi;
+        s1[k] = role == 0 ? (_Float16)(-2.0f * (float)lo) : lo;
+    }
+#pragma unroll
+    for (int c = 0; c < 2 * S + 1; ++c) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            _Float16 v0 = (_Float16)0.0f, v1 = (_Float16)0.0f;  // lane halves 0 / 1
+            if (c < 2 * S) {
+                const int k0 = 16 * (c % S) + j;
+                const _Float16 *sg = c < S ? s0 : s1;
+                v0 = k0 < D ? sg[k0] : (_Float16)0.0f;
+                v1 = k0 + 8 < D ? sg[k0 + 8] : (_Float16)0.0f;
+            } else {
+                if (j < 3) v0 = role == 0 ? np[j] : cval;
+                else if (j < 6) v0 = role == 0 ? cval : np[j - 3];
+                else if (j == 6 && role == 1) v0 = (_Float16)32768.0f;  // featnn_row8's bias
+            }
+            out[c][j] = h ? v1 : v0;
+        }
+    }
+}
 
 // RT row tiles per wave share every B fragment read (two MFMAs per ds_read):
 // a workgroup covers 8 * RT * 32 rows per pass over the pair's column stream,
@@ -1057,7 +1113,23 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         const int qt = qt0 + t;
         if (a.rlist) {  // gathered rows: lane l holds row slot qt*32 + (l & 31), half h
             const int k = qt * 32 + (l & 31);
-            if (k < nr) {
+            if (k < nr && a.Xr) {
+                const int j = a.rlist[(size_t)p * a.Rmax + k];
+                const float *xr = a.Xr + ((size_t)p * a.Rmax + j) * a.D;
+                const float sc = __uint_as_float(a.sc[p]);
+                float x[16 * S];
+                if (a.D == 16 * S && ((uintptr_t)xr & 15) == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4 * S; ++q) {
+                        const float4 v = reinterpret_cast<const float4 *>(xr)[q];
+                        x[4 * q] = v.x * sc; x[4 * q + 1] = v.y * sc; x[4 * q + 2] = v.z * sc; x[4 * q + 3] = v.w * sc;
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 16 * S; ++q) x[q] = q < a.D ? xr[q] * sc : 0.0f;
+                }
+                row_frags<S>(x, a.D, h, a.role, a.cs, A[t]);
+            } else if (k < nr) {
                 const int j = a.rlist[(size_t)p * a.Rmax + k];
                 const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + (j >> 5)) * NM * 64 + (j & 31) + 32 * h;
 #pragma unroll
@@ -1306,8 +1378,13 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             const int k = qt * 32 + (lr & 3) + 8 * (lr >> 2) + 4 * h;
             if (lr >= 16 || k >= nr) continue;
             const int j = a.rlist[(size_t)p * a.Rmax + k];
-            a.w1[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb1;
-            a.w2[(size_t)p * a.Rmax + j] = m == 0 ? __builtin_inff() : mb2;
+            // the row's bound beside its values: featmut_resolve gathers one
+            // 16-byte record per candidate (rounded up: a bound stays a bound)
+            const double e2 = 0.5 * bound5((double)a.rnr[(size_t)p * a.ntr * 32 + j],
+                                           (double)__uint_as_float(a.cmax[p]), 16 * NX, a.D);
+            a.wq[(size_t)p * a.Rmax + j] = make_float4(m == 0 ? __builtin_inff() : mb1,
+                                                       m == 0 ? __builtin_inff() : mb2,
+                                                       (float)(e2 * (1.0 + 1e-6)), 0.0f);
         }
     }
 }
@@ -1377,13 +1454,32 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     const unsigned ctmask = (1u << a.ctbits) - 1u;
     unsigned keep = ~ctmask;
     asm("" : "+v"(keep));  // a VGPR operand: one v_and_or_b32 per code with the SGPR tile number
+    // the row operand built from the f32 rows (one 128-byte row per lane, the
+    // operands exactly as the pack stores them: the packed row image is not read)
     f16x8 A[RT][NM];
+    {
+        const float sc = __uint_as_float(a.sc[p]);
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {  // padded row tiles (qt < ntr) hold sentinel rows
-        const f16x8 *qp = a.Ap + ((size_t)p * a.ntr + qt0 + t) * NM * 64 + l;
+        for (int t = 0; t < RT; ++t) {
+            const int row = (qt0 + t) * 32 + (l & 31);
+            float x[16 * S];
+            const float *xr = a.Xr + ((size_t)p * a.Rmax + row) * a.D;
+            if (row < nr && a.D == 16 * S && ((uintptr_t)xr & 15) == 0) {
 #pragma unroll
-        for (int c = 0; c < NM; ++c) A[t][c] = qp[(size_t)c * 64];
-        if (h == 0) A[t][NM - 1][6] = (_Float16)1.0f;  // the bias (see above)
+                for (int q = 0; q < 4 * S; ++q) {
+                    const float4 v = reinterpret_cast<const float4 *>(xr)[q];
+                    x[4 * q] = v.x * sc; x[4 * q + 1] = v.y * sc; x[4 * q + 2] = v.z * sc; x[4 * q + 3] = v.w * sc;
+                }
+            } else if (row < nr) {
+#pragma unroll
+                for (int q = 0; q < 16 * S; ++q) x[q] = q < a.D ? xr[q] * sc : 0.0f;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16 * S; ++q) x[q] = 0.0f;  // rows past the count write nothing
+            }
+            row_frags<S>(x, a.D, h, 0, a.cs, A[t]);
+            if (h == 0) A[t][NM - 1][6] = (_Float16)1.0f;  // the bias (see above)
+        }
     }
     unsigned b1[RT][16], b2[RT][16];
 #pragma unroll
@@ -1563,7 +1659,7 @@ struct MutArgs {
     int *jlist, *nj;  // [P][Mmax], [P]: the rows of pass 2, ascending
     const double *v12;
     const float *e12;
-    const float *w1, *w2, *gnr;
+    const float4 *wq;
     const unsigned *fmax;
     int *flag;        // [P][Nmax + 1]: mutual 0 / 1, 2 = decided by the exact column
     int *list21, *cnt21;
@@ -1604,9 +1700,8 @@ __global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
     int f = 0;
     if (j >= 0 && j < m) {
         const size_t oj = (size_t)p * a.Mmax + j, oi = (size_t)p * a.Nmax + i;
-        const double w1 = (double)a.w1[oj], w2 = (double)a.w2[oj];
-        const double e2 = 0.5 * bound5((double)a.gnr[(size_t)p * a.ntm * 32 + j],
-                                       (double)__uint_as_float(a.fmax[p]), a.Kt, a.D);
+        const float4 q = a.wq[oj];
+        const double w1 = (double)q.x, w2 = (double)q.y, e2 = (double)q.z;
         const double vi = a.v12[oi], e1 = (double)a.e12[oi];
         // slack: the f64 sums of a rescanned value vs the exact real distance
         const double sl = 1e-9 * (__builtin_fabs(w1) + __builtin_fabs(vi));
@@ -1903,18 +1998,18 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     int rc = v5_prepare(F, G, P, Nmax, Mmax, D, n_src, n_tgt, s, v);
     if (rc != PCR_OK) return rc;
     const int ntn = v.ntn, ntm = v.ntm;
-    // scratch: v12 [P][Nmax] f64 | e12 [P][Nmax] f32 | w1, w2 [P][Mmax] f32 | used, pos
+    // scratch: v12 [P][Nmax] f64 | e12 [P][Nmax] f32 | wq [P][Mmax] float4 | used, pos
     // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P]
     const size_t pn = (size_t)P * Nmax, pm = (size_t)P * Mmax;
-    const size_t bytes = 8 * pn + 4 * pn + 8 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P;
+    const size_t bytes = 8 * pn + 4 * pn + 16 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P + 16;
     bool fresh = false;
     char *ws = (char *)workspace(33, bytes + 256, &fresh);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
     MutArgs ma;
     double *v12 = (double *)ws;
     float *e12 = (float *)(v12 + pn);
-    float *w1 = e12 + pn, *w2 = w1 + pm;
-    ma.used = (int *)(w2 + pm);
+    float4 *wq = reinterpret_cast<float4 *>(((uintptr_t)(e12 + pn) + 15) & ~(uintptr_t)15);
+    ma.used = (int *)(wq + pm);
     ma.pos = ma.used + pm + P;
     ma.jlist = ma.pos + pm + P;
     int *nn21x = ma.jlist + pm;
@@ -1932,7 +2027,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     }
     ma.nn12 = nn12; ma.n_src = n_src; ma.n_tgt = n_tgt; ma.Nmax = Nmax; ma.Mmax = Mmax;
     ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * v.NX; ma.D = D; ma.ntm = ntm;
-    ma.v12 = v12; ma.e12 = e12; ma.w1 = w1; ma.w2 = w2; ma.gnr = v.gnr; ma.fmax = v.fmax;
+    ma.v12 = v12; ma.e12 = e12; ma.wq = wq; ma.fmax = v.fmax;
     ma.list21 = v.list21; ma.cnt21 = v.cnt21; ma.nn21x = nn21x;
     ma.corres = corres; ma.n_corres = n_corres;
     // pass 1: F rows x all G columns
@@ -1945,7 +2040,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     while ((1 << r.ctbits) < (PCR_ROW_TILECODE ? ntm : cdiv(ntm, row_group(v.S)))) ++r.ctbits;
     r.Fr = F; r.Gc = G;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
-    r.w1 = nullptr; r.w2 = nullptr;
+    r.wq = nullptr;
+    r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
     if (prep_event && prep_at == 2) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
     prof_begin(s, kProfFeatScreen);
     if (v.S <= 2) {  // two column tiles per step (featnn_row8)
@@ -1978,7 +2074,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         const int rt2 = pass_tiles(v.S, true);
         r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * rt2);
         r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
-        r2.w1 = w1; r2.w2 = w2;
+        r2.wq = wq;
+        r2.Xr = G; r2.sc = v.mx; r2.role = 1; r2.cs = v.sp.cs;
         prof_begin(s, kProfFeatScreen2);
         rc = launch_row7<false>(r2, v.S, s, rt2);
         if (rc != PCR_OK) return rc;
@@ -2072,7 +2169,7 @@ extern "C" int pcr_feature_correspondences(const float *src_feat, const float *t
                                     ransac_n, nn12, corres, n_corres, s);
 }
 
-// debug: copy the mutual path's scratch (v12 | e12 | w1 | w2 | used | pos | jlist |
+// debug: copy the mutual path's scratch (v12 | e12 | wq (16-B aligned) | used | pos | jlist |
 // nn21x | flag | nj, feature_corres_v5's layout) of the last call to dst
 extern "C" int pcr_featmut_debug_copy(void *dst, int64_t bytes, pcr_stream_t stream) {
     pcr::clear_error();
