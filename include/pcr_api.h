@@ -56,6 +56,10 @@ int pcr_shutdown(void);
  * to CUs / k and k of them can be resident at once. */
 int pcr_set_workspace_context(int32_t ctx);
 int pcr_set_concurrency(int32_t k);
+/* Diagnostics: one trivial launch of `blocks` (1..256) 256-thread blocks,
+ * cooperative or plain, writing out[b] = b -- nothing else of the library
+ * (tools/exit_probe.py isolates an exit-time fault under the profiler). */
+int pcr_coop_probe(int32_t *out, int32_t blocks, int32_t cooperative, pcr_stream_t stream);
 
 /* Optional per-kernel timing with HIP events recorded on the launch stream
  * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,

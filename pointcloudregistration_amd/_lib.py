@@ -86,6 +86,7 @@ SIGNATURES = {
     "pcr_adam_masked": [_p, _i32, _i32, _p, _f64, _f64, _f64, _f64, _p],
     "pcr_set_gate": [_p],
     "pcr_featmut_debug_copy": [_p, _i64, _p],
+    "pcr_coop_probe": [_p, _i32, _i32, _p],
     "pcr_ndp_train_forward": [_p, _p],
     "pcr_ndp_train_backward": [_p, _p, _i32, _p, _p],
     "pcr_ndp_chamfer_glue": [_p, _i32, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _p, _p, _i32, _p],
