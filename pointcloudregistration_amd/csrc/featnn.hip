@@ -249,6 +249,16 @@ struct PackCtl {
     unsigned *sc;          // [P] the scale used (f32 bits), for the rescans
 };
 
+// both clouds in one launch: blockIdx.z = role (0: F as rows, 1: G as columns)
+struct PackIO {
+    const float *X[2];
+    const int32_t *n[2];
+    int Nmax[2], ntiles[2];
+    f16x8 *Xp[2];
+    float *nrm[2];
+    unsigned *nmax[2];
+};
+
 template <class Body>
 __device__ __forceinline__ void pack_pairs(const PackCtl &c, int T, Body body) {
     if (!c.repair) {
@@ -269,9 +279,15 @@ __device__ __forceinline__ void pack_pairs(const PackCtl &c, int T, Body body) {
 // role 0: rows (A), role 1: columns (B).  256-thread blocks, one wave per
 // 32-row tile; each tile is staged through LDS with coalesced loads (scaled,
 // exact) and every lane emits its 2S + 1 stored 16-byte operand fragments.
-__global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t *n, int Nmax, int D,
-                                                  int S, int ntiles, int role, Split5 sp, PackCtl pc,
-                                                  f16x8 *Xp, float *nrm, unsigned *nmax) {
+__global__ __launch_bounds__(256) void feat_pack5(PackIO io, int D, int S, Split5 sp, PackCtl pc) {
+    const int role = blockIdx.z;
+    const float *X = io.X[role];
+    const int32_t *n = io.n[role];
+    const int Nmax = io.Nmax[role], ntiles = io.ntiles[role];
+    f16x8 *Xp = io.Xp[role];
+    float *nrm = io.nrm[role];
+    unsigned *nmax = io.nmax[role];
+    if ((int)blockIdx.x * 4 >= ntiles) return;  // whole block: the other cloud has more tiles
     __shared__ float xs[4][32][65];  // D <= 64 (+1 pad: conflict-free row reads)
     __shared__ unsigned wmax[4];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -368,9 +384,15 @@ __global__ __launch_bounds__(256) void feat_pack5(const float *X, const int32_t 
 // lane's half -- no LDS, no per-half segment arithmetic.  Same values as
 // feat_pack5 (same operations, same order).
 template <int D>
-__global__ __launch_bounds__(256) void feat_pack5r(const float *X, const int32_t *n, int Nmax,
-                                                   int ntiles, int role, Split5 sp, PackCtl pc,
-                                                   f16x8 *Xp, float *nrm, unsigned *nmax) {
+__global__ __launch_bounds__(256) void feat_pack5r(PackIO io, Split5 sp, PackCtl pc) {
+    const int role = blockIdx.z;
+    const float *X = io.X[role];
+    const int32_t *n = io.n[role];
+    const int Nmax = io.Nmax[role], ntiles = io.ntiles[role];
+    f16x8 *Xp = io.Xp[role];
+    float *nrm = io.nrm[role];
+    unsigned *nmax = io.nmax[role];
+    if ((int)blockIdx.x * 4 >= ntiles) return;  // whole block: the other cloud has more tiles
     constexpr int S = (D + 15) / 16;  // chunks per segment
     constexpr int NM = 2 * S + 1;     // stored chunks
     constexpr int G = 2 * S;          // 8-half fragments per segment
@@ -1009,7 +1031,6 @@ struct RowArgs5 {
     float *e;
     int *list, *count;
     float4 *wq;                 // pass 2: (top-2 values, the screen's error bound, -) by original row index
-    const float *Fr, *Gc;       // pass 1: the f32 rows / columns (the winner's tile in its group)
     // pass 2: the gathered rows built in registers from the f32 cloud (one
     // 128-byte row per lane instead of ten 16-byte pieces in ten lines of the
     // packed image), with the scale the packs used and the image's role
@@ -1073,21 +1094,9 @@ __device__ __forceinline__ void row_frags(const float *x, int D, int h, int role
 // which halves the L2 -> LDS traffic at RT = 2 (at RT = 1 the stream of the
 // packed columns ran near the chip's LDS-DMA rate: waves parked ~35 %).
 //
-// Pass 1's index (round 4): the row top-2 runs on the raw values (2 VALU per
-// distance), and the index is kept per LDS GROUP of G column tiles, not per
-// tile: at the end of a group every running minimum that changed during it
-// (bits != its copy from the group start) gets the group number in its low
-// ctbits mantissa bits (4 VALU per row value per group, i.e. 0.5 per distance
-// at G = 8, against 1 per distance for the per-tile code).  After the lane
-// merge a row's minimum names (group, column lane), i.e. G candidate columns;
-// for a certified row the winner is the exact f64 argmin among those G (a
-// certified winner is the row's exact argmin, so it is the argmin of any
-// candidate set holding it).  A minimum replaced by a value with the same bits
-// keeps its older group: then the row's top-2 holds two equal values, so it
-// is uncertified and rescanned exactly.
-#ifndef PCR_ROW_TILECODE
-#define PCR_ROW_TILECODE 1  // 0: the group code (measured slower)
-#endif
+// Pass 1's index: the column-tile number packed into the low ctbits mantissa
+// bits of every value (one v_and_or) before the top-2 (featnn_row8 does the
+// same on two column tiles at a time for S <= 2).
 template <int S, int G, bool kIdx, int RT>
 __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
     constexpr int W = 8;              // waves per workgroup, RT 32-row tiles each
@@ -1147,16 +1156,10 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
         }
     }
     float b1[RT][16], b2[RT][16];
-    float s1[kIdx ? RT : 1][16];  // pass 1: b1 at the start of the current group
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { b1[t][r] = __builtin_inff(); b2[t][r] = __builtin_inff(); }
-    if constexpr (kIdx)
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s1[t][r] = __builtin_inff();
     const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
     auto issue = [&](int grp, int bufi) {
         for (int c = wid; c < G * NM; c += W) {
@@ -1181,35 +1184,14 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 float vr = acc[t][r];
-                if constexpr (kIdx && PCR_ROW_TILECODE) vr = __uint_as_float((__float_as_uint(vr) & keep_r) | ct);
+                if constexpr (kIdx) vr = __uint_as_float((__float_as_uint(vr) & keep_r) | ct);
                 b2[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], b2[t][r], vr);
                 b1[t][r] = __builtin_amdgcn_fmed3f(b1[t][r], vr, -3.40282347e+38f);
             }
     };
-    // pass 1, end of group grp: the minima that changed during it take its number
-    auto group_code = [&](unsigned grp) {
-        asm("" : "+s"(grp));
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const unsigned cur = __float_as_uint(b1[t][r]);
-                unsigned pk;  // one v_and_or (the compiler splits the expression in two)
-                asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(pk) : "v"(cur), "v"(keep_r), "s"(grp));
-                const unsigned nv = cur != __float_as_uint(s1[t][r]) ? pk : cur;
-                b1[t][r] = __uint_as_float(nv);
-                s1[t][r] = __uint_as_float(nv);
-            }
-    };
-#ifndef PCR_ROW_KV1
-#define PCR_ROW_KV1 0  // pass 1's VALU per MFMA slot (0: the epilogue's VALU spread evenly)
-#endif
-#ifndef PCR_ROW_KV2
-#define PCR_ROW_KV2 0  // the same for pass 2
-#endif
-    constexpr int kV = (kIdx && PCR_ROW_KV1 > 0)    ? PCR_ROW_KV1
-                       : (!kIdx && PCR_ROW_KV2 > 0) ? PCR_ROW_KV2
-                                                    : ((kIdx && PCR_ROW_TILECODE) ? 48 : 32) * RT / NX + 1;  // VALU per MFMA slot below
+    // VALU per MFMA slot below: the epilogue spread evenly (denser or sparser
+    // spreads measured slower in round 4)
+    constexpr int kV = (kIdx ? 48 : 32) * RT / NX + 1;
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1251,7 +1233,6 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             __builtin_amdgcn_sched_barrier(0);
         }
         epilogue(acc[(G - 1) & 1], (unsigned)(grp * G + G - 1));
-        if constexpr (kIdx && !PCR_ROW_TILECODE) group_code((unsigned)grp);
         // the next group's DMA has landed for every wave, and every wave is done
         // reading this buffer before the group after next overwrites it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1285,7 +1266,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
             const int row = qt * 32 + rin;
             const bool own = lr < 16 && row < nr;
             const size_t o = (size_t)p * a.Rmax + row;
-            int want = -1;  // certified rows: (group, column lane) of the winner
+            int want = -1;  // certified rows: the winner's column
             if (own && m == 0) {
                 a.nn[o] = 0;
                 a.v[o] = __builtin_inf();
@@ -1304,59 +1285,7 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                     want = mi1;
                 }
             }
-#if PCR_ROW_TILECODE
             if (own && want >= 0) a.nn[o] = want;
-            continue;
-#endif
-            // certified rows: the exact argmin among the G columns of the winning
-            // group in the winning lane (f64, the oracle's k order), all 64
-            // lanes at once -- lane l takes tile row l & 31 and half (l >> 5) of
-            // its G candidates, the two halves merge (lower distance, then lower
-            // index), and the row's owner lane picks the result up
-            const int R = l & 31;
-            const int w = __shfl(want, (R & 3) + 4 * (R >> 3) + 32 * ((R >> 2) & 1), 64);
-            double best = __builtin_inf();
-            int bj = 0x7fffffff;
-            if (w >= 0) {
-                const int gw = w >> 5, col = w & 31, D = a.D;
-                const float *fr = a.Fr + ((size_t)p * a.Rmax + qt * 32 + R) * D;
-                const bool v4 = (D & 3) == 0 && ((uintptr_t)a.Fr & 15) == 0 && ((uintptr_t)a.Gc & 15) == 0;
-                constexpr int kH = G / 2;
-                for (int u = (l >> 5) * kH; u < ((l >> 5) + 1) * kH; ++u) {
-                    const int j = (gw * G + u) * 32 + col;
-                    if (j >= m) break;
-                    const float *gc = a.Gc + ((size_t)p * a.Cmax + j) * D;
-                    double acc = 0.0;
-                    if (v4) {
-                        const float4 *f4 = reinterpret_cast<const float4 *>(fr);
-                        const float4 *g4 = reinterpret_cast<const float4 *>(gc);
-                        for (int k = 0; k < (D >> 2); ++k) {
-                            const float4 x = f4[k], y = g4[k];
-                            double df = (double)x.x - (double)y.x;
-                            acc = acc + df * df;
-                            df = (double)x.y - (double)y.y;
-                            acc = acc + df * df;
-                            df = (double)x.z - (double)y.z;
-                            acc = acc + df * df;
-                            df = (double)x.w - (double)y.w;
-                            acc = acc + df * df;
-                        }
-                    } else {
-                        for (int k = 0; k < D; ++k) {
-                            const double df = (double)fr[k] - (double)gc[k];
-                            acc = acc + df * df;
-                        }
-                    }
-                    if (acc < best) { best = acc; bj = j; }
-                }
-            }
-            {
-                const double ob = __shfl_xor(best, 32, 64);
-                const int oj = __shfl_xor(bj, 32, 64);
-                if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
-            }
-            const int res = __shfl(bj, rin, 64);
-            if (own && want >= 0) a.nn[o] = res;
         } else {
 #pragma unroll
             for (int o = 1; o < 32; o <<= 1) {
@@ -1417,18 +1346,8 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 // accumulator is double-buffered.  The step's B fragments (10 ds_read_b128)
 // open phase A, their latency covered by the epilogue's first VALU.
 // ---------------------------------------------------------------------------
-#ifndef PCR_ROW8_PIN
-#define PCR_ROW8_PIN 1
-#endif
-#ifndef PCR_ROW8_HEAD
-#define PCR_ROW8_HEAD 24  // epilogue VALU in front of phase A's first MFMA (the B reads' latency)
-#endif
-#ifndef PCR_ROW8_G
-#define PCR_ROW8_G 8      // column tiles per LDS group
-#endif
-#ifndef PCR_ROW8_PRIO
-#define PCR_ROW8_PRIO 0
-#endif
+constexpr int kRow8Head = 24;  // epilogue VALU in front of phase A's first MFMA (the B reads' latency)
+constexpr int kRow8G = 8;      // column tiles per LDS group (16: the whole LDS, measured no faster)
 constexpr double kRowBias = 32768.0;  // B: 1.0 (row k = 6) x 2^15 (column image k = 6)
 
 __device__ __forceinline__ unsigned umin2(unsigned a, unsigned b) { return a < b ? a : b; }
@@ -1510,9 +1429,7 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
                 __builtin_amdgcn_fmed3f(__uint_as_float(b1[t][r]), __uint_as_float(cx), __uint_as_float(cy)));
             b2[t][r] = umin2(b2[t][r], md);
             b1[t][r] = umin2(b1[t][r], umin2(cx, cy));
-#if PCR_ROW8_PIN
-            asm("" : "+v"(b2[t][r]));  // no b2 min chain across steps (registers)
-#endif
+            asm("" : "+v"(b2[t][r]));  // no b2 min chain across steps (it held 32 more VGPRs and spilled)
         }
     };
     f32x16 acc[RT][2];
@@ -1523,9 +1440,6 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         for (int r = 0; r < 16; ++r) acc[1][c][r] = __builtin_inff();
     unsigned pend = 0u;
     const f32x16 zero = {};
-#if PCR_ROW8_PRIO
-    if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // the SIMD partners' later half (MI355X guide, two waves per SIMD)
-#endif
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1553,11 +1467,11 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
                                                                        c == 0 ? zero : acc[0][u], 0, 0, 0);
             epilogue(acc[1], 1, pend);
             if (st == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NM, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, PCR_ROW8_HEAD, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, kRow8Head, 0);
 #pragma unroll
             for (int i = 0; i < 2 * NX; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, (80 - PCR_ROW8_HEAD + 2 * NX - 1) / (2 * NX), 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, (80 - kRow8Head + 2 * NX - 1) / (2 * NX), 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             // phase B
@@ -1772,7 +1686,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     // row tiles, padded to whole blocks of the dual screen (8 tiles) and of the
     // row screens (8 waves x row_tiles(S) tiles; the sentinel rows are valid encodings)
     v.ntn = cdiv(cdiv(Nmax, 32), 16) * 16;
-    v.ntm = cdiv(cdiv(Mmax, 32), PCR_ROW8_G) * PCR_ROW8_G;  // column tiles, padded to whole groups (G | 8)
+    v.ntm = cdiv(cdiv(Mmax, 32), kRow8G) * kRow8G;  // column tiles, padded to whole groups (G | 8)
     v.ctbits = 1;
     while ((1 << v.ctbits) < std::max(v.ntm, v.ntn)) ++v.ctbits;
     PCR_REQUIRE(v.ctbits <= 16, PCR_ERR_ARG, "feature_match: N=%d / M=%d too large", Nmax, Mmax);
@@ -1812,21 +1726,11 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
             PCR_LAUNCH_CHECK();
         }
         const int gy = rep ? R : P;
-        if (D == 32) {  // the hot shape: register-resident pack
-            hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntn, 4), gy), dim3(256), 0, s, F, n_src, Nmax,
-                               ntn, 0, v.sp, pc, v.Ap, v.fnr, v.fmax);
-            PCR_LAUNCH_CHECK();
-            hipLaunchKernelGGL(feat_pack5r<32>, dim3(cdiv(ntm, 4), gy), dim3(256), 0, s, G, n_tgt, Mmax,
-                               ntm, 1, v.sp, pc, v.Bp, v.gnr, v.gmax);
-            PCR_LAUNCH_CHECK();
-        } else {
-            hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntn, 4), gy), dim3(256), 0, s, F, n_src, Nmax, D,
-                               v.S, ntn, 0, v.sp, pc, v.Ap, v.fnr, v.fmax);
-            PCR_LAUNCH_CHECK();
-            hipLaunchKernelGGL(feat_pack5, dim3(cdiv(ntm, 4), gy), dim3(256), 0, s, G, n_tgt, Mmax, D,
-                               v.S, ntm, 1, v.sp, pc, v.Bp, v.gnr, v.gmax);
-            PCR_LAUNCH_CHECK();
-        }
+        PackIO io{{F, G}, {n_src, n_tgt}, {Nmax, Mmax}, {ntn, ntm}, {v.Ap, v.Bp}, {v.fnr, v.gnr}, {v.fmax, v.gmax}};
+        const dim3 grid(cdiv(std::max(ntn, ntm), 4), gy, 2);
+        if (D == 32) hipLaunchKernelGGL(feat_pack5r<32>, grid, dim3(256), 0, s, io, v.sp, pc);  // register-resident
+        else hipLaunchKernelGGL(feat_pack5, grid, dim3(256), 0, s, io, D, v.S, v.sp, pc);
+        PCR_LAUNCH_CHECK();
     }
     prof_end(s, kProfFeatPack);
     return PCR_OK;
@@ -1855,12 +1759,8 @@ static int run_rescan(RescanArgs5 &ra, int P, int D, hipStream_t s) {
     // a pair's list is short (C4: 27 rows on average, 45 at most, one or two
     // 32-row batches), so a block is a short chain of dependent candidate
     // loads and more, shorter slices finish sooner (256 pairs: 4 / 8 / 16
-    // slices 0.575 / 0.489 / 0.471 ms per step); PCR_RESCAN_S (1..16) overrides
-    int S = std::max(1, std::min(16, 4096 / std::max(P, 1)));
-    if (const char *e = getenv("PCR_RESCAN_S")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 16) S = v;
-    }
+    // slices 0.575 / 0.489 / 0.471 ms per step)
+    const int S = std::max(1, std::min(16, 4096 / std::max(P, 1)));
     if (S > 1) {
         char *rw = (char *)workspace(6, (sizeof(double) + sizeof(int)) * (size_t)P * 2 * ra.cap * S + 64);
         PCR_REQUIRE(rw, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
@@ -1955,15 +1855,10 @@ constexpr int row_tiles(int S) { return S <= 2 ? 2 : 1; }
 // column tiles per LDS group of the row screens (featnn_row7's G)
 constexpr int row_group(int S) { return S <= 2 ? 8 : 4; }
 
-// row tiles per wave of pass 1 / pass 2 at S = 2: pass 1 two (3.64 ms per
-// 256-pair launch vs 3.80 with one), pass 2 one (128 VGPRs, four waves per SIMD
-// instead of two, at twice the B-fragment reads: 1.58 vs 1.64 ms); PCR_ROW1_RT /
-// PCR_ROW2_RT = 1 or 2 override; other S: row_tiles
-static int pass_tiles(int S, bool pass2) {
-    static const int rt1 = [] { const char *e = getenv("PCR_ROW1_RT"); return e ? atoi(e) : 2; }();
-    static const int rt2 = [] { const char *e = getenv("PCR_ROW2_RT"); return e ? atoi(e) : 1; }();
-    return (S == 2 && (pass2 ? rt2 : rt1) == 1) ? 1 : row_tiles(S);
-}
+// row tiles per wave of pass 2 at S = 2: one (128 VGPRs, four waves per SIMD
+// instead of two, at twice the B-fragment reads: 1.58 vs 1.64 ms); pass 1 at
+// S <= 2 is featnn_row8; other S: row_tiles
+static int pass_tiles(int S, bool pass2) { return (S == 2 && pass2) ? 1 : row_tiles(S); }
 
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
@@ -2036,9 +1931,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.rlist = nullptr; r.rcount = nullptr; r.P = P; r.Rmax = Nmax; r.Cmax = Mmax; r.ntr = ntn;
     const int rt1 = pass_tiles(v.S, false);
     r.ntc = ntm; r.nrb = cdiv(cdiv(Nmax, 32), v.W * rt1); r.D = D; r.ctbits = 1;
-    // pass 1 codes the LDS group of column tiles (featnn_row7's G), not the tile
-    while ((1 << r.ctbits) < (PCR_ROW_TILECODE ? ntm : cdiv(ntm, row_group(v.S)))) ++r.ctbits;
-    r.Fr = F; r.Gc = G;
+    while ((1 << r.ctbits) < ntm) ++r.ctbits;
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.wq = nullptr;
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
@@ -2048,8 +1941,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         r.nrb = cdiv(cdiv(Nmax, 32), v.W * 2);
         const long long nblk = 8LL * r.nrb * cdiv(P, 8);  // XCD-aware 1-D grid
         PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
-        if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, PCR_ROW8_G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
-        else hipLaunchKernelGGL((featnn_row8<2, PCR_ROW8_G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        else hipLaunchKernelGGL((featnn_row8<2, kRow8G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
         PCR_LAUNCH_CHECK();
     } else {
         rc = launch_row7<true>(r, v.S, s, rt1);

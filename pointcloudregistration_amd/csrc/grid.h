@@ -13,20 +13,6 @@
 #include <hip/hip_runtime.h>
 #include "geom.h"
 
-// grid_query's candidate test: 0 = one 16-byte read (x, y, z, index) and the
-// f64 distance; 1 = an 8-byte read of (x, y), the f64 partial (dx^2 + dy^2) --
-// exactly the first rounded term of dist2's ((dx^2 + dy^2) + dz^2), which
-// rounding can only raise, so a partial >= thr rejects the candidate as the
-// full test would -- and (z, index) read only for the survivors
-#ifndef PCR_GQ_XY
-#define PCR_GQ_XY 0
-#endif
-// 1: candidates screened in f32 with a rigorous error bound, the f64 distance
-// computed once per query (its winner), the exact f64 walk re-run only for a
-// query with a candidate the bound cannot place (grid_query_screened)
-#ifndef PCR_GQ_F32
-#define PCR_GQ_F32 0
-#endif
 
 namespace pcr {
 
@@ -53,8 +39,6 @@ struct GridView {
         ax = v.x; ay = v.y; az = v.z; aw = v.w;
     }
     __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
-    __device__ __forceinline__ float2 load_xy(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s]; }
-    __device__ __forceinline__ float2 load_zw(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s + 1]; }
 };
 
 // LDS copy for the consumers that own a pair (RANSAC, ICP): one float4 per
@@ -72,8 +56,6 @@ struct GridP4 {
         ax = v.x; ay = v.y; az = v.z; aw = v.w;
     }
     __device__ __forceinline__ int index_of(int, float aw) const { return __float_as_int(aw); }
-    __device__ __forceinline__ float2 load_xy(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s]; }
-    __device__ __forceinline__ float2 load_zw(int s) const { return reinterpret_cast<const float2 *>(pts)[2 * s + 1]; }
 };
 
 // squared distance from p to cell c's box [c*cell, (c+1)*cell] along one axis,
@@ -207,29 +189,6 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
                 s = (int)(q[0] & 0xffffu);
                 e = (int)(q[0] >> 16);
             }
-#if PCR_GQ_XY
-            float2 cxy[kW];
-#pragma unroll
-            for (int u = 0; u < kW; ++u) cxy[u] = g.load_xy(sl[u]);
-            double pxy[kW];
-#pragma unroll
-            for (int u = 0; u < kW; ++u) {
-                const double dx = (double)cxy[u].x - px, dy = (double)cxy[u].y - py;
-                pxy[u] = dx * dx + dy * dy;
-            }
-#pragma unroll
-            for (int u = 0; u < kW; ++u) {
-                if (ok[u] && pxy[u] < thr) {
-                    const float2 zw = g.load_zw(sl[u]);
-                    const double dz = (double)zw.x - pz;
-                    const double d2 = pxy[u] + dz * dz;
-                    if (d2 < thr) {
-                        const int j = g.index_of(sl[u], zw.y);
-                        if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; if constexpr (kSlot) bs = sl[u]; }
-                    }
-                }
-            }
-#else
             float cx[kW], cy[kW], cz[kW], cw[kW];
 #pragma unroll
             for (int u = 0; u < kW; ++u) g.load(sl[u], cx[u], cy[u], cz[u], cw[u]);
@@ -243,7 +202,6 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
                     if (dd[u] < best || (dd[u] == best && j < bj)) { best = dd[u]; bj = j; if constexpr (kSlot) bs = sl[u]; }
                 }
             }
-#endif
         }
     } else {
         for (int x = x0; x <= x1; ++x) {
@@ -283,127 +241,12 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
     return bj;
 }
 
-// The f32-screened query: the same candidates in the same order, each screened
-// in f32 against a rigorous bound E on |d32 - d| (d the f64 distance of
-// dist2), valid for every candidate within 2r of p:
-//   p32 = fl(p) (|p - p32| <= 2^-24 A per axis, A = max |p_i|); dx32 = fl(c - p32)
-//   is within eta = 2^-24 A + 2^-24 (2r + 2^-24 A) of c - p; squares and two adds
-//   of values <= (2r + eta)^2 add 5 roundings: E = 6 eta (4r + eta) + 2^-20 (2r + eta)^2.
-// A candidate with d32 > thr + E has d >= thr (if d < thr every |c_i - p_i| < r
-// and the bound holds): rejected, no f64 work.  A survivor decides only when
-// the bound separates it from the threshold (d32 < thr - E) and from the
-// running minimum (|d32 - best32| > 2.5E); otherwise the query is ambiguous and
-// runs the exact f64 walk instead (near-ties, duplicates, points at ~r, huge
-// coordinates with E >= thr, NaN / Inf).  The winner's f64 distance is computed
-// once.  Every decision is therefore the exact walk's: same index, same d2.
-template <typename View, bool kSlot = false, int kW = 2>
-__device__ __forceinline__ int grid_query_screened(const View &g, double r, double thr, double px,
-                                                   double py, double pz, double &d2out, int *slot = nullptr) {
-    const QueryBox bx = query_box(px, py, pz, 1.001 * r * g.inv_cell, g.inv_cell);
-    const int x0 = bx.x0, x1 = bx.x1, y0 = bx.y0, y1 = bx.y1, z0 = bx.z0, z1 = bx.z1;
-    const double A = __builtin_fmax(__builtin_fmax(__builtin_fabs(px), __builtin_fabs(py)), __builtin_fabs(pz));
-    const double eta = 0x1p-24 * A + 0x1p-24 * (2.0 * r + 0x1p-24 * A);
-    // (+1e-30: f32 underflow of a square is an absolute error below 2^-126)
-    const double E = 6.0 * eta * (4.0 * r + eta) + 0x1p-20 * (2.0 * r + eta) * (2.0 * r + eta) + 1e-30;
-    if (!(x1 - x0 <= 1 && y1 - y0 <= 1 && z1 - z0 <= 1 && g.S <= 32768) || !(E < 0.25 * thr))
-        return grid_query_exact<View, kSlot, kW>(g, r, thr, px, py, pz, d2out, slot);
-    // f32 thresholds rounded outward (x (1 +- 2^-20) covers the f64 -> f32 rounding)
-    const float hiT = (float)((thr + E) * (1.0 + 0x1p-20));
-    const float loT = (float)((thr - E) * (1.0 - 0x1p-20));
-    // 2E plus slack for the f32 rounding of best32 -+ E2 itself (<= 2^-24 thr,
-    // while 0.5 E >= 2^-19 thr)
-    const float E2 = (float)(2.5 * E);
-    const float qx = (float)px, qy = (float)py, qz = (float)pz;
-    float gx[2], gy[2], gz[2];
-    axis_gaps(px, x0, x1, g.cell, gx);
-    axis_gaps(py, y0, y1, g.cell, gy);
-    axis_gaps(pz, z0, z1, g.cell, gz);
-    const float lim32 = (float)(thr * (1.0 + 1e-6));
-    const unsigned hx[2] = {(unsigned)x0 * 73856093u, (unsigned)(x0 + 1) * 73856093u};
-    const unsigned hy[2] = {(unsigned)y0 * 19349663u, (unsigned)(y0 + 1) * 19349663u};
-    const unsigned hz[2] = {(unsigned)z0 * 83492791u, (unsigned)(z0 + 1) * 83492791u};
-    unsigned q[8];
-    int nq = 0, total = 0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int ix = c >> 2, iy = (c >> 1) & 1, iz = c & 1;
-        const bool in = x0 + ix <= x1 && y0 + iy <= y1 && z0 + iz <= z1 && (gx[ix] + gy[iy]) + gz[iz] <= lim32;
-        q[c] = 0u;
-        if (in) {
-            const unsigned h = (hx[ix] ^ hy[iy] ^ hz[iz]) & (unsigned)(g.S - 1);
-            const int lo = (int)g.start[h], hi = (int)g.start[h + 1];
-            if (hi > lo) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (k == nq) q[k] = (unsigned)lo | ((unsigned)hi << 16);
-                ++nq;
-                total += hi - lo;
-            }
-        }
-    }
-    float best32 = __builtin_inff();
-    int bj = -1, bs = -1;
-    bool amb = false;
-    int s = (int)(q[0] & 0xffffu), e = (int)(q[0] >> 16);
-    while (total > 0) {
-        int sl[kW];
-        bool ok[kW];
-#pragma unroll
-        for (int u = 0; u < kW; ++u) {
-            ok[u] = u == 0 || s + u < e;
-            sl[u] = ok[u] ? s + u : s;
-        }
-        int took = 1;
-#pragma unroll
-        for (int u = 1; u < kW; ++u) took += ok[u] ? 1 : 0;
-        s += took;
-        total -= took;
-        if (s >= e) {
-#pragma unroll
-            for (int k = 0; k < 7; ++k) q[k] = q[k + 1];
-            q[7] = 0u;
-            s = (int)(q[0] & 0xffffu);
-            e = (int)(q[0] >> 16);
-        }
-        float cx[kW], cy[kW], cz[kW], cw[kW];
-#pragma unroll
-        for (int u = 0; u < kW; ++u) g.load(sl[u], cx[u], cy[u], cz[u], cw[u]);
-#pragma unroll
-        for (int u = 0; u < kW; ++u) {
-            const float dx = cx[u] - qx, dy = cy[u] - qy, dz = cz[u] - qz;
-            const float d32 = (dx * dx + dy * dy) + dz * dz;
-            if (ok[u] && d32 <= hiT) {  // a survivor (NaN never gets here: the exact walk rejects it too)
-                amb = amb || !(d32 < loT);
-                if (bj < 0 || d32 < best32 - E2) {
-                    best32 = d32;
-                    bj = g.index_of(sl[u], cw[u]);
-                    bs = sl[u];
-                } else if (!(d32 > best32 + E2)) {
-                    amb = true;
-                }
-            }
-        }
-    }
-    if (amb) return grid_query_exact<View, kSlot, kW>(g, r, thr, px, py, pz, d2out, slot);
-    double d2 = __builtin_inf();
-    if (bj >= 0) {
-        float ax, ay, az, aw;
-        g.load(bs, ax, ay, az, aw);
-        d2 = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
-    }
-    d2out = d2;
-    if constexpr (kSlot) *slot = bs;
-    return bj;
-}
-
 template <typename View, bool kSlot = false, int kW = 2>
 __device__ __forceinline__ int grid_query(const View &g, double r, double thr, double px,
                                           double py, double pz, double &d2out, int *slot = nullptr) {
-#if PCR_GQ_F32
-    return grid_query_screened<View, kSlot, kW>(g, r, thr, px, py, pz, d2out, slot);
-#else
+    // (an f32-screened walk with a rigorous bound -- f64 only for the winner --
+    // measured no faster in round 4: the LDS candidate gathers bind as much)
     return grid_query_exact<View, kSlot, kW>(g, r, thr, px, py, pz, d2out, slot);
-#endif
 }
 
 // Grids for P target clouds (device, workspace-backed; see grid.hip).

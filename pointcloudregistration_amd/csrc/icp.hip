@@ -77,6 +77,21 @@ struct IArgs {
     unsigned long long *timing;  // debug (PCR_ICP_TIMING): per pair, phase clocks
 };
 
+// The working copy when a pair has G > 1 workgroups: each pair barrier's
+// release fence writes back the XCD L2's dirty lines, and a sweep dirtied ~48 KB
+// of working copy per workgroup (2,048 points x 24 B at 32 pairs, G = 4).
+// Stored write-through (sc1: the line leaves L2 clean) there is nothing of it to
+// write back; visibility is still the barrier's release / acquire.
+__device__ __forceinline__ void put3(double *q, double x, double y, double z, bool wt) {
+    if (wt) {
+        __hip_atomic_store(q, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 2, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        q[0] = x; q[1] = y; q[2] = z;
+    }
+}
+
 // a listed pair's state: T (16), C (9), ms (3), mt (3), fit, rmse, count, it
 constexpr int kSave = 36;
 
@@ -246,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                 xform12(T0, x, y, z, ox, oy, oz);
                 x = ox; y = oy; z = oz;
             }
-            P3[3 * k] = x; P3[3 * k + 1] = y; P3[3 * k + 2] = z;
+            put3(P3 + 3 * k, x, y, z, G > 1);
         }
         if (G > 1) pair_barrier(a.bar + 4 * (size_t)p, G);  // (G = 1: the barrier below)
     }
@@ -314,7 +329,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                         double ox, oy, oz;
                         xform12(U, x, y, z, ox, oy, oz);
                         x = ox; y = oy; z = oz;
-                        P3[3 * k] = x; P3[3 * k + 1] = y; P3[3 * k + 2] = z;
+                        put3(P3 + 3 * k, x, y, z, G > 1);
                     }
                     double d2;
                     int q, s;

@@ -54,9 +54,7 @@
 // (d, j) minimum -- the same bits as the grid path and pcr_nnd_forward -- from
 // any starting index.  Four launches and the far-query list (count / scan /
 // scatter, walk, fallback, emit) become two.
-#ifndef PCR_NC_SKIP
-#define PCR_NC_SKIP false  // ring_walk's per-cell bounds (nng.h): off for the level Chamfer
-#endif
+constexpr bool kNcSkip = false;  // ring_walk's per-cell bounds (nng.h): off for the level Chamfer (measured equal)
 #include "pcr_internal.h"
 #include "nng.h"
 #include "scan.h"
@@ -409,7 +407,7 @@ __global__ __launch_bounds__(256) void nc_query(NcArgs a, int nb0) {
     }
     const nng::View v = dir ? nng::View{a.hdr->cell_s, a.cs.S, a.cs.start, a.cs.pts}
                             : nng::View{a.hdr->cell_t, a.ct.S, a.ct.start, a.ct.pts};
-    const bool done = nng::ring_walk<LPQ, PCR_NC_SKIP>(v, qx, qy, qz, sub, a.kmax, best, bj);
+    const bool done = nng::ring_walk<LPQ, kNcSkip>(v, qx, qy, qz, sub, a.kmax, best, bj);
     // listed queries appended with one atomic per wave (thousands of far
     // queries on one counter serialised at the L2); a wave holds one direction
     const bool list = !done && sub == 0;
@@ -928,8 +926,7 @@ int nc_args(const pcr_ndp_chamfer *c, NcArgs &a) {
     a.fb = (int *)(s + L.fb);
     a.fbkey = (unsigned long long *)(s + L.fbkey);
     a.gate = current_gate();
-    a.fshift = -1;
-    if (const char *e = getenv("PCR_NDP_FIXSHIFT")) a.fshift = atoi(e);
+    a.fshift = -1;  // (a fixed exponent, hi words only: the round-3 form, kept for diagnostics)
     return PCR_OK;
 }
 
@@ -1015,11 +1012,7 @@ extern "C" int pcr_ndp_chamfer_step(const pcr_ndp_chamfer *c, pcr_stream_t strea
         hipLaunchKernelGGL(pcr::nc_leaves, dim3(nbz), dim3(1024), 0, s, a.xs, a.bs, a.hdr->sbad, a.gacc,
                            a.hdr->samax, a.gate);
         PCR_LAUNCH_CHECK();
-        int lpq = 8;
-        if (const char *e = getenv("PCR_NC_LPQ")) {
-            const int v = atoi(e);
-            if (v == 4 || v == 8 || v == 16) lpq = v;
-        }
+        const int lpq = 8;  // lanes per box query (4 / 8 / 16 measured, round 4)
         const int qpb = 256 / lpq;
         const int nb0 = (a.K + qpb - 1) / qpb, nb1 = (a.M + qpb - 1) / qpb;
         const size_t lds = sizeof(pcr::NcBox) * (size_t)(pcr::kGrp + std::max(a.bt.L, a.bs.L));  // <= 33 KiB

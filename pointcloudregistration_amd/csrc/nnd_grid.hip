@@ -35,7 +35,7 @@ struct NgArgs {
     const float *xyz[2];  // set 0: xyz1 (B, n0, 3), set 1: xyz2 (B, n1, 3)
     int n[2];
     int B, S, nmax;
-    float cf;             // cell factor (0.6; PCR_NND_CELL overrides, tuning hook)
+    float cf;             // cell factor (0.6)
     float *cell;          // [2][B]
     int *flag;            // [2][B]: set s of pair b holds a NaN/Inf or is too far out (both: the reference loop)
     int *hcnt;            // [2][B][S]
@@ -318,11 +318,7 @@ int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, co
     a.start = a.hcnt + hc;
     a.dist[0] = dist1; a.dist[1] = dist2; a.idx[0] = idx1; a.idx[1] = idx2;
     a.gate = current_gate();
-    a.cf = 0.6f;
-    if (const char *e = getenv("PCR_NND_CELL")) {
-        const float v = (float)atof(e);
-        if (v >= 0.1f && v <= 4.0f) a.cf = v;
-    }
+    a.cf = 0.6f;  // 0.4 / 0.5 / 0.6 / 0.8 / 1.0 x cbrt(V / n) measured
     const bool lds_build = S <= kLdsSlots;
     PCR_REQUIRE(lds_build || !src, PCR_ERR_ARG, "nnd_forward (grid): fused transform needs the LDS build");
     if (!lds_build) PCR_HIP_CHECK(hipMemsetAsync(a.hcnt, 0, sizeof(int) * hc, s));

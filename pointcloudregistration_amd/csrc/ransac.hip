@@ -40,9 +40,7 @@
 #include <cstdlib>
 #include <vector>
 
-#ifndef PCR_RANSAC_KW
-#define PCR_RANSAC_KW 4  // candidates per grid-walk step in the RANSAC sweeps
-#endif
+constexpr int kRansacKW = 4;  // candidates per grid-walk step in the sweeps (2 / 4 / 6 / 8 measured, round 4)
 
 namespace pcr {
 namespace {
@@ -323,9 +321,12 @@ __device__ TaskRes sweep_pair(const RArgs &a, Shared &sh, const Grid &gr, int p,
             }
             double px, py, pz, d2;
             xform12(Te, (double)sx, (double)sy, (double)sz, px, py, pz);
-            j = grid_query<Grid, false, PCR_RANSAC_KW>(gr, a.d, a.thr, px, py, pz, d2);
+            j = grid_query<Grid, false, kRansacKW>(gr, a.d, a.thr, px, py, pz, d2);
             if (j >= 0) { ++cnt; acc += (unsigned long long)(d2 * scale); }
-            if (cbuf) cbuf[by_order ? k : (ord ? ord[k] : k)] = j;
+            // written through (sc1): finish_task's release fence writes back the
+            // XCD L2's dirty lines, and a sweep's targets are 32 KB of them
+            if (cbuf) __hip_atomic_store(cbuf + (by_order ? k : (ord ? ord[k] : k)), j, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
         }
         const int miss = __popcll(__ballot(k < n && j < 0));
         int tot = 0;

@@ -239,3 +239,52 @@ def test_icp_tail_rebalance_bitexact(oracle, coop_g, relf):
         o = oracle.icp(B.src[p], B.tgt[p], 0.05, init=init[p], relative_fitness=relf, relative_rmse=relf)
         assert _bits(two[0][p], o["T"]), p
         assert tuple(two[3][p]) == (o["iters"], o["n_corr"])
+
+
+def test_icp_tail_concurrent_contexts_bitexact():
+    """two ICP batches at once on two streams and two workspace
+    contexts under pcr_set_concurrency(2), each large enough for the tail
+    hand-off (P >= phase-2 grid / 2 with the grid sized to half the chip): the
+    same bits as one launch per batch (PCR_ICP_TAIL=0), run one after the other."""
+    import torch
+    from pointcloudregistration_amd import _lib
+    os.environ.pop("PCR_COOP_G", None)
+    P, n = 160, 1500
+    Bs = [synth.make_batch(P, n=n, m=n, d=8, base_seed=5100 + 1000 * k, feat_noise=1.0) for k in range(2)]
+    inits = []
+    rng = np.random.default_rng(7)
+    for B in Bs:
+        init = np.zeros((P, 4, 4))
+        for p in range(P):
+            s = 0.002 + 0.05 * rng.random()
+            init[p, :3, :3] = synth.rotation_xyz(*rng.normal(0, s, 3)) @ B.R[p]
+            init[p, :3, 3] = B.t[p] + rng.normal(0, s, 3)
+            init[p, 3, 3] = 1
+        inits.append(init)
+    prm = reg.IcpParams(0.05)
+    old = os.environ.get("PCR_ICP_TAIL")
+    try:
+        os.environ["PCR_ICP_TAIL"] = "0"
+        want = []
+        for B, init in zip(Bs, inits):
+            r = reg.icp_batch(B.src, B.tgt, init, prm)
+            want.append([_np(t).copy() for t in (r.transformation, r.fitness, r.inlier_rmse, r.stats)])
+        os.environ.pop("PCR_ICP_TAIL")
+        _lib.call("pcr_set_concurrency", 2)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        got = [None, None]
+        for k in range(2):
+            _lib.call("pcr_set_workspace_context", k)
+            with torch.cuda.stream(streams[k]):
+                got[k] = reg.icp_batch(Bs[k].src, Bs[k].tgt, inits[k], prm)
+        _lib.call("pcr_set_workspace_context", 0)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("pcr_set_concurrency", 1)
+        _lib.call("pcr_set_workspace_context", 0)
+        if old is not None:
+            os.environ["PCR_ICP_TAIL"] = old
+    for k in range(2):
+        g = [_np(t) for t in (got[k].transformation, got[k].fitness, got[k].inlier_rmse, got[k].stats)]
+        for a, b in zip(want[k], g):
+            assert _bits(a, b), k

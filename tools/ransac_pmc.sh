@@ -4,6 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+export PCR_ICP_TAIL=0  # the cooperative tail launch faults at exit under the profiler
 OUT=${1:-gpurun_out/pmc_ransac}
 mkdir -p "$OUT"
 run() {
