@@ -23,7 +23,7 @@ void *workspace(int slot, size_t bytes, bool *fresh = nullptr);
 // writing it to xyz1, inside the grid's box pass (max(n, m) <= 32768)
 bool nnd_uses_grid(int b, int n, int m);
 
-// pcr_pipeline_step's hook into the feature stage (tuning, PCR_PREP_AT): when
+// pcr_pipeline_step's hook into the feature stage: when
 // set, feature_corres_v5 records prep_event on its stream before (at = 2) or
 // after (at = 1) the pass-1 launch, so the side stream's grid builds start there
 extern thread_local hipEvent_t prep_event;

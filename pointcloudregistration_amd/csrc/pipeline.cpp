@@ -114,11 +114,10 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     // when the prep starts: 0 with the step (it then competes with the
     // bandwidth-bound descriptor pack), 1 / 2 once pass 1 of the feature screen
     // is done / launched (an event recorded inside the feature stage).  Measured
-    // (tools/r04_check35.sh, 36.sh): 256 pairs 9.47 / 9.36 / 9.48 ms, 128 pairs
-    // 5.14 / 5.16 / 5.16, 64 pairs 2.90 / 2.91 / 2.93, 32 pairs 1.84 / 1.83 /
-    // 1.81 ms; PCR_PREP_AT overrides.  D > 64 (no hook in that screen): 0
+    // (round 4): 256 pairs 9.47 / 9.36 / 9.48 ms, 128 pairs 5.14 / 5.16 / 5.16,
+    // 64 pairs 2.90 / 2.91 / 2.93, 32 pairs 1.84 / 1.83 / 1.81 ms.  D > 64 (no
+    // hook in that screen): 0
     int at = P >= 192 ? 1 : P <= 48 ? 2 : 0;
-    if (const char *e = getenv("PCR_PREP_AT")) at = atoi(e) == 1 || atoi(e) == 2 ? atoi(e) : 0;
     if (io->D > 64) at = 0;
     pcr::GridBatch grid_r{}, grid_i{};
     const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP
