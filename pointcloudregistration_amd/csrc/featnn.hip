@@ -353,7 +353,8 @@ __global__ __launch_bounds__(256) void feat_pack5(PackIO io, int D, int S, Split
                 } else {
                     if (k < 3) v = role == 0 ? np[k] : cval;
                     else if (k < 6) v = role == 0 ? cval : np[k - 3];
-                    else if (k == 6 && role == 1) v = (_Float16)32768.0f;  // featnn_row8's bias
+                    else if (k == 6 && role == 1) v = (_Float16)32768.0f;  // featnn_row8's biases
+                    else if (k == 7 && role == 0) v = (_Float16)32768.0f;
                 }
                 o[j] = v;
             }
@@ -467,7 +468,8 @@ __global__ __launch_bounds__(256) void feat_pack5r(PackIO io, Split5 sp, PackCtl
                 else if (g == 2 * G) {
                     if (j < 3) v = role == 0 ? np[j] : cval;
                     else if (j < 6) v = role == 0 ? cval : np[j - 3];
-                    else if (j == 6 && role == 1) v = (_Float16)32768.0f;  // featnn_row8's bias
+                    else if (j == 6 && role == 1) v = (_Float16)32768.0f;  // featnn_row8's biases
+                    else if (j == 7 && role == 0) v = (_Float16)32768.0f;
                 }
                 o[j] = v;
             }
@@ -1082,7 +1084,8 @@ __device__ __forceinline__ void row_frags(const float *x, int D, int h, int role
             } else {
                 if (j < 3) v0 = role == 0 ? np[j] : cval;
                 else if (j < 6) v0 = role == 0 ? cval : np[j - 3];
-                else if (j == 6 && role == 1) v0 = (_Float16)32768.0f;  // featnn_row8's bias
+                else if (j == 6 && role == 1) v0 = (_Float16)32768.0f;  // featnn_row8's biases
+                else if (j == 7 && role == 0) v0 = (_Float16)32768.0f;
             }
             out[c][j] = h ? v1 : v0;
         }
@@ -1348,12 +1351,15 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 // ---------------------------------------------------------------------------
 constexpr int kRow8Head = 24;  // epilogue VALU in front of phase A's first MFMA (the B reads' latency)
 constexpr int kRow8G = 8;      // column tiles per LDS group (16: the whole LDS, measured no faster)
-constexpr double kRowBias = 32768.0;  // B: 1.0 (row k = 6) x 2^15 (column image k = 6)
+// B: pass 1 1.0 (row k = 6) x 2^15 (G's column image, k = 6); pass 2 (featnn_row8
+// <.., false>, the J rows of G against F's image) 1.0 (row k = 7) x 2^15 (F's
+// image, k = 7).  dual7 pairs F's image with G's: 0 x 2^15 at both slots.
+constexpr double kRowBias = 32768.0;
 
 __device__ __forceinline__ unsigned umin2(unsigned a, unsigned b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned umax2(unsigned a, unsigned b) { return a > b ? a : b; }
 
-template <int S, int G>
+template <int S, int G, bool kIdx>
 __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     constexpr int W = 8, RT = 2;                   // waves per workgroup, row tiles per wave
     constexpr int NX = 3 * S + 1, NM = 2 * S + 1;  // executed / stored k-chunks
@@ -1363,7 +1369,8 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
     if (p >= a.P) return;  // whole block
-    const int nr = count_of(a.n_rows, p, a.Rmax);
+    // pass 1: the F rows in order; pass 2: the listed rows J of G (rlist)
+    const int nr = kIdx ? count_of(a.n_rows, p, a.Rmax) : a.rcount[p];
     if (rb * W * RT * 32 >= nr) return;  // whole block: no rows here
     const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
     const int m = count_of(a.n_cols, p, a.Cmax);
@@ -1380,24 +1387,25 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         const float sc = __uint_as_float(a.sc[p]);
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
-            const int row = (qt0 + t) * 32 + (l & 31);
+            const int k = (qt0 + t) * 32 + (l & 31);
+            const int row = kIdx ? k : (k < nr ? a.rlist[(size_t)p * a.Rmax + k] : 0);
             float x[16 * S];
             const float *xr = a.Xr + ((size_t)p * a.Rmax + row) * a.D;
-            if (row < nr && a.D == 16 * S && ((uintptr_t)xr & 15) == 0) {
+            if (k < nr && a.D == 16 * S && ((uintptr_t)xr & 15) == 0) {
 #pragma unroll
                 for (int q = 0; q < 4 * S; ++q) {
                     const float4 v = reinterpret_cast<const float4 *>(xr)[q];
                     x[4 * q] = v.x * sc; x[4 * q + 1] = v.y * sc; x[4 * q + 2] = v.z * sc; x[4 * q + 3] = v.w * sc;
                 }
-            } else if (row < nr) {
+            } else if (k < nr) {
 #pragma unroll
                 for (int q = 0; q < 16 * S; ++q) x[q] = q < a.D ? xr[q] * sc : 0.0f;
             } else {
 #pragma unroll
                 for (int q = 0; q < 16 * S; ++q) x[q] = 0.0f;  // rows past the count write nothing
             }
-            row_frags<S>(x, a.D, h, 0, a.cs, A[t]);
-            if (h == 0) A[t][NM - 1][6] = (_Float16)1.0f;  // the bias (see above)
+            row_frags<S>(x, a.D, h, kIdx ? 0 : 1, a.cs, A[t]);
+            if (h == 0) A[t][NM - 1][kIdx ? 6 : 7] = (_Float16)1.0f;  // the bias (see above)
         }
     }
     unsigned b1[RT][16], b2[RT][16];
@@ -1420,8 +1428,9 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         const unsigned ct1 = ct + 1u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const unsigned cx = (__float_as_uint(x[0][r]) & keep) | ct;
-            const unsigned cy = (__float_as_uint(x[1][r]) & keep) | ct1;
+            // pass 1: the tile numbers in the low bits; pass 2: values only
+            const unsigned cx = kIdx ? (__float_as_uint(x[0][r]) & keep) | ct : __float_as_uint(x[0][r]);
+            const unsigned cy = kIdx ? (__float_as_uint(x[1][r]) & keep) | ct1 : __float_as_uint(x[1][r]);
             // the median as v_med3_f32 (the same order on these non-negative
             // patterns; an integer median shares min(b1, cx) with the min3
             // below and costs a v_min more)
@@ -1542,6 +1551,15 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         const int mi1 = (int)(B1 & ctmask) * 32 + jw;
         const int row = qt * 32 + R;
         if (h != 0 || row >= nr) continue;
+        if constexpr (!kIdx) {  // pass 2: the row's biased top-2 values and its bound, by original row
+            const int j = a.rlist[(size_t)p * a.Rmax + row];
+            const double e2 = 0.5 * (bound5((double)a.rnr[(size_t)p * a.ntr * 32 + j],
+                                            (double)__uint_as_float(a.cmax[p]), 16 * NX, a.D) +
+                                     4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kRowBias);
+            a.wq[(size_t)p * a.Rmax + j] = make_float4(m == 0 ? __builtin_inff() : mb1, m == 0 ? __builtin_inff() : mb2,
+                                                       (float)(e2 * (1.0 + 1e-6)), 0.0f);
+            continue;
+        }
         const size_t o = (size_t)p * a.Rmax + row;
         if (m == 0) {
             a.nn[o] = 0;
@@ -1574,6 +1592,7 @@ struct MutArgs {
     const double *v12;
     const float *e12;
     const float4 *wq;
+    double wbias;     // the bias in wq's values (featnn_row8: kRowBias; featnn_row7: 0)
     const unsigned *fmax;
     int *flag;        // [P][Nmax + 1]: mutual 0 / 1, 2 = decided by the exact column
     int *list21, *cnt21;
@@ -1614,8 +1633,8 @@ __global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
     int f = 0;
     if (j >= 0 && j < m) {
         const size_t oj = (size_t)p * a.Mmax + j, oi = (size_t)p * a.Nmax + i;
-        const float4 q = a.wq[oj];
-        const double w1 = (double)q.x, w2 = (double)q.y, e2 = (double)q.z;
+        const float4 q = a.wq[oj];  // featnn_row8's pass 2 stores biased values (exact in f64)
+        const double w1 = (double)q.x - a.wbias, w2 = (double)q.y - a.wbias, e2 = (double)q.z;
         const double vi = a.v12[oi], e1 = (double)a.e12[oi];
         // slack: the f64 sums of a rescanned value vs the exact real distance
         const double sl = 1e-9 * (__builtin_fabs(w1) + __builtin_fabs(vi));
@@ -1923,6 +1942,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     ma.nn12 = nn12; ma.n_src = n_src; ma.n_tgt = n_tgt; ma.Nmax = Nmax; ma.Mmax = Mmax;
     ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * v.NX; ma.D = D; ma.ntm = ntm;
     ma.v12 = v12; ma.e12 = e12; ma.wq = wq; ma.fmax = v.fmax;
+    ma.wbias = v.S <= 2 ? kRowBias : 0.0;
     ma.list21 = v.list21; ma.cnt21 = v.cnt21; ma.nn21x = nn21x;
     ma.corres = corres; ma.n_corres = n_corres;
     // pass 1: F rows x all G columns
@@ -1941,8 +1961,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         r.nrb = cdiv(cdiv(Nmax, 32), v.W * 2);
         const long long nblk = 8LL * r.nrb * cdiv(P, 8);  // XCD-aware 1-D grid
         PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
-        if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
-        else hipLaunchKernelGGL((featnn_row8<2, kRow8G>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G, true>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+        else hipLaunchKernelGGL((featnn_row8<2, kRow8G, true>), dim3((unsigned)nblk), dim3(512), 0, s, r);
         PCR_LAUNCH_CHECK();
     } else {
         rc = launch_row7<true>(r, v.S, s, rt1);
@@ -1970,8 +1990,17 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         r2.wq = wq;
         r2.Xr = G; r2.sc = v.mx; r2.role = 1; r2.cs = v.sp.cs;
         prof_begin(s, kProfFeatScreen2);
-        rc = launch_row7<false>(r2, v.S, s, rt2);
-        if (rc != PCR_OK) return rc;
+        if (v.S <= 2) {  // two column tiles per step, values only (featnn_row8<.., false>)
+            r2.nrb = cdiv(cdiv(Mmax, 32), v.W * 2);
+            const long long nblk = 8LL * r2.nrb * cdiv(P, 8);
+            PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
+            if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G, false>), dim3((unsigned)nblk), dim3(512), 0, s, r2);
+            else hipLaunchKernelGGL((featnn_row8<2, kRow8G, false>), dim3((unsigned)nblk), dim3(512), 0, s, r2);
+            PCR_LAUNCH_CHECK();
+        } else {
+            rc = launch_row7<false>(r2, v.S, s, rt2);
+            if (rc != PCR_OK) return rc;
+        }
         prof_end(s, kProfFeatScreen2);
         hipLaunchKernelGGL(featmut_resolve, dim3(cdiv(Nmax, 256), P), dim3(256), 0, s, ma);
         PCR_LAUNCH_CHECK();
