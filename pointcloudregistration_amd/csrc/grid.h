@@ -110,18 +110,32 @@ __device__ __forceinline__ void axis_gaps(double p, int c0, int c1, double cell,
 // LDS loads overlap.  The update order (slot order, strict < then lower index
 // on ties) makes the result independent of both.
 // kSlot: also report the winner's slot (its coordinates are g.x/y/z[slot])
-template <typename View, bool kSlot = false, int kW = 2>
+// kClear: also report in *s2out the second smallest computed d2 over EVERY
+// examined candidate (inside the radius or not; +inf when fewer than two) --
+// with the walk's guarantee that every unexamined target lies farther than r
+// from p, min(sqrt(s2), r) bounds the distance from p to any target other
+// than the winner (icp.hip's correspondence reuse)
+template <typename View, bool kSlot = false, int kW = 2, bool kClear = false>
 __device__ __forceinline__ int grid_query_exact(const View &g, double r, double thr, double px,
-                                                double py, double pz, double &d2out, int *slot = nullptr) {
+                                                double py, double pz, double &d2out, int *slot = nullptr,
+                                                double *s2out = nullptr) {
     const QueryBox bx = query_box(px, py, pz, 1.001 * r * g.inv_cell, g.inv_cell);
     const int x0 = bx.x0, x1 = bx.x1, y0 = bx.y0, y1 = bx.y1, z0 = bx.z0, z1 = bx.z1;
     const double lim = thr * (1.0 + 1e-9);
     double best = __builtin_inf();
+    double e1 = __builtin_inf(), e2 = __builtin_inf();  // kClear: the two smallest examined d2
+    auto seen = [&](double d) {
+        if constexpr (kClear) {
+            e2 = __builtin_fmin(e2, __builtin_fmax(e1, d));
+            e1 = __builtin_fmin(e1, d);
+        }
+    };
     int bj = -1, bs = -1;
     auto take = [&](int s) {
         float ax, ay, az, aw;
         g.load(s, ax, ay, az, aw);
         const double d2 = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
+        seen(d2);
         if (d2 < thr) {
             const int j = g.index_of(s, aw);
             if (d2 < best || (d2 == best && j < bj)) { best = d2; bj = j; if constexpr (kSlot) bs = s; }
@@ -196,6 +210,9 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
 #pragma unroll
             for (int u = 0; u < kW; ++u) dd[u] = dist2(px, py, pz, (double)cx[u], (double)cy[u], (double)cz[u]);
 #pragma unroll
+            for (int u = 0; u < kW; ++u)
+                if (ok[u]) seen(dd[u]);
+#pragma unroll
             for (int u = 0; u < kW; ++u) {
                 if (ok[u] && dd[u] < thr) {
                     const int j = g.index_of(sl[u], cw[u]);
@@ -222,6 +239,8 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
                         g.load(s + 1, bx, by, bz, bw);
                         const double da = dist2(px, py, pz, (double)ax, (double)ay, (double)az);
                         const double db = dist2(px, py, pz, (double)bx, (double)by, (double)bz);
+                        seen(da);
+                        seen(db);
                         if (da < thr) {
                             const int j = g.index_of(s, aw);
                             if (da < best || (da == best && j < bj)) { best = da; bj = j; if constexpr (kSlot) bs = s; }
@@ -238,6 +257,7 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
     }
     d2out = best;
     if constexpr (kSlot) *slot = bs;
+    if constexpr (kClear) *s2out = e2;
     return bj;
 }
 

@@ -55,6 +55,7 @@ struct IArgs {
     int max_iter;
     GridBatch grid;
     double *P3;          // P x Nmax x 3 working copy by position in the order
+    int4 *cst;           // P x Nmax correspondence state by position (see CorrState)
     const float *srcp;   // (P, Nmax, 3) the source points in that order, or null
     double *T_out, *fit_out;
     int32_t *stats;
@@ -92,6 +93,30 @@ __device__ __forceinline__ void put3(double *q, double x, double y, double z, bo
     }
 }
 
+// Correspondence reuse.  A point's grid walk also reports the second smallest
+// distance it computed; with every unexamined target farther than ~r, that
+// gives a clearance c: every target other than the winner w lies at least c
+// from the point.  Moved since by at most D (the summed step lengths), the
+// point is still strictly nearest to w -- the walk would return w, with the same
+// d2 bits -- while |p - w| < c - D and d2 < thr.  Such a point skips the walk.
+// Per position, int4 {w's grid slot or -1, c (f32, rounded down), D (f32,
+// rounded up), unused}; rewritten by every walk (D = 0).
+__device__ __forceinline__ void put_state(int4 *q, int4 v, bool wt) {
+    if (wt) {
+        int *w = reinterpret_cast<int *>(q);
+        __hip_atomic_store(w, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *q = v;
+    }
+}
+__device__ __forceinline__ void put_step(int4 *q, int z, bool wt) {
+    int *w = reinterpret_cast<int *>(q) + 2;
+    if (wt) __hip_atomic_store(w, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *w = z;
+}
+
 // a listed pair's state: T (16), C (9), ms (3), mt (3), fit, rmse, count, it
 constexpr int kSave = 36;
 
@@ -116,6 +141,8 @@ struct IShared {  // LDS header; the grid copy (if any) follows
     int nred;         // reductions done (parity of the HBM partial slots)
     int chunk[2];     // next 64-position chunk of the current sweep, by parity (G = 1)
     int handoff;      // phase 1: this pair is listed for phase 2
+    int pend[kWaves][128];  // per wave: positions waiting for a grid walk (a stack)
+    int nwalk;        // debug (PCR_ICP_PHASES): walks done by this workgroup
 };
 
 // wave-level sums of NQ exact f64 values (integer multiples of the quantum:
@@ -214,10 +241,12 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     const int32_t *ord = a.order ? a.order + (size_t)p * a.Nmax : nullptr;
     // working copy (f64 xyz) by source INDEX, AoS
     double *P3 = a.P3 + (size_t)p * a.Nmax * 3;
+    int4 *cst = a.cst + (size_t)p * a.Nmax;
+    const bool wt = G > 1;  // working copy / state stores write-through (put3)
     int32_t *CT = a.corr_tgt ? a.corr_tgt + (size_t)p * a.Nmax : nullptr;
     const double *sv = resume ? a.save + (size_t)p * kSave : nullptr;
     if (tid < 16) sh.T[tid] = resume ? sv[tid] : a.init[(size_t)p * 16 + tid];
-    if (tid == 0) { sh.nred = 0; sh.chunk[0] = 0; sh.chunk[1] = 0; sh.handoff = 0; }
+    if (tid == 0) { sh.nred = 0; sh.chunk[0] = 0; sh.chunk[1] = 0; sh.handoff = 0; sh.nwalk = 0; }
     __syncthreads();
     const bool valid = a.d > 0.0 && n > 0 && m > 0;
     bool ident = true;
@@ -273,6 +302,10 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     }
     __syncthreads();
     const double scale = fx_scale(a.thr);
+    // every target a walk did not examine lies at least this far from the query
+    // (outside the query box: >= r; in a skipped cell: > sqrt(thr))
+    const double rclr = __builtin_fmin(a.d, __builtin_sqrt(a.thr)) * (1.0 - 1e-6);
+    const int wid = tid >> 6;
     // debug phase clocks (s_memtime) of workgroup 0's thread 0: only in a build
     // with -DPCR_ICP_PHASES (the registers they hold cost the normal build)
 #ifdef PCR_ICP_PHASES
@@ -313,58 +346,105 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             int *ctr = G > 1 ? a.chunk + 4 * p + (nsweep & 1) : &sh.chunk[nsweep & 1];
             const int nch = (n + 63) >> 6;
             const double c0x = sh.c0[0], c0y = sh.c0[1], c0z = sh.c0[2];
+            // the exact Umeyama terms of a correspondence, in quanta: trunc(s'_a
+            // 2^k), trunc(t'_b 2^k), trunc(s'_a t'_b 2^k) -- the scaling by 2^k is
+            // exact, so (s'_a 2^k) t'_b rounds to the same value as (s'_a t'_b)
+            // 2^k; the sums (integers below 2^52) are scaled back by 2^-k after
+            // the reduction
+            auto add_corr = [&](double *vv, int &cn, unsigned long long &ac, double x, double y, double z,
+                                float qx, float qy, float qz, double d2) {
+                ++cn;
+                ac += (unsigned long long)(d2 * scale);
+                const volatile double *skv = &sh.sk;
+                const double sk = skv[0];
+                const double sps[3] = {(x - c0x) * sk, (y - c0y) * sk, (z - c0z) * sk};
+                const double tp[3] = {(double)qx - c0x, (double)qy - c0y, (double)qz - c0z};
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) {
+                    vv[cc] = vv[cc] + __builtin_trunc(sps[cc]);
+                    vv[3 + cc] = vv[3 + cc] + __builtin_trunc(tp[cc] * sk);
+#pragma unroll
+                    for (int e = 0; e < 3; ++e)
+                        vv[6 + 3 * cc + e] = vv[6 + 3 * cc + e] + __builtin_trunc(sps[cc] * tp[e]);
+                }
+            };
+            // the grid walk of position k (its point already transformed): the
+            // correspondence, and the state that lets later sweeps reuse it
+            auto walk = [&](int k) {
+#ifdef PCR_ICP_PHASES
+                atomicAdd(&sh.nwalk, 1);
+#endif
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // this wave's P3 stores
+                const double x = P3[3 * k], y = P3[3 * k + 1], z = P3[3 * k + 2];
+                double d2, e2;
+                int q, sl;
+                float qx = 0.f, qy = 0.f, qz = 0.f, qw;
+                if constexpr (kLds) {
+                    q = grid_query_exact<GridP4, true, 2, true>(gl, a.d, a.thr, x, y, z, d2, &sl, &e2);
+                    if (q >= 0) gl.load(sl, qx, qy, qz, qw);
+                } else {
+                    q = grid_query_exact<GridView, true, 2, true>(gg, a.d, a.thr, x, y, z, d2, &sl, &e2);
+                    if (q >= 0) gg.load(sl, qx, qy, qz, qw);
+                }
+                if (CT) CT[ord ? ord[k] : k] = q;
+                const float cf = (float)(__builtin_fmin(__builtin_sqrt(e2), rclr) * (1.0 - 2e-6));
+                put_state(cst + k, make_int4(q >= 0 ? sl : -1, __float_as_int(cf), 0, 0), wt);
+                if (q >= 0) add_corr(v, cnt, acc, x, y, z, qx, qy, qz, d2);
+            };
+            int np = 0;  // positions on this wave's stack
             for (;;) {
                 int c = 0;
                 if (lane == 0) c = G > 1 ? coop_fetch_add(ctr, 1) : atomicAdd(ctr, 1);
                 c = __shfl(c, 0, 64);
                 if (c >= nch) break;
                 const int k = (c << 6) + lane;
+                // phase A: transform; reuse the correspondence when certified
+                bool need = false;
                 if (k < n) {
                     double x = P3[3 * k], y = P3[3 * k + 1], z = P3[3 * k + 2];
-                    if (with_u) {  // U from LDS per chunk (volatile: not held across the query)
+                    if (!with_u) {
+                        need = true;
+                    } else {  // U from LDS per chunk (volatile: not held across the query)
                         const volatile double *Uv = sh.U;
                         double U[12];
 #pragma unroll
                         for (int q = 0; q < 12; ++q) U[q] = Uv[q];
                         double ox, oy, oz;
                         xform12(U, x, y, z, ox, oy, oz);
-                        x = ox; y = oy; z = oz;
-                        put3(P3 + 3 * k, x, y, z, G > 1);
-                    }
-                    double d2;
-                    int q, s;
-                    float qx = 0.f, qy = 0.f, qz = 0.f;
-                    if constexpr (kLds) {
-                        q = grid_query<GridP4, true>(gl, a.d, a.thr, x, y, z, d2, &s);
-                        if (q >= 0) { float w; gl.load(s, qx, qy, qz, w); }
-                    } else {
-                        q = grid_query<GridView, true>(gg, a.d, a.thr, x, y, z, d2, &s);
-                        if (q >= 0) { float w; gg.load(s, qx, qy, qz, w); }
-                    }
-                    if (CT) CT[ord ? ord[k] : k] = q;
-                    if (q >= 0) {
-                        ++cnt;
-                        acc += (unsigned long long)(d2 * scale);
-                        // the exact Umeyama terms of this correspondence, in quanta:
-                        // trunc(s'_a 2^k), trunc(t'_b 2^k), trunc(s'_a t'_b 2^k) -- the
-                        // scaling by 2^k is exact, so (s'_a 2^k) t'_b rounds to the
-                        // same value as (s'_a t'_b) 2^k; the sums (integers below
-                        // 2^52) are scaled back by 2^-k after the reduction
-                        const volatile double *skv = &sh.sk;
-                        const double sk = skv[0];
-                        const double sps[3] = {(x - c0x) * sk, (y - c0y) * sk, (z - c0z) * sk};
-                        const double tp[3] = {(double)qx - c0x, (double)qy - c0y, (double)qz - c0z};
-#pragma unroll
-                        for (int cc = 0; cc < 3; ++cc) {
-                            v[cc] = v[cc] + __builtin_trunc(sps[cc]);
-                            v[3 + cc] = v[3 + cc] + __builtin_trunc(tp[cc] * sk);
-#pragma unroll
-                            for (int e = 0; e < 3; ++e)
-                                v[6 + 3 * cc + e] = v[6 + 3 * cc + e] + __builtin_trunc(sps[cc] * tp[e]);
+                        put3(P3 + 3 * k, ox, oy, oz, wt);
+                        const int4 st = cst[k];
+                        need = true;
+                        if (st.x >= 0) {
+                            // D += this step's length (rounded up)
+                            const double dx = ox - x, dy = oy - y, dz = oz - z;
+                            const double Dn = (double)__int_as_float(st.z) +
+                                              __builtin_sqrt((dx * dx + dy * dy) + dz * dz) * (1.0 + 1e-9);
+                            float qx, qy, qz, qw;
+                            if constexpr (kLds) gl.load(st.x, qx, qy, qz, qw);
+                            else gg.load(st.x, qx, qy, qz, qw);
+                            const double d2 = dist2(ox, oy, oz, (double)qx, (double)qy, (double)qz);
+                            if (d2 < a.thr && __builtin_sqrt(d2) * (1.0 + 1e-9) <
+                                                  ((double)__int_as_float(st.y) - Dn) * (1.0 - 1e-12)) {
+                                need = false;
+                                put_step(cst + k, __float_as_int((float)(Dn * (1.0 + 1e-6) + 1e-30)), wt);
+                                if (CT) CT[ord ? ord[k] : k] = __float_as_int(qw);
+                                add_corr(v, cnt, acc, ox, oy, oz, qx, qy, qz, d2);
+                            }
                         }
                     }
                 }
+                // phase B: the positions needing a walk wait on the wave's stack and
+                // are walked 64 at a time (full waves)
+                const unsigned long long need_m = __ballot(need);
+                if (need) sh.pend[wid][np + __builtin_amdgcn_mbcnt_hi((unsigned)(need_m >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((unsigned)need_m, 0u))] = k;
+                np += __popcll(need_m);
+                if (np >= 64) {
+                    np -= 64;
+                    walk(sh.pend[wid][np + lane]);
+                }
             }
+            if (lane < np) walk(sh.pend[wid][lane]);  // the rest of the stack
         }
         mark(0);
         wave_park<kQ>(sh, v);
@@ -483,6 +563,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             for (int k = 0; k < 5; ++k) tt[k] = tph[k];
             tt[5] = __builtin_readcyclecounter() - t00;
             tt[6] = (unsigned long long)it;
+            tt[7] = (unsigned long long)sh.nwalk;
         }
     }
 }
@@ -511,6 +592,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     a.rel_rmse = prm->relative_rmse;
     a.max_iter = prm->max_iteration;
     a.P3 = nullptr;
+    a.cst = nullptr;
     a.srcp = nullptr;
     if (a.d > 0.0) {
         int rc = PCR_OK;
@@ -574,6 +656,8 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     char *ws = (char *)workspace(8, sizeof(double) * 3 * (size_t)P * nm + 64);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
     a.P3 = (double *)ws;
+    a.cst = (int4 *)workspace(38, sizeof(int4) * (size_t)P * nm + 64);
+    PCR_REQUIRE(a.cst, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
     if (a.G > 1 || two_phase) {
         const int gp = two_phase ? a.gmax2 : a.G;  // partial slots per pair
         char *cw = (char *)workspace(10, sizeof(XPart) * 2 * (size_t)gp * (size_t)P + 64);
@@ -641,12 +725,12 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         std::vector<unsigned long long> h(8 * (size_t)P);
         PCR_HIP_CHECK(hipMemcpyAsync(h.data(), a.timing, h.size() * 8, hipMemcpyDeviceToHost, s));
         PCR_HIP_CHECK(hipStreamSynchronize(s));
-        double m[7] = {0, 0, 0, 0, 0, 0, 0};
+        double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int q = 0; q < P; ++q)
-            for (int k = 0; k < 7; ++k) m[k] += (double)h[8 * q + k] / P;
+            for (int k = 0; k < 8; ++k) m[k] += (double)h[8 * q + k] / P;
         fprintf(stderr, "icp timing (clocks, mean over %d pairs, G=%d): sweep %.0f means %.0f cov %.0f "
-                "horn %.0f transform %.0f total %.0f iters %.2f\n", P, a.G, m[0], m[1], m[2], m[3], m[4],
-                m[5], m[6]);
+                "horn %.0f transform %.0f total %.0f iters %.2f walks (workgroup 0) %.0f\n", P, a.G, m[0], m[1],
+                m[2], m[3], m[4], m[5], m[6], m[7]);
     }
     return PCR_OK;
 }

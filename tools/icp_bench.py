@@ -35,7 +35,7 @@ for _ in range(10):
 e1.record()
 torch.cuda.synchronize()
 print(f"P={P} G={os.environ.get('PCR_COOP_G', 'auto')}: {e0.elapsed_time(e1) / 10:.3f} ms/launch, "
-      f"iters mean {res.stats[:, 0].float().mean().item():.2f}")
+      f"iters mean {res.stats[:, 0].float().mean().item():.2f}, fitness mean {res.fitness.mean().item():.3f}")
 if timing:
     os.environ["PCR_ICP_TIMING"] = timing
     reg.icp_batch(S, T, I, prm, want_corr=False)
