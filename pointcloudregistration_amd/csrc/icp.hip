@@ -30,6 +30,7 @@
 #include "grid.h"
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 namespace pcr {
@@ -71,10 +72,9 @@ struct IArgs {
     int *list;           // (P) listed pairs
     double *save;        // (P, kSave) the listed pairs' state
     XPart *part;         // (P, 2, G) when G > 1
-    // when G > 1: per pair 4 words at bar + 4 p -- the pair barrier (arrivals,
-    // generation) and, at chunk + 4 p, the sweep chunk counters by sweep parity
+    // when G > 1: per pair 4 words at bar + 4 p, the pair barrier (arrivals,
+    // generation)
     unsigned *bar;
-    int *chunk;
     unsigned long long *timing;  // debug (PCR_ICP_TIMING): per pair, phase clocks
 };
 
@@ -139,31 +139,52 @@ struct IShared {  // LDS header; the grid copy (if any) follows
     double T[16];     // the running transformation (init, then U * T per iteration)
     double U[12];     // this iteration's update
     int nred;         // reductions done (parity of the HBM partial slots)
-    int chunk[2];     // next 64-position chunk of the current sweep, by parity (G = 1)
+    int chunk[2];     // next 64-position chunk of this workgroup's range, by sweep parity
     int handoff;      // phase 1: this pair is listed for phase 2
     int pend[kWaves][128];  // per wave: positions waiting for a grid walk (a stack)
     int nwalk;        // debug (PCR_ICP_PHASES): walks done by this workgroup
 };
 
-// wave-level sums of NQ exact f64 values (integer multiples of the quantum:
-// the additions are exact, so the tree shape is free); lane 0 parks them in
-// sh.ws[wave][0..NQ)
-template <int NQ>
-__device__ __forceinline__ void wave_park(IShared &sh, double *v) {
+// wave-level sums of the kQ exact f64 values (integer multiples of the quantum:
+// the additions are exact, so the tree shape is free), parked in
+// sh.ws[wave][0..kQ).  A reduce-scatter butterfly: at each of the offsets 32,
+// 16, 8, 4 a lane keeps half of its values and adds its partner's copy of that
+// half (8 + 4 + 2 + 1 shuffles instead of 6 per value), then offsets 2, 1 finish
+// the one value left -- lane l ends with value (l >> 2) summed over the wave.
+__device__ __forceinline__ void wave_park(IShared &sh, const double *v) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double w[16];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
+    for (int q = 0; q < 16; ++q) w[q] = q < kQ ? v[q] : 0.0;
+    auto step = [&](auto hc) {
+        constexpr int h = decltype(hc)::value, o = 4 * h;
+        const bool up = (lane & o) != 0;  // keeps the upper half
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
-        if (lane == 0) sh.ws[wid][q] = v[q];
-    }
+        for (int i = 0; i < h; ++i) {
+            const double keep = up ? w[i + h] : w[i], send = up ? w[i] : w[i + h];
+            w[i] = keep + __shfl_xor(send, o, 64);
+        }
+    };
+    step(std::integral_constant<int, 8>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 1>{});
+    double t = w[0];
+    t += __shfl_xor(t, 2, 64);
+    t += __shfl_xor(t, 1, 64);
+    // lane bits 5..2 picked the half at offsets 32..4: lane l holds value
+    // (l >> 5 & 1) * 8 + (l >> 4 & 1) * 4 + (l >> 3 & 1) * 2 + (l >> 2 & 1)
+    const int q = lane >> 2;
+    if ((lane & 3) == 0 && q < kQ) sh.ws[wid][q] = t;
 }
 
 // sum the NV parked values + (cnt, acc) over the pair's workgroups; result in
 // sh.tot / sh.cnt / sh.acc (all threads call; ends with a barrier)
-template <int NV>
+// mk(ph): debug phase clocks (PCR_ICP_PHASES): 5 = the workgroup's waves
+// joined, 6 = the pair barrier passed
+template <int NV, typename Mark>
 __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int G, int cnt,
-                            unsigned long long acc) {
+                            unsigned long long acc, Mark mk) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -175,6 +196,7 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int G, in
         sh.wacc[wid] = acc;
     }
     __syncthreads();
+    mk(5);
     if (tid < NV + 2) {  // thread q sums quantity q (NV: count, NV+1: error sum)
         double s = 0.0;
         unsigned long long A = 0;
@@ -197,6 +219,7 @@ __device__ void pair_reduce(const IArgs &a, IShared &sh, int p, int g, int G, in
     }
     if (G > 1) {
         pair_barrier(a.bar + 4 * (size_t)p, G);
+        mk(6);
         if (tid < NV + 2) {
             const XPart *all = a.part + ((size_t)p * 2 + (sh.nred & 1)) * G;
             double s = 0.0;
@@ -252,6 +275,11 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     bool ident = true;
     for (int k = 0; k < 16; ++k) ident = ident && (sh.T[k] == ((k % 5 == 0) ? 1.0 : 0.0));
     const int stride = G * kThreads, base = g * kThreads + tid;
+    // the workgroup's share of the sweep order: 64-position chunks [c_lo, c_hi),
+    // the same in every sweep (its waves take them from an LDS counter), so a
+    // position's working copy and state are only ever touched by one workgroup
+    const int nch = (n + 63) >> 6;
+    const int c_lo = (int)((long long)nch * g / G), c_hi = (int)((long long)nch * (g + 1) / G);
     // the pair's reference point and quantum of the exact Umeyama sums
     // (oracle_icp_quantum): c0 = the first target point, 2^k from the largest
     // |t - c0| (every workgroup computes the same values)
@@ -282,7 +310,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         double T0[12];
         for (int q = 0; q < 12; ++q) T0[q] = sh.T[q];
         const float *Sp = (a.srcp && ord) ? a.srcp + (size_t)p * a.Nmax * 3 : nullptr;
-        for (int k = base; k < n; k += stride) {
+        for (int k = 64 * c_lo + tid; k < min(n, 64 * c_hi); k += kThreads) {
             const float *q = Sp ? Sp + 3 * k : S + 3 * (ord ? ord[k] : k);
             double x = (double)q[0], y = (double)q[1], z = (double)q[2];
             if (!ident) {
@@ -290,9 +318,8 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                 xform12(T0, x, y, z, ox, oy, oz);
                 x = ox; y = oy; z = oz;
             }
-            put3(P3 + 3 * k, x, y, z, G > 1);
+            put3(P3 + 3 * k, x, y, z, wt);
         }
-        if (G > 1) pair_barrier(a.bar + 4 * (size_t)p, G);  // (G = 1: the barrier below)
     }
     GridP4 gl{};
     GridView gg{};
@@ -313,7 +340,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
 #else
     const bool tmg = false;
 #endif
-    unsigned long long tph[6] = {0, 0, 0, 0, 0, 0}, tlast = tmg ? __builtin_readcyclecounter() : 0ull;
+    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = tmg ? __builtin_readcyclecounter() : 0ull;
     const unsigned long long t00 = tlast;
     auto mark = [&](int ph) {
         if (tmg) {
@@ -343,8 +370,7 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         {  // 64-query chunks of the spatial order taken from a counter (dense and
            // sparse regions cost different time); the counter of this sweep's
            // parity was re-armed after the previous sweep's reduction
-            int *ctr = G > 1 ? a.chunk + 4 * p + (nsweep & 1) : &sh.chunk[nsweep & 1];
-            const int nch = (n + 63) >> 6;
+            int *ctr = &sh.chunk[nsweep & 1];
             const double c0x = sh.c0[0], c0y = sh.c0[1], c0z = sh.c0[2];
             // the exact Umeyama terms of a correspondence, in quanta: trunc(s'_a
             // 2^k), trunc(t'_b 2^k), trunc(s'_a t'_b 2^k) -- the scaling by 2^k is
@@ -394,9 +420,9 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
             int np = 0;  // positions on this wave's stack
             for (;;) {
                 int c = 0;
-                if (lane == 0) c = G > 1 ? coop_fetch_add(ctr, 1) : atomicAdd(ctr, 1);
-                c = __shfl(c, 0, 64);
-                if (c >= nch) break;
+                if (lane == 0) c = atomicAdd(ctr, 1);
+                c = __shfl(c, 0, 64) + c_lo;
+                if (c >= c_hi) break;
                 const int k = (c << 6) + lane;
                 // phase A: transform; reuse the correspondence when certified
                 bool need = false;
@@ -444,18 +470,17 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                     walk(sh.pend[wid][np + lane]);
                 }
             }
+            mark(7);
             if (lane < np) walk(sh.pend[wid][lane]);  // the rest of the stack
         }
         mark(0);
-        wave_park<kQ>(sh, v);
-        pair_reduce<kQ>(a, sh, p, g, G, cnt, acc);
+        wave_park(sh, v);
+        mark(4);
+        pair_reduce<kQ>(a, sh, p, g, G, cnt, acc, mark);
         // every workgroup has left this sweep (pair_reduce's barrier): re-arm its
         // counter for the sweep after next (the next sweep uses the other one,
         // re-armed one reduction ago)
-        if (tid == 0 && g == 0) {
-            if (G > 1) __hip_atomic_store(a.chunk + 4 * p + (nsweep & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else sh.chunk[nsweep & 1] = 0;
-        }
+        if (tid == 0) sh.chunk[nsweep & 1] = 0;
         ++nsweep;
         mark(1);
         count = sh.cnt;
@@ -559,11 +584,11 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
         a.stats[2 * p] = it;
         a.stats[2 * p + 1] = valid ? count : 0;
         if (tmg) {
-            unsigned long long *tt = a.timing + (size_t)p * 8;
-            for (int k = 0; k < 5; ++k) tt[k] = tph[k];
-            tt[5] = __builtin_readcyclecounter() - t00;
-            tt[6] = (unsigned long long)it;
-            tt[7] = (unsigned long long)sh.nwalk;
+            unsigned long long *tt = a.timing + (size_t)p * 12;
+            for (int k = 0; k < 8; ++k) tt[k] = tph[k];
+            tt[8] = __builtin_readcyclecounter() - t00;
+            tt[9] = (unsigned long long)it;
+            tt[10] = (unsigned long long)sh.nwalk;
         }
     }
 }
@@ -663,33 +688,30 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         char *cw = (char *)workspace(10, sizeof(XPart) * 2 * (size_t)gp * (size_t)P + 64);
         PCR_REQUIRE(cw, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
         a.part = (XPart *)cw;
-        // barriers and chunk counters in a slot of their own, zeroed when
-        // allocated: every launch leaves the arrivals and the counters zero (a
-        // barrier resets its arrivals, a sweep re-arms its counter) and the
-        // barrier works from any generation, so no memset per call; the
+        // barriers in a slot of their own, zeroed when allocated: every launch
+        // leaves the arrivals zero (a barrier resets them) and the barrier
+        // works from any generation, so no memset per call; the
         // (pair, 4) layout does not move with P, and a power-of-two size either
         // fits the zeroed range or outgrows the slot's headroom (fresh, zeroed)
         size_t nb = 16384;
         while (nb < 4 * (size_t)P) nb <<= 1;
         // A launch that failed after some of its workgroups arrived could leave
-        // arrivals or counters behind: the call after any failed one re-zeroes.
+        // arrivals behind: the call after any failed one re-zeroes.
         bool fresh = false;
         a.bar = (unsigned *)workspace(39, sizeof(unsigned) * nb, &fresh);
         PCR_REQUIRE(a.bar, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
         if (fresh || t_icp_failed) PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * nb, s));
         t_icp_failed = false;
-        a.chunk = (int *)(a.bar + 2);
     } else {
         a.part = nullptr;
         a.bar = nullptr;
-        a.chunk = nullptr;
     }
     a.timing = nullptr;
     const bool want_timing = getenv("PCR_ICP_TIMING") != nullptr;
     if (want_timing) {
-        a.timing = (unsigned long long *)workspace(12, sizeof(unsigned long long) * 8 * (size_t)P);
+        a.timing = (unsigned long long *)workspace(12, sizeof(unsigned long long) * 12 * (size_t)P);
         PCR_REQUIRE(a.timing, PCR_ERR_NOMEM, "icp timing: %s", pcr_last_error());
-        PCR_HIP_CHECK(hipMemsetAsync(a.timing, 0, sizeof(unsigned long long) * 8 * (size_t)P, s));
+        PCR_HIP_CHECK(hipMemsetAsync(a.timing, 0, sizeof(unsigned long long) * 12 * (size_t)P, s));
     }
     if (two_phase) {
         char *tw = (char *)workspace(37, sizeof(int) * (2 + (size_t)P) + sizeof(double) * kSave * (size_t)P + 64);
@@ -722,15 +744,15 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     t_icp_failed = false;
     prof_end(s, kProfIcp);
     if (want_timing) {  // debug: phase split in shader clocks, mean over pairs, to stderr
-        std::vector<unsigned long long> h(8 * (size_t)P);
+        std::vector<unsigned long long> h(12 * (size_t)P);
         PCR_HIP_CHECK(hipMemcpyAsync(h.data(), a.timing, h.size() * 8, hipMemcpyDeviceToHost, s));
         PCR_HIP_CHECK(hipStreamSynchronize(s));
-        double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double m[11] = {};
         for (int q = 0; q < P; ++q)
-            for (int k = 0; k < 8; ++k) m[k] += (double)h[8 * q + k] / P;
-        fprintf(stderr, "icp timing (clocks, mean over %d pairs, G=%d): sweep %.0f means %.0f cov %.0f "
-                "horn %.0f transform %.0f total %.0f iters %.2f walks (workgroup 0) %.0f\n", P, a.G, m[0], m[1],
-                m[2], m[3], m[4], m[5], m[6], m[7]);
+            for (int k = 0; k < 11; ++k) m[k] += (double)h[12 * q + k] / P;
+        fprintf(stderr, "icp timing (clocks, mean over %d pairs, G=%d): chunks %.0f drain %.0f park %.0f join %.0f "
+                "pair-barrier %.0f partials %.0f means %.0f horn %.0f total %.0f iters %.2f walks (workgroup 0) %.0f\n",
+                P, a.G, m[7], m[0], m[4], m[5], m[6], m[1], m[2], m[3], m[8], m[9], m[10]);
     }
     return PCR_OK;
 }

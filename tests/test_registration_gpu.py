@@ -166,6 +166,39 @@ def test_icp_bitexact_vs_oracle(oracle, r, noise_init):
         assert int((_np(res.corr_tgt)[p] >= 0).sum()) == o["n_corr"]
 
 
+@pytest.mark.parametrize("P", [2, 300])
+def test_icp_correspondence_reuse_stress(oracle, P):
+    """The sweep reuses a point's last correspondence while its clearance bound
+    certifies it (icp.hip CorrState).  Adversarial inputs for that certificate: a
+    lattice target with exact duplicate points (ties broken by the lowest index),
+    sources on the lattice's mid-planes (near-equidistant targets), and 30 full
+    iterations of ever smaller motion (relative criteria 0).  P = 2: G > 1
+    workgroups per pair; P = 300: one workgroup per pair plus the tail launch."""
+    rng = np.random.default_rng(11)
+    g = np.stack(np.meshgrid(*[np.arange(12)] * 3, indexing="ij"), -1).reshape(-1, 3) * 0.01
+    n = 1500
+    S = np.zeros((P, n, 3), np.float32)
+    T = np.zeros((P, g.shape[0] + 64, 3), np.float32)
+    init = np.zeros((P, 4, 4))
+    for p in range(P):
+        t = g + rng.normal(0, 0.0005 if p % 2 else 0.0, g.shape)
+        t = np.concatenate([t, t[rng.choice(len(t), 64, replace=False)]])  # exact duplicates
+        T[p] = t
+        s = t[rng.choice(len(t), n)] + 0.005 * (rng.random((n, 3)) < 0.3)  # some on mid-planes
+        S[p] = s + rng.normal(0, 0.002, s.shape)
+        init[p, :3, :3] = synth.rotation_xyz(*rng.normal(0, 0.01, 3))
+        init[p, :3, 3] = rng.normal(0, 0.004, 3)
+        init[p, 3, 3] = 1
+    prm = reg.IcpParams(0.012, relative_fitness=0.0, relative_rmse=0.0, max_iteration=30)
+    res = reg.icp_batch(S, T, init, prm)
+    for p in list(range(min(P, 4))) + [P - 1]:
+        o = oracle.icp(S[p], T[p], 0.012, init=init[p], relative_fitness=0.0, relative_rmse=0.0)
+        assert _bits_equal(_np(res.transformation)[p], o["T"]), p
+        assert _bits_equal(_np(res.fitness)[p], o["fitness"]), p
+        assert _bits_equal(_np(res.inlier_rmse)[p], o["inlier_rmse"]), p
+        assert tuple(_np(res.stats)[p]) == (o["iters"], o["n_corr"]), p
+
+
 def test_radius_nn_vs_oracle_bruteforce(oracle):
     rng = np.random.default_rng(2)
     tgt = (rng.random((2, 3000, 3)) * 2 - 1).astype(np.float32)
