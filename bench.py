@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured: no gain at 256 pairs, "
                          "slower at 32 / 64 where the cooperative launches are recorded)")
+    ap.add_argument("--s8d-chunks", type=int, default=0,
+                    help="s8d_job: copy chunks per rank (0: by shard size)")
+    ap.add_argument("--s8d-lanes", type=int, default=0,
+                    help="s8d_job: chunk pipelines in flight (0: 1)")
     ap.add_argument("--streams", type=int, default=1,
                     help="split the rank's shard into this many sub-batches run concurrently on "
                          "their own HIP streams (1..4)")
@@ -882,17 +886,18 @@ def grid_candidates(src, tgt, T, d):
 
 # Per 32 x 32 tile and wave, the inner loop of the shipped build's screens
 # (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 8
-# column tiles, D = 32 -> NCH = 7 k-chunks of 16):
-#  pass 1 featnn_row7<2,8,true,2>:  7 v_mfma_f32_32x32x16_f16, 48 VALU (32 v_med3
-#    for the top-2 update, 16 v_and_or packing the column code), 3.5 ds_read_b128
-#    (each B fragment shared by the 2 row tiles), ~1.2 SALU;
-#  pass 2 featnn_row7<2,8,false,2>: 7 MFMA, 32 v_med3 (values only), 3.5 LDS,
+# column tiles = 16 tiles, D = 32 -> NX = 7 k-chunks of 16):
+#  pass 1 featnn_row8<2,8,true>:  7 v_mfma_f32_32x32x16_f16, 40.1 VALU per tile
+#    (16 v_and_or_b32 tagging the u32 distance bits with the column code, and the
+#    pairs top-2 update: 8 v_med3 + 8 v_min3_u32 + 8 v_min_u32), 2.5 ds_read_b128,
+#    1.4 SALU, 0.25 s_nop;
+#  pass 2 featnn_row8<2,8,false>: 7 MFMA, 24.1 VALU (values only: no tag), 2.5 LDS,
 #    0.44 s_nop.
 # SIMD issue cycles (MI355X guide, 'vector-instruction ISSUE cost'): an MFMA holds
 # vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the two waves of a
 # SIMD share that port.  The MFMA pipe needs 7 x 32 = 224 cycles per tile.
-SCREEN_TILE_ISSUE = {"mfma": 7 * 8, "valu": 48 * 4, "lds": 3.5 * 4}
-SCREEN2_TILE_ISSUE = {"mfma": 7 * 8, "valu": 32 * 4, "lds": 3.5 * 4, "s_nop": 0.44 * 4}
+SCREEN_TILE_ISSUE = {"mfma": 7 * 8, "valu": 642 / 16 * 4, "lds": 40 / 16 * 4, "s_nop": 4 / 16 * 4}
+SCREEN2_TILE_ISSUE = {"mfma": 7 * 8, "valu": 386 / 16 * 4, "lds": 40 / 16 * 4, "s_nop": 7 / 16 * 4}
 
 
 def _screen_issue_model(tiles, ms, table):
@@ -1059,19 +1064,25 @@ def measure_host_resident(batch, params, pair_ids, steps, warmup, world, total_p
                     "batch's pipeline; records all-gathered and copied back to the host"}
 
 
-def measure_s8d_job(batch, params, pair_ids, world, total_pairs, warmup=3, runs=10):
+def measure_s8d_job(batch, params, pair_ids, world, total_pairs, warmup=3, runs=10, chunks=None,
+                    lanes=None):
     """SURVEY 8d / BASELINE.md's C4 definition, literally: throughput = the job's
     pairs / the wall time of ONE job from "inputs resident on the host" to "all
     (R,t) gathered on rank 0" (H2D and the RCCL gather included, data generation
     excluded); 3 warm-up jobs, the median of 10.  Each job is a synchronous unit
-    (nothing carried over from the previous one); inside it the rank's shard is
-    split into C chunks whose H2D copy (pinned host -> HBM, own stream) overlaps
-    the pipeline of the previous chunk, so the job costs ~ one chunk's copy plus
-    the C pipelines instead of the whole copy plus the pipeline."""
+    (nothing carried over from the previous one).  Inside it the rank's shard is
+    split into C chunks copied in order (pinned host -> HBM, one copy stream);
+    chunk c's pipeline runs as soon as its copy lands, on the current stream
+    (lanes > 1: chunk c on lane c mod L, each lane its own stream and libpcr
+    workspace context).  The job then costs about the whole copy (PCIe-bound:
+    ~41 us per pair at 56 GB/s) plus the last chunk's pipeline."""
+    from pointcloudregistration_amd import _lib
     from pointcloudregistration_amd.multigpu import gather_records
     from pointcloudregistration_amd.pipeline import PairPipeline
     P = batch.src.shape[0]
-    C = 4 if P >= 128 else (2 if P >= 32 else 1)
+    C = chunks or (4 if P >= 128 else (2 if P >= 32 else 1))
+    C = max(1, min(C, P))
+    L = max(1, min(lanes or 1, C, 4))
     bounds = [P * c // C for c in range(C + 1)]
     hosts, devs, pipes = [], [], []
     for c in range(C):
@@ -1081,40 +1092,59 @@ def measure_s8d_job(batch, params, pair_ids, world, total_pairs, warmup=3, runs=
         d = [torch.empty(t.shape, dtype=t.dtype, device="cuda") for t in h]
         hosts.append(h)
         devs.append(d)
-        pipes.append(PairPipeline(*d, params, pair_ids=pair_ids[a:b]))
+        pipes.append(PairPipeline(*d, params, pair_ids=pair_ids[a:b], context=c % L))
     rows = -(-total_pairs // world)
     rec_host = torch.empty((rows * world, 40), dtype=torch.float64).pin_memory()
     rec_dev = torch.empty((P, 40), dtype=torch.float64, device="cuda")
-    copy_s = torch.cuda.Stream()
+    # the copies on a high-priority stream (torch's pool of those): measured
+    # (tools/s8d_probe.py) a copy stream that shares a hardware queue with the
+    # pipeline's stream serialises the chunk pipelines behind every copy (25.6 vs
+    # 13.7 ms per job); lane 0 is the current stream, more lanes measured slower
+    # (two 32-pair pipelines in flight: 13.4-16.4 ms, box to box)
+    copy_s = torch.cuda.Stream(priority=-1)
     comp = torch.cuda.current_stream()
+    lane_s = [comp] + [torch.cuda.Stream() for _ in range(L - 1)]
     copied = [torch.cuda.Event() for _ in range(C)]
+    if L > 1:
+        _lib.call("pcr_set_concurrency", L)
 
     def job():
+        for s_ in lane_s[1:]:
+            s_.wait_stream(comp)
         with torch.cuda.stream(copy_s):
             for c in range(C):
                 for d, h in zip(devs[c], hosts[c]):
                     d.copy_(h, non_blocking=True)
                 copied[c].record(copy_s)
         for c in range(C):
-            comp.wait_event(copied[c])
-            pipes[c].run()
-            rec_dev[bounds[c]:bounds[c + 1]].copy_(pipes[c].records())
+            s_ = lane_s[c % L]
+            s_.wait_event(copied[c])
+            with torch.cuda.stream(s_):
+                pipes[c].run()
+                rec_dev[bounds[c]:bounds[c + 1]].copy_(pipes[c].records())
+        for s_ in lane_s[1:]:
+            comp.wait_stream(s_)
         rec = gather_records(rec_dev, world, rows)
         rec_host.copy_(rec, non_blocking=True)
         torch.cuda.synchronize()
 
-    for _ in range(warmup):
-        job()
-    times = []
-    for _ in range(runs):
-        barrier(world)
-        t0 = time.perf_counter()
-        job()
-        times.append(max_over_ranks(time.perf_counter() - t0, world))
+    try:
+        for _ in range(warmup):
+            job()
+        times = []
+        for _ in range(runs):
+            barrier(world)
+            t0 = time.perf_counter()
+            job()
+            times.append(max_over_ranks(time.perf_counter() - t0, world))
+    finally:
+        if L > 1:
+            _lib.call("pcr_set_concurrency", 1)
     med = float(np.median(times))
     return {"value": total_pairs / med, "unit": "pairs/s", "ms_per_job": med * 1e3,
             "ms_per_job_min": min(times) * 1e3, "ms_per_job_max": max(times) * 1e3,
-            "warmup_jobs": warmup, "timed_jobs": runs, "chunks_per_rank": C,
+            "warmup_jobs": warmup, "timed_jobs": runs, "chunks_per_rank": C, "pipelines_in_flight": L,
+            "records": rec_host[:total_pairs].clone(),
             "note": "SURVEY 8d: one job of the whole C4 batch, pinned host inputs -> (R,t) records "
                     "all-gathered and on the host of rank 0; median of 10 after 3 warm-ups; the "
                     "contract's `value` is the HBM-resident rate (inputs already on the GPU)"}
@@ -1217,7 +1247,7 @@ def main():
     stages = dict(zip(("feature_match", "corres+ransac", "icp", "transform", "chamfer"),
                       pipe.stage_ms()))
 
-    # dominant kernel: pass 1 of the feature screen, featnn_row7 (one launch = the
+    # dominant kernel: pass 1 of the feature screen, featnn_row8 (one launch = the
     # source->target row screen of all P pairs, index packed in).  Algorithmic
     # work: the P*N*M*D MACs of the distance matrix = 2*P*N*M*D flops,
     # which pass 1 computes in full; pass 2 re-screens only the target rows J that
@@ -1284,24 +1314,24 @@ def main():
                    "inputs": "resident in HBM (see host_resident for the PCIe-inclusive rate)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_F16_MFMA_TFLOPS,
-                     "traffic": _pmc_traffic("featnn_row7<", "true"),
+                     "traffic": _pmc_traffic("featnn_row8<", "true"),
                      "traffic_source": f"{_traffic_source()} (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this bench; FETCH_SIZE x2 per the "
                                        "gfx950 note)",
-                     "kernel": "featnn_row7<2,8,true,2> (pass 1: v_mfma_f32_32x32x16_f16, f16x3 "
-                               "split, row top-2 with packed column code)",
+                     "kernel": "featnn_row8<2,8,true> (pass 1: v_mfma_f32_32x32x16_f16, f16x3 "
+                               "split, row top-2 on biased u32 bits tagged with the column code)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,
                      "executed_mfma_tflops": executed,
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS,
                      "issue_model": _screen_issue_model(tiles1, per_launch_ms, SCREEN_TILE_ISSUE),
-                     "pass2": {"kernel": "featnn_row7<2,8,false,2> (target rows J = unique(nn12), "
+                     "pass2": {"kernel": "featnn_row8<2,8,false> (target rows J = unique(nn12), "
                                          "values only)",
                                "kernel_ms_per_launch": per2_ms, "launches": launches2,
                                "j_rows_mean": float(jrows.mean()),
                                "flops_per_launch": 2.0 * float(jrows.sum()) * N * D,
-                               "traffic": _pmc_traffic("featnn_row7<", "false"),
+                               "traffic": _pmc_traffic("featnn_row8<", "false"),
                                "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN2_TILE_ISSUE)},
                      "screen_stage": {"ms_per_launch": stage_ms, "achieved": stage_tf,
                                       "frac": stage_tf / PEAK_F16_MFMA_TFLOPS,
@@ -1325,10 +1355,18 @@ def main():
     if not args.no_host_resident:
         del pipe
         torch.cuda.empty_cache()
+        # the s8d job first: its copy stream must not share a hardware queue with
+        # the pipeline's (measured: a job after the host_resident leg's streams
+        # took 16.3 ms, first 13.8)
+        job = measure_s8d_job(batch, params, pair_ids, world, args.pairs, chunks=args.s8d_chunks,
+                              lanes=args.s8d_lanes)
+        # the job's records are the headline step's, bit for bit
+        job["records_equal_headline"] = bool(np.array_equal(job.pop("records").numpy(),
+                                                            recs[:args.pairs]))
+        torch.cuda.empty_cache()
         out["host_resident"] = measure_host_resident(batch, params, pair_ids, args.steps,
                                                      args.warmup, world, args.pairs)
-        torch.cuda.empty_cache()
-        out["s8d_job"] = measure_s8d_job(batch, params, pair_ids, world, args.pairs)
+        out["s8d_job"] = job
     if world > 1:
         # secondary: weak scaling, `pairs` pairs on EVERY rank
         wfirst = rank * args.pairs

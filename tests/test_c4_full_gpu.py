@@ -156,9 +156,17 @@ def test_sampled_pairs_bitexact_vs_oracle(c4, oracle, p):
     assert np.isclose(c4["rec"][p, 36], ch, rtol=1e-6)
 
 
-def test_graph_replay_equals_eager(c4):
-    """bench.py's headline replays the step as one captured HIP graph: the same
-    records bit for bit as the eager step, replay after replay."""
+@pytest.mark.parametrize("tail", ["1", "0"])
+def test_graph_replay_equals_eager(c4, tail, monkeypatch):
+    """`bench.py --graph` replays the step as one captured HIP graph: the same
+    records bit for bit as the eager step, replay after replay.  At 256 pairs
+    the step's ICP is one workgroup per pair plus, by default, the tail
+    hand-off's second launch -- a cooperative one (its pair barriers need its
+    workgroups co-resident), which the graph records as a node; the replays
+    are checked with the hand-off (PCR_ICP_TAIL=1) and without it (0: one
+    plain launch).  The eager records are the same either way (G is
+    bit-neutral)."""
+    monkeypatch.setenv("PCR_ICP_TAIL", tail)
     b = c4["batch"]
     pipe = PairPipeline(b.src, b.tgt, b.src_feat, b.tgt_feat, c4["params"],
                         pair_ids=np.arange(P, dtype=np.int32), graph=True)
@@ -166,7 +174,7 @@ def test_graph_replay_equals_eager(c4):
         pipe.run()
         torch.cuda.synchronize()
         assert _bits(pipe.records().cpu().numpy(), c4["rec"])
-    assert pipe._graph is not None  # 256 pairs: no cooperative launch, capturable
+    assert pipe._graph is not None  # captured (the runtime recorded every launch)
 
 
 def test_graph_small_shard_equals_eager():

@@ -3,7 +3,7 @@
 branch back to it; reports per-loop counts of MFMA / VALU / LDS / SALU / s_nop /
 waitcnt, used for the issue models in bench.py and DESIGN.md.
 
-usage: python tools/isa_loop_mix.py featnn.s 'featnn_row7ILi7ELi8ELb1ELi2E'"""
+usage: python tools/isa_loop_mix.py featnn.s 'featnn_row8ILi2ELi8ELb1E'"""
 import re
 import sys
 from collections import Counter

@@ -21,5 +21,5 @@ run() {
 }
 run a SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES || exit 1
 run b SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES || exit 1
-python3 tools/sq_summary.py "$OUT" featnn_row7 ransac_sweep icp_kernel nng_query featnn_rescan3 > "$OUT/summary.json"
+python3 tools/sq_summary.py "$OUT" featnn_row8 ransac_sweep icp_kernel nng_query featnn_rescan3 > "$OUT/summary.json"
 cat "$OUT/summary.json"
