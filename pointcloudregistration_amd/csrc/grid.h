@@ -20,9 +20,25 @@ __device__ __forceinline__ int cell_coord(double v, double cell) {
     return (int)__builtin_floor(v / cell);
 }
 
+// Slot of cell (x, y, z): the three coordinates' low 10 bits packed into one
+// word, then murmur3's 32-bit finaliser.  (The classic x*73856093 ^ y*19349663 ^
+// z*83492791 collides on small coordinate ranges: a C4 target at d = 0.04 has
+// 1,365 cells but only 1,105 distinct 32-bit values, so a RANSAC query walked
+// ~56 candidates where its own cells held ~34; with this mix ~40.)  Cells 1024
+// apart share a slot -- collisions only add candidates.
+__device__ __forceinline__ unsigned cell_key(int x, int y, int z) {
+    return ((unsigned)x & 1023u) | (((unsigned)y & 1023u) << 10) | (((unsigned)z & 1023u) << 20);
+}
+__device__ __forceinline__ unsigned key_slot(unsigned k, int S) {
+    k ^= k >> 16;
+    k *= 0x85ebca6bu;
+    k ^= k >> 13;
+    k *= 0xc2b2ae35u;
+    k ^= k >> 16;
+    return k & (unsigned)(S - 1);
+}
 __device__ __forceinline__ unsigned cell_hash(int x, int y, int z, int S) {
-    return (((unsigned)x * 73856093u) ^ ((unsigned)y * 19349663u) ^ ((unsigned)z * 83492791u)) &
-           (unsigned)(S - 1);
+    return key_slot(cell_key(x, y, z), S);
 }
 
 // view of one pair's grid in HBM: one float4 per point (x, y, z, index bits)
@@ -155,9 +171,9 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
         axis_gaps(py, y0, y1, g.cell, gy);
         axis_gaps(pz, z0, z1, g.cell, gz);
         const float lim32 = (float)(thr * (1.0 + 1e-6));
-        const unsigned hx[2] = {(unsigned)x0 * 73856093u, (unsigned)(x0 + 1) * 73856093u};
-        const unsigned hy[2] = {(unsigned)y0 * 19349663u, (unsigned)(y0 + 1) * 19349663u};
-        const unsigned hz[2] = {(unsigned)z0 * 83492791u, (unsigned)(z0 + 1) * 83492791u};
+        const unsigned hx[2] = {(unsigned)x0 & 1023u, (unsigned)(x0 + 1) & 1023u};
+        const unsigned hy[2] = {((unsigned)y0 & 1023u) << 10, ((unsigned)(y0 + 1) & 1023u) << 10};
+        const unsigned hz[2] = {((unsigned)z0 & 1023u) << 20, ((unsigned)(z0 + 1) & 1023u) << 20};
         unsigned q[8];
         int nq = 0, total = 0;
 #pragma unroll
@@ -167,7 +183,7 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
                             (gx[ix] + gy[iy]) + gz[iz] <= lim32;
             q[c] = 0u;
             if (in) {
-                const unsigned h = (hx[ix] ^ hy[iy] ^ hz[iz]) & (unsigned)(g.S - 1);
+                const unsigned h = key_slot(hx[ix] | hy[iy] | hz[iz], g.S);
                 const int lo = (int)g.start[h], hi = (int)g.start[h + 1];
                 if (hi > lo) {
                     // compact: the k-th non-empty range goes to q[k]
@@ -317,6 +333,6 @@ int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double ce
 
 // host: allocate (workspace slot) + build; returns PCR_OK or error
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r,
-                hipStream_t s, int ws_slot, GridBatch &out);
+                hipStream_t s, int ws_slot, GridBatch &out, double cell_factor = 2.01);
 
 }  // namespace pcr

@@ -201,7 +201,7 @@ int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double ce
 }
 
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r, hipStream_t s,
-                int ws_slot, GridBatch &out) {
+                int ws_slot, GridBatch &out, double cell_factor) {
     int S = 256;
     while (S < Mmax) S <<= 1;
     const size_t cnt_b = sizeof(int) * (size_t)P * S;
@@ -214,7 +214,7 @@ int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double 
     a.n_tgt = n_tgt;
     a.Mmax = Mmax;
     a.S = S;
-    a.cell = 2.01 * r;
+    a.cell = cell_factor * r;
     a.cnt = (int *)ws;
     a.start = (int *)(ws + cnt_b);
     size_t off = (cnt_b + start_b + 15) & ~size_t(15);

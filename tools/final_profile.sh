@@ -1,8 +1,10 @@
-# Round evidence for profiles/rNN/ (ROUND=r05 TAG=vN; the profiled runs with
-# PCR_ICP_TAIL=0: ICP's second, cooperative launch makes the process fault at
-# exit under rocprofv3): the -m gpu suite, smoke, the
-# default bench line (all legs), the 32 / 64-pair shards, the kernel stats of the
-# 256-pair bench, PMC traffic and SQ counters, the C5 / f4 kernel stats.
+# Round evidence for profiles/rNN/ (ROUND=r05 TAG=vN): the -m gpu suite, smoke,
+# the default bench line (all legs), the 32 / 64-pair shards, the kernel stats of
+# the 256-pair bench, PMC traffic and SQ counters, the C5 / f4 kernel stats.  The
+# profiled and PMC runs here use one ICP launch (PCR_ICP_TAIL=0) because the tail
+# hand-off's cooperative launch makes the process fault at exit under the profiler
+# (the HIP runtime) and nothing may run after a fault in the same
+# call; tools/final_profile_tail.sh profiles the shipped path in a call of its own.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
