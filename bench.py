@@ -801,7 +801,12 @@ def grid_walk_replay(q, c, max_ring=3):
     S = 256
     while S < len(c):
         S <<= 1
-    qh = ((qc[:, 0] * 73856093) ^ (qc[:, 1] * 19349663) ^ (qc[:, 2] * 83492791)) & (S - 1)
+    k = ((qc[:, 0] & 1023) | ((qc[:, 1] & 1023) << 10) | ((qc[:, 2] & 1023) << 20)).astype(np.uint64)
+    for sh, mul in ((16, 0x85ebca6b), (13, 0xc2b2ae35), (16, None)):  # nng.h nhash (murmur3 fmix32)
+        k ^= k >> np.uint64(sh)
+        if mul is not None:
+            k = (k * np.uint64(mul)) & np.uint64(0xffffffff)
+    qh = (k & np.uint64(S - 1)).astype(np.int64)
     return trips[np.argsort(qh, kind="stable")], float(far.mean())
 
 
