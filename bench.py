@@ -862,15 +862,29 @@ def _chamfer_roofline(prof, P, N, samples):
             "traffic": _pmc_traffic("nng_query"), "bytes_per_launch": nbytes}
 
 
+def _slot_of(c, S):
+    """grid.h cell_hash on integer cell coordinates c (..., 3): the low 10 bits of
+    each packed, murmur3's 32-bit finaliser, & (S - 1)."""
+    k = ((c[..., 0] & 1023) | ((c[..., 1] & 1023) << 10) | ((c[..., 2] & 1023) << 20)).astype(np.uint64)
+    for sh, mul in ((16, 0x85ebca6b), (13, 0xc2b2ae35), (16, None)):
+        k ^= k >> np.uint64(sh)
+        if mul is not None:
+            k = (k * np.uint64(mul)) & np.uint64(0xffffffff)
+    return (k & np.uint64(S - 1)).astype(np.int64)
+
+
 def grid_candidates(src, tgt, T, d):
     """Mean candidates c_bar examined per radius-d grid query of src (through T)
     against tgt: a host replay of grid.h's walk (cells 2.01 d, the <=2x2x2 cells
-    of the 1.001 d box that the cell-gap test keeps; hash collisions ignored)."""
+    of the 1.001 d box that the cell-gap test keeps, each kept cell's hash slot
+    walked whole -- points of other cells in the same slot included)."""
     cell = 2.01 * d
     thr = float(np.float32(d * d))
+    S = 256
+    while S < len(tgt):
+        S <<= 1
     kt = np.floor(tgt.astype(np.float64) / cell).astype(np.int64)
-    key = lambda c: (c[..., 0] * 1_000_003 + c[..., 1]) * 1_000_033 + c[..., 2]  # noqa: E731
-    uk, cnt = np.unique(key(kt), return_counts=True)
+    slot_cnt = np.bincount(_slot_of(kt, S), minlength=S)
     p = src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]
     lo = np.floor((p - 1.001 * d) / cell).astype(np.int64)
     hi = np.floor((p + 1.001 * d) / cell).astype(np.int64)
@@ -882,10 +896,7 @@ def grid_candidates(src, tgt, T, d):
                 ok = np.all(c <= hi, axis=1)
                 gap = np.maximum(np.maximum(c * cell - p, p - (c + 1) * cell), 0.0)
                 ok &= (gap * gap).sum(1) <= thr
-                k = key(c)
-                pos = np.clip(np.searchsorted(uk, k), 0, len(uk) - 1)
-                hit = ok & (uk[pos] == k)
-                total += np.where(hit, cnt[pos], 0)
+                total += np.where(ok, slot_cnt[_slot_of(c, S)], 0)
     return float(total.mean())
 
 
