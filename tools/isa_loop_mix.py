@@ -58,7 +58,7 @@ def main():
             c[classify(t[0])] += 1
             if classify(t[0]) == "valu":
                 ops[t[0]] += 1
-        if c["mfma"]:
+        if c["mfma"] or "--all" in sys.argv:
             print(f"loop {tgt} lines {j}-{i}: {dict(c)}")
             print("   valu:", ", ".join(f"{k} {v}" for k, v in ops.most_common(12)))
 
