@@ -126,15 +126,19 @@ __device__ __forceinline__ void axis_gaps(double p, int c0, int c1, double cell,
 // LDS loads overlap.  The update order (slot order, strict < then lower index
 // on ties) makes the result independent of both.
 // kSlot: also report the winner's slot (its coordinates are g.x/y/z[slot])
-// kClear: also report in *s2out the second smallest computed d2 over EVERY
-// examined candidate (inside the radius or not; +inf when fewer than two) --
-// with the walk's guarantee that every unexamined target lies farther than r
-// from p, min(sqrt(s2), r) bounds the distance from p to any target other
-// than the winner (icp.hip's correspondence reuse)
+// kClear (icp.hip's correspondence reuse): also report the smallest and the
+// second smallest d2 computed over EVERY examined candidate (inside the radius
+// or not; +inf when there are fewer) in s12out[0..1], and in s12out[2] a lower
+// bound rho^2 on the squared distance from p to any target the walk did NOT
+// examine: the distance to the faces of the walked block of cells and the
+// gaps of its skipped cells (each shrunk by the build's rounding slack; the
+// general walk reports (min(r, sqrt(thr)) (1 - 1e-6))^2).  So every target
+// lies at least min(sqrt(s1), rho) from p, and every target other than the
+// winner at least min(sqrt(s2), rho).
 template <typename View, bool kSlot = false, int kW = 2, bool kClear = false>
 __device__ __forceinline__ int grid_query_exact(const View &g, double r, double thr, double px,
                                                 double py, double pz, double &d2out, int *slot = nullptr,
-                                                double *s2out = nullptr) {
+                                                double *s12out = nullptr) {
     const QueryBox bx = query_box(px, py, pz, 1.001 * r * g.inv_cell, g.inv_cell);
     const int x0 = bx.x0, x1 = bx.x1, y0 = bx.y0, y1 = bx.y1, z0 = bx.z0, z1 = bx.z1;
     const double lim = thr * (1.0 + 1e-9);
@@ -146,6 +150,11 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
             e1 = __builtin_fmin(e1, d);
         }
     };
+    double rho2 = 0.0;
+    if constexpr (kClear) {
+        const double rl = __builtin_fmin(r, __builtin_sqrt(thr)) * (1.0 - 1e-6);
+        rho2 = rl * rl;
+    }
     int bj = -1, bs = -1;
     auto take = [&](int s) {
         float ax, ay, az, aw;
@@ -171,6 +180,7 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
         axis_gaps(py, y0, y1, g.cell, gy);
         axis_gaps(pz, z0, z1, g.cell, gz);
         const float lim32 = (float)(thr * (1.0 + 1e-6));
+        float skip_min = __builtin_inff();  // kClear: smallest gap^2 of a skipped cell of the block
         const unsigned hx[2] = {(unsigned)x0 & 1023u, (unsigned)(x0 + 1) & 1023u};
         const unsigned hy[2] = {((unsigned)y0 & 1023u) << 10, ((unsigned)(y0 + 1) & 1023u) << 10};
         const unsigned hz[2] = {((unsigned)z0 & 1023u) << 20, ((unsigned)(z0 + 1) & 1023u) << 20};
@@ -179,8 +189,11 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const int ix = c >> 2, iy = (c >> 1) & 1, iz = c & 1;
-            const bool in = x0 + ix <= x1 && y0 + iy <= y1 && z0 + iz <= z1 &&
-                            (gx[ix] + gy[iy]) + gz[iz] <= lim32;
+            const bool inb = x0 + ix <= x1 && y0 + iy <= y1 && z0 + iz <= z1;
+            const float gsum = (gx[ix] + gy[iy]) + gz[iz];
+            const bool in = inb && gsum <= lim32;
+            if constexpr (kClear)
+                if (inb && !in) skip_min = __builtin_fminf(skip_min, gsum);
             q[c] = 0u;
             if (in) {
                 const unsigned h = key_slot(hx[ix] | hy[iy] | hz[iz], g.S);
@@ -194,6 +207,18 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
                     total += hi - lo;
                 }
             }
+        }
+        if constexpr (kClear) {
+            // faces of the walked block [x0, x1+1] x ... (cells by floor(v / cell):
+            // the relative 1e-12 slack of axis_gaps), then the skipped cells (f32
+            // sums of f32-rounded squares: -2^-20 relative covers them)
+            auto face = [&](double p, int c0, int c1) {
+                const double lo = (double)c0 * g.cell, hi = (double)(c1 + 1) * g.cell;
+                const double eps = 1e-12 * (__builtin_fabs(lo) + __builtin_fabs(hi) + g.cell);
+                return __builtin_fmax(__builtin_fmin(p - lo, hi - p) - eps, 0.0);
+            };
+            const double b = __builtin_fmin(__builtin_fmin(face(px, x0, x1), face(py, y0, y1)), face(pz, z0, z1));
+            rho2 = __builtin_fmin(b * b * (1.0 - 1e-12), (double)skip_min * (1.0 - 0x1p-20));
         }
         int s = (int)(q[0] & 0xffffu), e = (int)(q[0] >> 16);
         // up to two candidates per step, both from the current range (one site
@@ -273,7 +298,11 @@ __device__ __forceinline__ int grid_query_exact(const View &g, double r, double 
     }
     d2out = best;
     if constexpr (kSlot) *slot = bs;
-    if constexpr (kClear) *s2out = e2;
+    if constexpr (kClear) {
+        s12out[0] = e1;
+        s12out[1] = e2;
+        s12out[2] = rho2;
+    }
     return bj;
 }
 

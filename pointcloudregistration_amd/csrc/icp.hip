@@ -93,14 +93,17 @@ __device__ __forceinline__ void put3(double *q, double x, double y, double z, bo
     }
 }
 
-// Correspondence reuse.  A point's grid walk also reports the second smallest
-// distance it computed; with every unexamined target farther than ~r, that
-// gives a clearance c: every target other than the winner w lies at least c
-// from the point.  Moved since by at most D (the summed step lengths), the
-// point is still strictly nearest to w -- the walk would return w, with the same
-// d2 bits -- while |p - w| < c - D and d2 < thr.  Such a point skips the walk.
-// Per position, int4 {w's grid slot or -1, c (f32, rounded down), D (f32,
-// rounded up), unused}; rewritten by every walk (D = 0).
+// Correspondence reuse.  A point's grid walk also reports the two smallest
+// distances it computed and a lower bound rho on the distance to any target it
+// did not examine (grid.h kClear), which give a clearance c: every target other
+// than the winner w lies at least c = min(second smallest, rho) from the point
+// (with no correspondence: every target at least min(smallest, rho)).  Moved
+// since by at most D (the summed step lengths), the point is still strictly
+// nearest to w -- the walk would return w, with the same d2 bits -- while
+// |p - w| < c - D and d2 < thr; without one it still has none while c - D >
+// sqrt(thr).  Such a point skips the walk.  Per position, int4 {w's grid slot
+// or -1, c (f32, rounded down), D (f32, rounded up), unused}; rewritten by every
+// walk (D = 0).
 __device__ __forceinline__ void put_state(int4 *q, int4 v, bool wt) {
     if (wt) {
         int *w = reinterpret_cast<int *>(q);
@@ -329,9 +332,6 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     }
     __syncthreads();
     const double scale = fx_scale(a.thr);
-    // every target a walk did not examine lies at least this far from the query
-    // (outside the query box: >= r; in a skipped cell: > sqrt(thr))
-    const double rclr = __builtin_fmin(a.d, __builtin_sqrt(a.thr)) * (1.0 - 1e-6);
     const int wid = tid >> 6;
     // debug phase clocks (s_memtime) of workgroup 0's thread 0: only in a build
     // with -DPCR_ICP_PHASES (the registers they hold cost the normal build)
@@ -402,18 +402,21 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
 #endif
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // this wave's P3 stores
                 const double x = P3[3 * k], y = P3[3 * k + 1], z = P3[3 * k + 2];
-                double d2, e2;
+                double d2, e12[3];
                 int q, sl;
                 float qx = 0.f, qy = 0.f, qz = 0.f, qw;
                 if constexpr (kLds) {
-                    q = grid_query_exact<GridP4, true, 2, true>(gl, a.d, a.thr, x, y, z, d2, &sl, &e2);
+                    q = grid_query_exact<GridP4, true, 2, true>(gl, a.d, a.thr, x, y, z, d2, &sl, e12);
                     if (q >= 0) gl.load(sl, qx, qy, qz, qw);
                 } else {
-                    q = grid_query_exact<GridView, true, 2, true>(gg, a.d, a.thr, x, y, z, d2, &sl, &e2);
+                    q = grid_query_exact<GridView, true, 2, true>(gg, a.d, a.thr, x, y, z, d2, &sl, e12);
                     if (q >= 0) gg.load(sl, qx, qy, qz, qw);
                 }
                 if (CT) CT[ord ? ord[k] : k] = q;
-                const float cf = (float)(__builtin_fmin(__builtin_sqrt(e2), rclr) * (1.0 - 2e-6));
+                // the clearance: to every target other than the winner (a
+                // correspondence), or to every target (none within d)
+                const float cf = (float)(__builtin_sqrt(__builtin_fmin(q >= 0 ? e12[1] : e12[0], e12[2])) *
+                                         (1.0 - 2e-6));
                 put_state(cst + k, make_int4(q >= 0 ? sl : -1, __float_as_int(cf), 0, 0), wt);
                 if (q >= 0) add_corr(v, cnt, acc, x, y, z, qx, qy, qz, d2);
             };
@@ -439,18 +442,27 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
                         xform12(U, x, y, z, ox, oy, oz);
                         put3(P3 + 3 * k, ox, oy, oz, wt);
                         const int4 st = cst[k];
+                        // D += this step's length (rounded up)
+                        const double dx = ox - x, dy = oy - y, dz = oz - z;
+                        const double Dn = (double)__int_as_float(st.z) +
+                                          __builtin_sqrt((dx * dx + dy * dy) + dz * dz) * (1.0 + 1e-9);
+                        const double room = ((double)__int_as_float(st.y) - Dn) * (1.0 - 1e-12);
                         need = true;
-                        if (st.x >= 0) {
-                            // D += this step's length (rounded up)
-                            const double dx = ox - x, dy = oy - y, dz = oz - z;
-                            const double Dn = (double)__int_as_float(st.z) +
-                                              __builtin_sqrt((dx * dx + dy * dy) + dz * dz) * (1.0 + 1e-9);
+                        if (st.x < 0) {
+                            // no target within d at the walk: still none while every
+                            // target stays farther than sqrt(thr) (the walk would find
+                            // d2 >= thr for each)
+                            if (room > __builtin_sqrt(a.thr) * (1.0 + 1e-9)) {
+                                need = false;
+                                put_step(cst + k, __float_as_int((float)(Dn * (1.0 + 1e-6) + 1e-30)), wt);
+                                if (CT) CT[ord ? ord[k] : k] = -1;
+                            }
+                        } else {
                             float qx, qy, qz, qw;
                             if constexpr (kLds) gl.load(st.x, qx, qy, qz, qw);
                             else gg.load(st.x, qx, qy, qz, qw);
                             const double d2 = dist2(ox, oy, oz, (double)qx, (double)qy, (double)qz);
-                            if (d2 < a.thr && __builtin_sqrt(d2) * (1.0 + 1e-9) <
-                                                  ((double)__int_as_float(st.y) - Dn) * (1.0 - 1e-12)) {
+                            if (d2 < a.thr && __builtin_sqrt(d2) * (1.0 + 1e-9) < room) {
                                 need = false;
                                 put_step(cst + k, __float_as_int((float)(Dn * (1.0 + 1e-6) + 1e-30)), wt);
                                 if (CT) CT[ord ? ord[k] : k] = __float_as_int(qw);
