@@ -1600,16 +1600,37 @@ struct MutArgs {
     int32_t *corres, *n_corres;
 };
 
-// J = {nn12[i]} of each pair, ascending (one workgroup per pair)
+// J = {nn12[i]} of each pair, ascending (one workgroup per pair).  kLds: the
+// flags and their scan in LDS ((Mmax + 1) ints of dynamic LDS), the used flags
+// written once, coalesced, for featmut_resolve; else all in the HBM scratch.
+template <bool kLds>
 __global__ __launch_bounds__(1024) void featmut_jbuild(MutArgs a) {
+    extern __shared__ int jsh[];
     const int p = blockIdx.x;
     const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
-    int *u = a.used + (size_t)p * (a.Mmax + 1);
-    int *ps = a.pos + (size_t)p * (a.Mmax + 1);
+    int *ug = a.used + (size_t)p * (a.Mmax + 1);
+    int *u = kLds ? jsh : ug;
+    int *ps = kLds ? jsh : a.pos + (size_t)p * (a.Mmax + 1);
     int *jl = a.jlist + (size_t)p * a.Mmax;
     const int32_t *nn = a.nn12 + (size_t)p * a.Nmax;
     for (int j = threadIdx.x; j < m; j += 1024) u[j] = 0;
     __syncthreads();
+    if constexpr (kLds) {
+        for (int i = threadIdx.x; i < n; i += 1024) {
+            const int j = nn[i];
+            if (j >= 0 && j < m) jsh[j] = 1;
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < m; j += 1024) ug[j] = jsh[j];
+        // in place: flags -> exclusive starts (the scan reads each flag before it
+        // writes that position's start; a flag is set iff start[j + 1] > start[j])
+        block_exclusive_scan_1024(jsh, jsh, m, false);
+        __syncthreads();
+        for (int j = threadIdx.x; j < m; j += 1024)
+            if (jsh[j + 1] > jsh[j]) jl[jsh[j]] = j;
+        if (threadIdx.x == 0) a.nj[p] = jsh[m];
+        return;
+    }
     for (int i = threadIdx.x; i < n; i += 1024) {
         const int j = nn[i];
         if (j >= 0 && j < m) u[j] = 1;  // plain stores of one value: no race on the result
@@ -1977,7 +1998,14 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     rc = run_rescan(ra, P, D, s);
     if (rc != PCR_OK) return rc;
     if (mutual) {
-        hipLaunchKernelGGL(featmut_jbuild, dim3(P), dim3(1024), 0, s, ma);
+        const size_t jsm = sizeof(int) * ((size_t)Mmax + 1);
+        if (jsm <= 64 * 1024) {
+            PCR_HIP_CHECK(hipFuncSetAttribute((const void *)featmut_jbuild<true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+            hipLaunchKernelGGL(featmut_jbuild<true>, dim3(P), dim3(1024), jsm, s, ma);
+        } else {
+            hipLaunchKernelGGL(featmut_jbuild<false>, dim3(P), dim3(1024), 0, s, ma);
+        }
         PCR_LAUNCH_CHECK();
         // pass 2: the rows J of G (B-role fragments as the register operand) x all F
         // columns (A-role fragments streamed): the same products, values only

@@ -145,25 +145,44 @@ extern "C" int pcr_transform_batch(const float *xyz, int32_t B, int32_t N, const
 }
 
 // ---------------------------------------------------------------------------
-// C4 pipeline records (pcr_pipeline_step): one 256-thread block per pair; the
-// Chamfer means as f64 sums of the f32 distances in index order (a fixed
-// 256-lane split and tree), then / N and / M.
+// C4 pipeline records (pcr_pipeline_step): one 1024-thread block per pair; the
+// Chamfer means as f64 sums of the f32 distances in a fixed order (thread t
+// sums indices t, t + 1024, ... in 8-wide unrolled runs, then a fixed shuffle
+// tree per wave and the 16 wave totals in order), then / N and / M.
 // ---------------------------------------------------------------------------
 namespace pcr {
 namespace {
-__global__ __launch_bounds__(256) void pipeline_records_kernel(pcr_pipeline_io io) {
-    const int p = blockIdx.x, t = threadIdx.x;
-    __shared__ double red[2][256];
-    double s1 = 0.0, s2 = 0.0;
-    for (int i = t; i < io.N; i += 256) s1 += (double)io.d1[(size_t)p * io.N + i];
-    for (int i = t; i < io.M; i += 256) s2 += (double)io.d2[(size_t)p * io.M + i];
-    red[0][t] = s1;
-    red[1][t] = s2;
+__global__ __launch_bounds__(1024) void pipeline_records_kernel(pcr_pipeline_io io) {
+    const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    __shared__ double red[2][16];
+    // loads of a run issued together (independent), summed in index order
+    auto sum = [&](const float *d, int len) {
+        double acc = 0.0;
+        for (int i0 = t; i0 < len; i0 += 8 * 1024) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * 1024;
+                v[u] = i < len ? d[i] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += (double)v[u];
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        return acc;
+    };
+    const double s1 = sum(io.d1 + (size_t)p * io.N, io.N);
+    const double s2 = sum(io.d2 + (size_t)p * io.M, io.M);
+    if (lane == 0) { red[0][wid] = s1; red[1][wid] = s2; }
     __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-        if (t < h) { red[0][t] += red[0][t + h]; red[1][t] += red[1][t + h]; }
-        __syncthreads();
+    if (t == 0) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int w = 0; w < 16; ++w) { a1 += red[0][w]; a2 += red[1][w]; }
+        red[0][0] = a1;
+        red[1][0] = a2;
     }
+    __syncthreads();
     double *r = io.records + (size_t)p * 40;
     if (t < 16) {
         r[t] = io.T_ransac[(size_t)p * 16 + t];
@@ -184,7 +203,7 @@ __global__ __launch_bounds__(256) void pipeline_records_kernel(pcr_pipeline_io i
 
 int pipeline_records(const pcr_pipeline_io *io, hipStream_t s) {
     PCR_REQUIRE(io->N >= 1 && io->M >= 1, PCR_ERR_ARG, "pipeline_records: empty clouds");
-    hipLaunchKernelGGL(pipeline_records_kernel, dim3(io->P), dim3(256), 0, s, *io);
+    hipLaunchKernelGGL(pipeline_records_kernel, dim3(io->P), dim3(1024), 0, s, *io);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
