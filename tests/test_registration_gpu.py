@@ -199,6 +199,28 @@ def test_icp_correspondence_reuse_stress(oracle, P):
         assert tuple(_np(res.stats)[p]) == (o["iters"], o["n_corr"]), p
 
 
+@pytest.mark.parametrize("P", [2, 260])
+def test_icp_hbm_grid_vs_oracle(oracle, P):
+    """Targets too large for the LDS grid copy (M = 12,000: the walks read the
+    HBM grid, GridView) through the correspondence-reuse sweep, at G > 1 (P = 2)
+    and one workgroup per pair with the tail launch (P = 260): bit-exact."""
+    n, m = 2500, 12000
+    B = synth.make_batch(P, n=n, m=m, d=4, base_seed=900, feat_noise=1.0)
+    init = np.zeros((P, 4, 4))
+    rng = np.random.default_rng(8)
+    for p in range(P):
+        init[p, :3, :3] = synth.rotation_xyz(*rng.normal(0, 0.01, 3)) @ B.R[p]
+        init[p, :3, 3] = B.t[p] + rng.normal(0, 0.005, 3)
+        init[p, 3, 3] = 1
+    res = reg.icp_batch(B.src, B.tgt, init, reg.IcpParams(0.02))
+    for p in list(range(min(P, 3))) + [P - 1]:
+        o = oracle.icp(B.src[p], B.tgt[p], 0.02, init=init[p])
+        assert _bits_equal(_np(res.transformation)[p], o["T"]), p
+        assert _bits_equal(_np(res.fitness)[p], o["fitness"]), p
+        assert _bits_equal(_np(res.inlier_rmse)[p], o["inlier_rmse"]), p
+        assert tuple(_np(res.stats)[p]) == (o["iters"], o["n_corr"]), p
+
+
 def test_radius_nn_vs_oracle_bruteforce(oracle):
     rng = np.random.default_rng(2)
     tgt = (rng.random((2, 3000, 3)) * 2 - 1).astype(np.float32)
