@@ -870,10 +870,10 @@ def _slot_of(c, S):
         k ^= k >> np.uint64(sh)
         if mul is not None:
             k = (k * np.uint64(mul)) & np.uint64(0xffffffff)
-    return (k & np.uint64(S - 1)).astype(np.int64)
+    return ((k * np.uint64(S)) >> np.uint64(32)).astype(np.int64)
 
 
-def grid_candidates(src, tgt, T, d):
+def grid_candidates(src, tgt, T, d, slot_num=2):
     """Mean candidates c_bar examined per radius-d grid query of src (through T)
     against tgt: a host replay of grid.h's walk (cells 2.01 d, the <=2x2x2 cells
     of the 1.001 d box that the cell-gap test keeps, each kept cell's hash slot
@@ -883,6 +883,7 @@ def grid_candidates(src, tgt, T, d):
     S = 256
     while S < len(tgt):
         S <<= 1
+    S = S // 2 * slot_num  # grid.hip build_grids (RANSAC's grids: 3)
     kt = np.floor(tgt.astype(np.float64) / cell).astype(np.int64)
     slot_cnt = np.bincount(_slot_of(kt, S), minlength=S)
     p = src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]
@@ -1298,7 +1299,7 @@ def main():
     icp_sweeps = int((ir.stats[:, 0] + 1).sum().item())
     samp = list(range(min(4, P)))
     cb_r = float(np.mean([grid_candidates(batch.src[p], batch.tgt[p], mine[p, 0:16].reshape(4, 4),
-                                          params.ransac.max_correspondence_distance) for p in samp]))
+                                          params.ransac.max_correspondence_distance, 3) for p in samp]))
     cb_i = float(np.mean([grid_candidates(batch.src[p], batch.tgt[p], T_icp[p],
                                           params.icp.max_correspondence_distance) for p in samp]))
     chamfer_samples = []

@@ -35,7 +35,7 @@ __device__ __forceinline__ unsigned key_slot(unsigned k, int S) {
     k ^= k >> 13;
     k *= 0xc2b2ae35u;
     k ^= k >> 16;
-    return k & (unsigned)(S - 1);
+    return (unsigned)(((unsigned long long)k * (unsigned)S) >> 32);  // any S, not only powers of two
 }
 __device__ __forceinline__ unsigned cell_hash(int x, int y, int z, int S) {
     return key_slot(cell_key(x, y, z), S);
@@ -361,7 +361,9 @@ int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double ce
                   int ws_slot, const int32_t **order, const float **perm = nullptr, int perm_slot = -1);
 
 // host: allocate (workspace slot) + build; returns PCR_OK or error
+// slots: the power of two >= Mmax (>= 256), times slot_num / 2 (3: 1.5x the
+// slots -- fewer collisions -- where the consumer's LDS has room for them)
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r,
-                hipStream_t s, int ws_slot, GridBatch &out, double cell_factor = 2.01);
+                hipStream_t s, int ws_slot, GridBatch &out, double cell_factor = 2.01, int slot_num = 2);
 
 }  // namespace pcr

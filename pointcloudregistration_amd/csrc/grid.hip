@@ -201,9 +201,10 @@ int spatial_order(const float *pts, const int32_t *n, int P, int Nmax, double ce
 }
 
 int build_grids(const float *tgt, const int32_t *n_tgt, int P, int Mmax, double r, hipStream_t s,
-                int ws_slot, GridBatch &out, double cell_factor) {
+                int ws_slot, GridBatch &out, double cell_factor, int slot_num) {
     int S = 256;
     while (S < Mmax) S <<= 1;
+    S = S / 2 * slot_num;
     const size_t cnt_b = sizeof(int) * (size_t)P * S;
     const size_t start_b = sizeof(int) * (size_t)P * (S + 1);
     const size_t pts_b = 16 * (size_t)P * (Mmax > 0 ? Mmax : 1);

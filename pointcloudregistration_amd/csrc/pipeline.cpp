@@ -126,7 +126,7 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     auto prep = [&]() -> int {
         PCR_HIP_CHECK(hipStreamWaitEvent(side, ev_in, 0));
         if (gr) {
-            int r = pcr::build_grids(io->tgt_xyz, nullptr, P, M, rp->max_correspondence_distance, side, 4, grid_r);
+            int r = pcr::build_grids(io->tgt_xyz, nullptr, P, M, rp->max_correspondence_distance, side, 4, grid_r, 2.01, 3);
             if (r != PCR_OK) return r;
             r = pcr::spatial_order(io->src_xyz, nullptr, P, N, grid_r.cell, side, 13, &order, &perm, 36);
             if (r != PCR_OK) return r;

@@ -766,7 +766,7 @@ int ransac_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax,
             a.order = Nmax > 0 ? order_in : nullptr;
             a.srcp = Nmax > 0 ? perm_in : nullptr;
         } else {
-            int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 4, a.grid);
+            int rc = build_grids(tgt, n_tgt, P, Mmax, a.d, s, 4, a.grid, 2.01, 3);
             if (rc != PCR_OK) return rc;
             if (Nmax > 0) {
                 rc = spatial_order(src, n_src, P, Nmax, a.grid.cell, s, 13, &a.order, &a.srcp, 36);
