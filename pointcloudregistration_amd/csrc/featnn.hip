@@ -1281,12 +1281,11 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
                 const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
                 a.v[o] = (double)mb1;
                 a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-                if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)))) {
-                    a.nn[o] = 0;  // the exact rescan writes it
+                // uncertified rows too: the screened argmin, which the exact
+                // rescan overwrites (featmut_jbuild may read either)
+                want = mi1;
+                if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
                     a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
-                } else {
-                    want = mi1;
-                }
             }
             if (own && want >= 0) a.nn[o] = want;
         } else {
@@ -1574,19 +1573,18 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
         a.v[o] = (double)mb1 - kRowBias;  // exact (both multiples of mb1's ulp)
         a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-        if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)))) {
-            a.nn[o] = 0;  // the exact rescan writes it
+        // uncertified rows too: the screened argmin, which the exact rescan
+        // overwrites (featmut_jbuild, beside that rescan, may read either)
+        a.nn[o] = mi1;
+        if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
             a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
-        } else {
-            a.nn[o] = mi1;
-        }
     }
 }
 
 struct MutArgs {
     const int32_t *nn12, *n_src, *n_tgt;
     int Nmax, Mmax, mutual, ransac_n, Kt, D, ntm;
-    int *used;        // [P][Mmax + 1]: 1 = some i has nn12[i] = j (2: listed for the rescan)
+    int *used;        // [P][Mmax + 1]: 1 = j in J (2: listed for the rescan), 3: listed, not in J
     int *pos;         // [P][Mmax + 1] scan scratch
     int *jlist, *nj;  // [P][Mmax], [P]: the rows of pass 2, ascending
     const double *v12;
@@ -1652,7 +1650,14 @@ __global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
     if (i >= n) return;
     const int j = a.nn12[(size_t)p * a.Nmax + i];
     int f = 0;
-    if (j >= 0 && j < m) {
+    int *uj = a.used + (size_t)p * (a.Mmax + 1) + j;
+    if (j >= 0 && j < m && (*uj == 0 || *uj == 3)) {
+        // J was built from the screened argmins, beside the exact row rescan:
+        // a rescanned row's exact argmin j may have no pass-2 values.  Its
+        // exact column argmin decides (listed once: 0 -> 3)
+        f = 2;
+        if (atomicCAS(uj, 0, 3) == 0) a.list21[(size_t)p * a.Mmax + atomicAdd(a.cnt21 + p, 1)] = j;
+    } else if (j >= 0 && j < m) {
         const size_t oj = (size_t)p * a.Mmax + j, oi = (size_t)p * a.Nmax + i;
         const float4 q = a.wq[oj];  // featnn_row8's pass 2 stores biased values (exact in f64)
         const double w1 = (double)q.x - a.wbias, w2 = (double)q.y - a.wbias, e2 = (double)q.z;
@@ -1663,7 +1668,7 @@ __global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
             f = (vi <= w1 + e2 + e1 + sl) ? 1 : 0;
         } else {
             f = 2;
-            if (atomicCAS(a.used + (size_t)p * (a.Mmax + 1) + j, 1, 2) == 1)
+            if (atomicCAS(uj, 1, 2) == 1)
                 a.list21[(size_t)p * a.Mmax + atomicAdd(a.cnt21 + p, 1)] = j;
         }
     }
@@ -1995,8 +2000,21 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     ra.list12 = v.list12; ra.list21 = v.list21; ra.cnt12 = v.cnt12; ra.cnt21 = zero;
     ra.nn12 = nn12; ra.nn21 = nn21x;
     ra.v12 = v12; ra.e12 = e12; ra.mx = v.mx; ra.T = v.sp.T;
-    rc = run_rescan(ra, P, D, s);
+    // mutual: the exact rescan of the uncertified rows runs on a side stream
+    // beside J's build and pass 2, which read none of its results (J from the
+    // screened argmins; featmut_resolve, after the join, sends a rescanned
+    // row's new argmin outside J to the exact column rescan)
+    hipStream_t rs = s;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    if (mutual) {
+        rc = side_stream(&rs, &ev_fork, &ev_join, 1);
+        if (rc != PCR_OK) return rc;
+        PCR_HIP_CHECK(hipEventRecord(ev_fork, s));
+        PCR_HIP_CHECK(hipStreamWaitEvent(rs, ev_fork, 0));
+    }
+    rc = run_rescan(ra, P, D, rs);
     if (rc != PCR_OK) return rc;
+    if (rs != s) PCR_HIP_CHECK(hipEventRecord(ev_join, rs));
     if (mutual) {
         const size_t jsm = sizeof(int) * ((size_t)Mmax + 1);
         if (jsm <= 64 * 1024) {
@@ -2030,6 +2048,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
             if (rc != PCR_OK) return rc;
         }
         prof_end(s, kProfFeatScreen2);
+        if (rs != s) PCR_HIP_CHECK(hipStreamWaitEvent(s, ev_join, 0));
         hipLaunchKernelGGL(featmut_resolve, dim3(cdiv(Nmax, 256), P), dim3(256), 0, s, ma);
         PCR_LAUNCH_CHECK();
         RescanArgs5 rb = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);

@@ -35,10 +35,11 @@ int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, co
 
 inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
-// A second stream of the calling thread's (device, workspace context) and two
+// A side stream of the calling thread's (device, workspace context) and two
 // events for fork / join with the caller's stream; created once, destroyed by
-// pcr_shutdown.
-int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out);
+// pcr_shutdown.  which = 0: the pipeline's grid prep; 1: the feature stage's
+// exact row rescan (beside pass 2 of the mutual path).
+int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which = 0);
 
 // per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)
 enum ProfId { kProfFeatScreen = 0, kProfNndFwd = 1, kProfRansacValidate = 2, kProfIcp = 3,

@@ -116,8 +116,10 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     // is done / launched (an event recorded inside the feature stage).  Measured
     // (round 4): 256 pairs 9.47 / 9.36 / 9.48 ms, 128 pairs 5.14 / 5.16 / 5.16,
     // 64 pairs 2.90 / 2.91 / 2.93, 32 pairs 1.84 / 1.83 / 1.81 ms.  D > 64 (no
-    // hook in that screen): 0
-    int at = P >= 192 ? 1 : P <= 48 ? 2 : 0;
+    // hook in that screen): 0.  Round 5, with the feature stage's row rescan on
+    // its own side stream beside pass 2: 256 pairs at 1 / 2 8.21 / 8.08 ms (one
+    // box), 32 pairs 1.59 / 1.57, 64 and 128 pairs 0 / 1 / 2 within 0.03 ms
+    int at = (P >= 192 || P <= 48) ? 2 : 0;
     if (io->D > 64) at = 0;
     pcr::GridBatch grid_r{}, grid_i{};
     const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP

@@ -79,18 +79,22 @@ struct Side {
     hipStream_t s = nullptr;
     hipEvent_t e[2] = {nullptr, nullptr};
 };
-Side g_side[kMaxDevices][kMaxCtx];
+Side g_side[kMaxDevices][kMaxCtx][2];
 }  // namespace
 
-int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out) {
+int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
         (void)hipGetLastError();
         set_error("side_stream: no current device");
         return PCR_ERR_HIP;
     }
+    if (which < 0 || which > 1) {
+        set_error("side_stream: no side stream %d", which);
+        return PCR_ERR_ARG;
+    }
     std::lock_guard<std::mutex> lk(g_mu);
-    Side &d = g_side[dev][t_ctx];
+    Side &d = g_side[dev][t_ctx][which];
     if (!d.s) {
         if (hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&d.e[0], hipEventDisableTiming) != hipSuccess ||
@@ -313,16 +317,17 @@ extern "C" int pcr_shutdown(void) {
                 }
         }
         for (int dev = 0; dev < pcr::kMaxDevices; ++dev)
-            for (auto &sd : pcr::g_side[dev]) {
-                if (!sd.s) continue;
-                if (hipSetDevice(dev) == hipSuccess) {
-                    (void)hipStreamSynchronize(sd.s);
-                    (void)hipStreamDestroy(sd.s);
-                    (void)hipEventDestroy(sd.e[0]);
-                    (void)hipEventDestroy(sd.e[1]);
+            for (auto &pair : pcr::g_side[dev])
+                for (auto &sd : pair) {
+                    if (!sd.s) continue;
+                    if (hipSetDevice(dev) == hipSuccess) {
+                        (void)hipStreamSynchronize(sd.s);
+                        (void)hipStreamDestroy(sd.s);
+                        (void)hipEventDestroy(sd.e[0]);
+                        (void)hipEventDestroy(sd.e[1]);
+                    }
+                    sd = pcr::Side{};
                 }
-                sd = pcr::Side{};
-            }
         std::vector<std::pair<int, void *>> keep;
         for (auto &r : pcr::g_retired) {
             if (!unsynced[r.first] && hipSetDevice(r.first) == hipSuccess) (void)hipFree(r.second);

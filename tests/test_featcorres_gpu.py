@@ -52,6 +52,12 @@ def _cases():
     a[0, :] = np.nan
     b[[0, 7, 100], 0] = np.nan
     c["nan_rows"] = (a, b)
+    # twin targets a few ulps from each source row: the screen cannot order a
+    # twin pair, so its argmin (J is built from it, beside the exact row rescan)
+    # is often the exact loser, and the exact winner is in no other row's J
+    a = rng.standard_normal((600, 32)).astype(np.float32)
+    tw = np.repeat(a, 2, axis=0) + (rng.standard_normal((1200, 32)) * 1e-6).astype(np.float32)
+    c["near_twins"] = (a, np.concatenate([tw, rng.standard_normal((100, 32)).astype(np.float32)]))
     c["subnormal"] = ((rng.standard_normal((300, 16)) * 1e-39).astype(np.float32),
                       (rng.standard_normal((280, 16)) * 1e-39).astype(np.float32))
     # the packs' speculative scale (feat_sample: the first 64 rows' max with one
