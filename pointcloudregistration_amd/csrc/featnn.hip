@@ -1981,7 +1981,11 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.wq = nullptr;
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
-    if (prep_event && prep_at == 2) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
+    if (prep_event && prep_at == 2) {
+        PCR_HIP_CHECK(hipEventRecord(prep_event, s));
+        if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
+        prep_fn = nullptr;
+    }
     prof_begin(s, kProfFeatScreen);
     if (v.S <= 2) {  // two column tiles per step (featnn_row8)
         r.nrb = cdiv(cdiv(Nmax, 32), v.W * 2);
@@ -1995,7 +1999,11 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         if (rc != PCR_OK) return rc;
     }
     prof_end(s, kProfFeatScreen);
-    if (prep_event && prep_at == 1) PCR_HIP_CHECK(hipEventRecord(prep_event, s));
+    if (prep_event && prep_at == 1) {
+        PCR_HIP_CHECK(hipEventRecord(prep_event, s));
+        if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
+        prep_fn = nullptr;
+    }
     RescanArgs5 ra = rescan_args(F, G, n_src, n_tgt, Nmax, Mmax, D);
     ra.list12 = v.list12; ra.list21 = v.list21; ra.cnt12 = v.cnt12; ra.cnt21 = zero;
     ra.nn12 = nn12; ra.nn21 = nn21x;
@@ -2003,10 +2011,12 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     // mutual: the exact rescan of the uncertified rows runs on a side stream
     // beside J's build and pass 2, which read none of its results (J from the
     // screened argmins; featmut_resolve, after the join, sends a rescanned
-    // row's new argmin outside J to the exact column rescan)
+    // row's new argmin outside J to the exact column rescan).  Large batches
+    // only: at 32-128 pairs it gained nothing.  The side stream is the
+    // pipeline's prep stream (its grid builds are enqueued first, prep_fn)
     hipStream_t rs = s;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    if (mutual) {
+    if (mutual && P >= 192) {
         rc = side_stream(&rs, &ev_fork, &ev_join, 1);
         if (rc != PCR_OK) return rc;
         PCR_HIP_CHECK(hipEventRecord(ev_fork, s));

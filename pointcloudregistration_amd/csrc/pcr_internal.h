@@ -25,9 +25,13 @@ bool nnd_uses_grid(int b, int n, int m);
 
 // pcr_pipeline_step's hook into the feature stage: when
 // set, feature_corres_v5 records prep_event on its stream before (at = 2) or
-// after (at = 1) the pass-1 launch, so the side stream's grid builds start there
+// after (at = 1) the pass-1 launch and calls prep_fn(prep_ctx) there (then
+// clears prep_fn), so the side stream's grid builds are enqueued -- and start
+// -- at that point, ahead of the feature stage's own side-stream work
 extern thread_local hipEvent_t prep_event;
 extern thread_local int prep_at;
+extern thread_local int (*prep_fn)(void *);
+extern thread_local void *prep_ctx;
 int nnd_forward_grid(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
                      float *dist2, int32_t *idx1, int32_t *idx2, hipStream_t s);
 int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, const float *xyz2, int b, int n,
@@ -35,10 +39,12 @@ int nnd_forward_grid_xf(const float *xyz1, const float *src, const double *T, co
 
 inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
-// A side stream of the calling thread's (device, workspace context) and two
-// events for fork / join with the caller's stream; created once, destroyed by
-// pcr_shutdown.  which = 0: the pipeline's grid prep; 1: the feature stage's
-// exact row rescan (beside pass 2 of the mutual path).
+// The side stream of the calling thread's (device, workspace context) and a
+// pair of events for fork / join with the caller's stream; created once,
+// destroyed by pcr_shutdown.  which = the event pair: 0 the pipeline's grid
+// prep, 1 the feature stage's exact row rescan (beside pass 2).  One stream for
+// both: a second stream per context moved other streams' hardware queues (the
+// process has 4) and cost the s8d job 18 %.
 int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which = 0);
 
 // per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)

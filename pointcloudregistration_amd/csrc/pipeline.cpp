@@ -146,14 +146,23 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
         if (rc != PCR_OK) return rc;
     }
     lap("prep");
+    // at != 0: the feature stage enqueues the prep at its hook point (prep_fn),
+    // ahead of its own side-stream work; if it took no hook, it runs here
+    auto prep_tramp = [](void *c) -> int { return (*static_cast<decltype(prep) *>(c))(); };
     pcr::prep_event = at ? ev_in : nullptr;
     pcr::prep_at = at;
+    pcr::prep_fn = at ? +prep_tramp : nullptr;
+    pcr::prep_ctx = &prep;
     rc = pcr::feature_corres_impl(io->src_feat, io->tgt_feat, P, N, M, io->D, nullptr, nullptr,
                                   rp->mutual_filter, rp->ransac_n, io->nn12, io->corres, io->n_corres, s);
+    const bool prep_left = pcr::prep_fn != nullptr;
     pcr::prep_event = nullptr;
     pcr::prep_at = 0;
+    pcr::prep_fn = nullptr;
+    pcr::prep_ctx = nullptr;
     if (rc != PCR_OK) return rc;
-    if (at) {
+    if (at && prep_left) {
+        PCR_HIP_CHECK(hipEventRecord(ev_in, s));
         rc = prep();
         if (rc != PCR_OK) return rc;
     }

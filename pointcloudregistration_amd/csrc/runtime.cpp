@@ -72,14 +72,16 @@ void *workspace(int slot, size_t bytes, bool *fresh) {
 
 thread_local hipEvent_t prep_event = nullptr;
 thread_local int prep_at = 0;
+thread_local int (*prep_fn)(void *) = nullptr;
+thread_local void *prep_ctx = nullptr;
 
 // ---- side stream of a (device, workspace context) -------------------------
 namespace {
 struct Side {
     hipStream_t s = nullptr;
-    hipEvent_t e[2] = {nullptr, nullptr};
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
 };
-Side g_side[kMaxDevices][kMaxCtx][2];
+Side g_side[kMaxDevices][kMaxCtx];
 }  // namespace
 
 int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which) {
@@ -90,23 +92,25 @@ int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which) 
         return PCR_ERR_HIP;
     }
     if (which < 0 || which > 1) {
-        set_error("side_stream: no side stream %d", which);
+        set_error("side_stream: no event pair %d", which);
         return PCR_ERR_ARG;
     }
     std::lock_guard<std::mutex> lk(g_mu);
-    Side &d = g_side[dev][t_ctx][which];
+    Side &d = g_side[dev][t_ctx];
     if (!d.s) {
         if (hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&d.e[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.e[1], hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&d.e[1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d.e[2], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d.e[3], hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
             set_error("side_stream: stream / event creation failed");
             return PCR_ERR_HIP;
         }
     }
     *s = d.s;
-    *e_in = d.e[0];
-    *e_out = d.e[1];
+    *e_in = d.e[2 * which];
+    *e_out = d.e[2 * which + 1];
     return PCR_OK;
 }
 
@@ -317,17 +321,15 @@ extern "C" int pcr_shutdown(void) {
                 }
         }
         for (int dev = 0; dev < pcr::kMaxDevices; ++dev)
-            for (auto &pair : pcr::g_side[dev])
-                for (auto &sd : pair) {
-                    if (!sd.s) continue;
-                    if (hipSetDevice(dev) == hipSuccess) {
-                        (void)hipStreamSynchronize(sd.s);
-                        (void)hipStreamDestroy(sd.s);
-                        (void)hipEventDestroy(sd.e[0]);
-                        (void)hipEventDestroy(sd.e[1]);
-                    }
-                    sd = pcr::Side{};
+            for (auto &sd : pcr::g_side[dev]) {
+                if (!sd.s) continue;
+                if (hipSetDevice(dev) == hipSuccess) {
+                    (void)hipStreamSynchronize(sd.s);
+                    (void)hipStreamDestroy(sd.s);
+                    for (hipEvent_t e : sd.e) (void)hipEventDestroy(e);
                 }
+                sd = pcr::Side{};
+            }
         std::vector<std::pair<int, void *>> keep;
         for (auto &r : pcr::g_retired) {
             if (!unsynced[r.first] && hipSetDevice(r.first) == hipSuccess) (void)hipFree(r.second);
