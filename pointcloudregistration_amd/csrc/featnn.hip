@@ -1648,20 +1648,23 @@ __global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
     const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
     const int n = count_of(a.n_src, p, a.Nmax), m = count_of(a.n_tgt, p, a.Mmax);
     if (i >= n) return;
-    const int j = a.nn12[(size_t)p * a.Nmax + i];
+    const size_t oi = (size_t)p * a.Nmax + i;
+    const int j = a.nn12[oi];
     int f = 0;
     int *uj = a.used + (size_t)p * (a.Mmax + 1) + j;
-    if (j >= 0 && j < m && (*uj == 0 || *uj == 3)) {
+    const double e1 = (double)a.e12[oi];  // 0: rescanned (or a zero bound)
+    if (j >= 0 && j < m && e1 == 0.0 && (*uj == 0 || *uj == 3)) {
         // J was built from the screened argmins, beside the exact row rescan:
-        // a rescanned row's exact argmin j may have no pass-2 values.  Its
-        // exact column argmin decides (listed once: 0 -> 3)
+        // a rescanned row's exact argmin j may have no pass-2 values (pass-1
+        // certified rows kept the argmin J was built from).  Its exact column
+        // argmin decides (listed once: used 0 -> 3)
         f = 2;
         if (atomicCAS(uj, 0, 3) == 0) a.list21[(size_t)p * a.Mmax + atomicAdd(a.cnt21 + p, 1)] = j;
     } else if (j >= 0 && j < m) {
-        const size_t oj = (size_t)p * a.Mmax + j, oi = (size_t)p * a.Nmax + i;
+        const size_t oj = (size_t)p * a.Mmax + j;
         const float4 q = a.wq[oj];  // featnn_row8's pass 2 stores biased values (exact in f64)
         const double w1 = (double)q.x - a.wbias, w2 = (double)q.y - a.wbias, e2 = (double)q.z;
-        const double vi = a.v12[oi], e1 = (double)a.e12[oi];
+        const double vi = a.v12[oi];
         // slack: the f64 sums of a rescanned value vs the exact real distance
         const double sl = 1e-9 * (__builtin_fabs(w1) + __builtin_fabs(vi));
         if (w2 - w1 > 2.0 * (e2 + e1 + sl)) {
