@@ -62,8 +62,9 @@ int pcr_set_concurrency(int32_t k);
 int pcr_coop_probe(int32_t *out, int32_t blocks, int32_t cooperative, pcr_stream_t stream);
 
 /* Optional per-kernel timing with HIP events recorded on the launch stream
- * around the hot kernels (id 0 feature screen, 1 nnd forward, 2 RANSAC verify,
- * 3 ICP, 4 RANSAC hypotheses, 5 feature rescan, 6 feature pack).  pcr_profile_read synchronizes the pending
+ * around the hot kernels (id 0 feature screen (pass 1), 1 nnd forward, 2 RANSAC verify,
+ * 3 ICP, 4 RANSAC hypotheses, 5 feature rescan, 6 feature pack, 7 nnd grid query,
+ * 8 feature screen pass 2, 9 / 10 the 3-term screens behind passes 1 / 2).  pcr_profile_read synchronizes the pending
  * events and returns the accumulated milliseconds and launch count. */
 void pcr_profile_enable(int32_t on);
 int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset);
@@ -72,6 +73,10 @@ int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset
  * certify and sent to the exact f64 rescan since the last reset.  Synchronizes
  * the device. */
 int pcr_featnn_rescan_rows(int64_t *rows12, int64_t *rows21, int32_t reset);
+/* Diagnostic: source rows (pass 1) and target columns of J (pass 2) that the
+ * 1-term f16 feature screens could not certify and left to the 3-term split
+ * screen since the last reset.  Synchronizes the device. */
+int pcr_featnn_fallback_rows(int64_t *rows12, int64_t *cols21, int32_t reset);
 /* diagnostic: copy `bytes` of pcr_feature_correspondences' scratch from its
  * last call (device to device, on `stream`) */
 int pcr_featmut_debug_copy(void *dst, int64_t bytes, pcr_stream_t stream);

@@ -130,6 +130,8 @@ def load():
         lib.pcr_profile_read.argtypes = [_i32, ctypes.POINTER(_f64), ctypes.POINTER(_i64), _i32]
         lib.pcr_featnn_rescan_rows.restype = ctypes.c_int
         lib.pcr_featnn_rescan_rows.argtypes = [ctypes.POINTER(_i64), ctypes.POINTER(_i64), _i32]
+        lib.pcr_featnn_fallback_rows.restype = ctypes.c_int
+        lib.pcr_featnn_fallback_rows.argtypes = [ctypes.POINTER(_i64), ctypes.POINTER(_i64), _i32]
         lib.pcr_ndp_train_partial_floats.restype = _i64
         lib.pcr_ndp_train_partial_floats.argtypes = [_i32, _i32, _i32, _i32]
         lib.pcr_ndp_chamfer_scratch_bytes.restype = _i64
@@ -156,7 +158,7 @@ def load():
 
 def exported_symbols():
     return ["pcr_last_error", "pcr_version", "pcr_workspace_release", "pcr_profile_enable", "pcr_profile_read",
-            "pcr_featnn_rescan_rows", "pcr_ndp_train_partial_floats", "pcr_ndp_chamfer_scratch_bytes",
+            "pcr_featnn_rescan_rows", "pcr_featnn_fallback_rows", "pcr_ndp_train_partial_floats", "pcr_ndp_chamfer_scratch_bytes",
             "pcr_ndp_loss_scratch_bytes", "pcr_ndp_chamfer_gacc_words", "pcr_ndp_chamfer_max_points",
             "pcr_shutdown"] + \
         list(SIGNATURES)
@@ -164,7 +166,8 @@ def exported_symbols():
 
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
 PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID, PROF_FEAT_SCREEN2 = 5, 6, 7, 8
-PROF_SLOTS = 9   # pcr_internal.h kProfSlots
+PROF_FEAT_SCREEN1B, PROF_FEAT_SCREEN2B = 9, 10   # the 3-term screens behind the 1-term ones
+PROF_SLOTS = 11   # pcr_internal.h kProfSlots
 
 
 # bumped by every shutdown(): a HIP graph captured before it points at freed
@@ -205,6 +208,16 @@ def featnn_rescan_rows(reset=True):
     """(rows12, rows21) sent to the exact feature-NN rescan since the last reset."""
     a, b = _i64(0), _i64(0)
     rc = load().pcr_featnn_rescan_rows(ctypes.byref(a), ctypes.byref(b), 1 if reset else 0)
+    if rc != PCR_OK:
+        raise PcrError(load().pcr_last_error().decode())
+    return a.value, b.value
+
+
+def featnn_fallback_rows(reset=True):
+    """(rows12, cols21) the 1-term feature screens left to the 3-term ones since
+    the last reset."""
+    a, b = _i64(0), _i64(0)
+    rc = load().pcr_featnn_fallback_rows(ctypes.byref(a), ctypes.byref(b), 1 if reset else 0)
     if rc != PCR_OK:
         raise PcrError(load().pcr_last_error().decode())
     return a.value, b.value

@@ -170,6 +170,10 @@ __global__ __launch_bounds__(256) void feat_sample(const float *F, const int32_t
         clr[P + p] = 0u;      // fmax
         clr[3 * P + p] = 0u;  // cnt12
         clr[4 * P + p] = 0u;  // cnt21
+        clr[5 * P + p] = 0u;  // gemax
+        clr[6 * P + p] = 0u;  // femax
+        clr[7 * P + p] = 0u;  // fbc12
+        clr[8 * P + p] = 0u;  // fbc21
         bad[p] = 0;
     }
 }
@@ -210,9 +214,11 @@ __global__ __launch_bounds__(1024) void feat_maxabs(const float *F, const int32_
             float r = wm[0];
             for (int w = 1; w < 16; ++w) r = fmaxf(r, wm[w]);
             mxp[((size_t)p * 2 + which) * Z + z] = __float_as_uint(r);  // r >= 0, never NaN
-            if (which == 0 && z == 0) {  // gmax, fmax: the repair packs max into them again
+            if (which == 0 && z == 0) {  // gmax, fmax, gemax, femax: the repair packs max into them again
                 clr[p] = 0u;
                 clr[P + p] = 0u;
+                clr[5 * P + p] = 0u;
+                clr[6 * P + p] = 0u;
             }
         }
         __syncthreads();
@@ -257,7 +263,27 @@ struct PackIO {
     f16x8 *Xp[2];
     float *nrm[2];
     unsigned *nmax[2];
+    unsigned *emax[2];  // per pair: max over the cloud's rows of |x s - f16(x s)| (the 1-term screen's bound)
 };
+
+// |x - f16(x)| of one row (x already scaled), rounded up: e^2 summed exactly
+// enough in f64 (each term exact), the sqrt's rounding covered by the factor
+__device__ __forceinline__ float split_err_norm(double e2) {
+    return (float)(__builtin_sqrt(e2) * (1.0 + 1e-6));
+}
+
+// one atomic per workgroup: max of the four waves' values (bit patterns of
+// non-negative floats; unsigned order = float order)
+__device__ __forceinline__ void block_max_atomic(unsigned v, unsigned *wm, unsigned *dst) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o, 64));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned m = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+        if (m != 0u) atomicMax(dst, m);
+    }
+}
 
 template <class Body>
 __device__ __forceinline__ void pack_pairs(const PackCtl &c, int T, Body body) {
@@ -311,10 +337,12 @@ __global__ __launch_bounds__(256) void feat_pack5(PackIO io, int D, int S, Split
         __syncthreads();
         const int rr = l & 31, h = l >> 5;
         const bool valid = rr < nrows;
-        double acc = 0.0;
+        double acc = 0.0, ea = 0.0;
         for (int k = 0; k < D; ++k) {
             const double v = (double)x[rr][k];
             acc = acc + v * v;
+            const double e = (double)(x[rr][k] - (float)(_Float16)x[rr][k]);  // exact in f32
+            ea = ea + e * e;
         }
         // norm parts of acc / c (exact power-of-two division)
         _Float16 np[3];
@@ -366,15 +394,9 @@ __global__ __launch_bounds__(256) void feat_pack5(PackIO io, int D, int S, Split
         // same word per-lane atomics would leave, NaN included.
         const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
         if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
-        unsigned rb = __float_as_uint(r);
-#pragma unroll
-        for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
-        if (l == 0) wmax[w] = rb;
+        block_max_atomic(__float_as_uint(r), wmax, nmax + p);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-            if (m != 0u) atomicMax(nmax + p, m);
-        }
+        block_max_atomic(valid ? __float_as_uint(split_err_norm(ea)) : 0u, wmax, io.emax[role] + p);
     });
 }
 
@@ -424,11 +446,13 @@ __global__ __launch_bounds__(256) void feat_pack5r(PackIO io, Split5 sp, PackCtl
             for (int k = 0; k < D; ++k) ok = ok && __builtin_fabsf(x[k]) < lim;  // NaN / inf: not ok
             if (!ok) pc.bad[p] = 1;
         }
-        double acc = 0.0;
+        double acc = 0.0, ea = 0.0;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const double v = (double)x[k];
             acc = acc + v * v;
+            const double e = (double)(x[k] - (float)(_Float16)x[k]);  // exact in f32
+            ea = ea + e * e;
         }
         _Float16 np[3];
         if (valid) {
@@ -484,15 +508,9 @@ __global__ __launch_bounds__(256) void feat_pack5r(PackIO io, Split5 sp, PackCtl
         // the pair's max norm: one atomic per WORKGROUP (see feat_pack5)
         const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
         if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
-        unsigned rb = __float_as_uint(r);
-#pragma unroll
-        for (int o = 32; o; o >>= 1) rb = max(rb, (unsigned)__shfl_xor((int)rb, o, 64));
-        if (l == 0) wmax[w] = rb;
+        block_max_atomic(__float_as_uint(r), wmax, nmax + p);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-            if (m != 0u) atomicMax(nmax + p, m);
-        }
+        block_max_atomic(valid ? __float_as_uint(split_err_norm(ea)) : 0u, wmax, io.emax[role] + p);
     });
 }
 
@@ -1039,7 +1057,15 @@ struct RowArgs5 {
     const float *Xr;
     const unsigned *sc;
     int role, cs;
+    const unsigned *cemax;      // featnn_row8<.., kOne>: per pair max |y - f16(y)| of the column image
+    int32_t *nns;               // pass 1: a copy of the screened argmin for featmut_jbuild (nullable)
+    int fbdiag;                 // 1 / 2: count the listed rows in g_featnn_fallback_rows[0 / 1]
+    int rbmajor;                // featnn_row8: blocks ordered row block first (short lists, below)
 };
+
+// rows (pass 1) and J columns (pass 2) the 1-term screens left to the 3-term
+// ones since the last reset (diagnostic, pcr_featnn_fallback_rows)
+__device__ unsigned long long g_featnn_fallback_rows[2];
 
 // One row's operand fragments exactly as feat_pack5 / feat_pack5r store them
 // (same scale, same operations in the same order), for lane half h: x the
@@ -1358,18 +1384,70 @@ constexpr double kRowBias = 32768.0;
 __device__ __forceinline__ unsigned umin2(unsigned a, unsigned b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned umax2(unsigned a, unsigned b) { return a > b ? a : b; }
 
-template <int S, int G, bool kIdx>
+// The 1-term screen (round 6, kOne): the row operand is -2 f16(x) and the column
+// operand f16(y) -- one k-segment instead of the split's three (hi.hi', hi.lo',
+// lo.hi'), so S + 1 MFMAs per 32 x 32 tile instead of 3 S + 1, and the column
+// stream carries only the [hi | norms] chunks of the stored image.  Its error
+// is larger: with e_x = x - f16(x) (exact in f32),
+//   |x.y - f16(x).f16(y)| = |e_x.y + f16(x).e_y| <= |e_x| |y| + (|x| + |e_x|) |e_y|
+// by Cauchy-Schwarz; the row's |e_x| is computed here from the row itself, the
+// columns' max |e_y| by the pack (emax), and both carry 2^-14 sqrt(D) for f16
+// subnormals the MFMA may flush (bound1).  ~4 % of the rows (C4) do not
+// certify under it: they are listed for the 3-term screen of the same rows
+// (featnn_row8<.., false> over the list, the rows it cannot certify going on to
+// the exact rescan as before).  The bias is 2^21 (the row patch 64 against the
+// image's 2^15): the 1-term error reaches ~2^20 at the split's range.
+constexpr double kRowBias1 = 2097152.0;  // 2^21
+#ifdef PCR_NOSCHED
+#define SGB(...) ((void)0)
+#else
+#define SGB(...) __builtin_amdgcn_sched_group_barrier(__VA_ARGS__)
+#endif
+#ifndef PCR_VA
+#define PCR_VA ((80 - kRow8Head + 2 * NX - 1) / (2 * NX))
+#endif
+#ifndef PCR_VB
+#define PCR_VB ((80 - 16 + 2 * NX - 3) / (2 * NX - 2))
+#endif
+
+// certification threshold of the 1-term screen (scaled units), 2 x the error
+// bound; ex, E: the row's and the columns' max |x - f16(x)|, subnormal term added
+__device__ __forceinline__ double bound1(double q, double ex, double G, double E, int Kt) {
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double qg = q + G;
+    const double err = 2.0 * (Kt + 2) * u * qg * qg + 2.0 * (ex * G + (q + ex) * E) +
+                       1.1641532182693481e-10 * (q * q + G * G) + 4.0;
+    return 2.0 * err;
+}
+__device__ __forceinline__ double sub_term(int D) { return 6.103515625e-05 * __builtin_sqrt((double)D); }  // 2^-14 sqrt(D)
+
+template <int S, int G, bool kIdx, bool kOne>
 __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     constexpr int W = 8, RT = 2;                   // waves per workgroup, row tiles per wave
-    constexpr int NX = 3 * S + 1, NM = 2 * S + 1;  // executed / stored k-chunks
-    constexpr int kB = G * NM * 64;                // f16x8 per B buffer
+    constexpr int NM = 2 * S + 1;                  // stored k-chunks of the packed images
+    constexpr int NX = kOne ? S + 1 : 3 * S + 1;   // executed k-chunks (MFMAs per tile)
+    constexpr int NB = kOne ? S + 1 : NM;          // chunks per column tile in LDS / per row tile in registers
+    constexpr int kB = G * NB * 64;                // f16x8 per B buffer
+    constexpr double kBias = kOne ? kRowBias1 : kRowBias;
     static_assert(G % 2 == 0 && S <= 2, "column tiles in pairs; two row tiles fit up to S = 2");
-    __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
+    constexpr int kMerge = W * 64 * 17 * 8 / 16;  // the row merge's (b1, b2) slots, in f16x8
+    __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB > kMerge ? 2 * kB : kMerge];
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const int p = (slot / a.nrb) * 8 + xcd, rb = slot - (slot / a.nrb) * a.nrb;
+    // pair-major (a pair's row blocks back to back on its XCD, sharing its
+    // column image in that L2) or, for the short lists the 3-term screens
+    // take from the 1-term ones (one block per pair, the rest exit at once),
+    // row-block-major: pair-major placed the working blocks 16 apart in an
+    // XCD's dispatch order, and they piled onto a few of its CUs (3x slower)
+    const int ppx = (a.P + 7) >> 3;
+    const int p = a.rbmajor ? (slot % ppx) * 8 + xcd : (slot / a.nrb) * 8 + xcd;
+    const int rb = a.rbmajor ? slot / ppx : slot - (slot / a.nrb) * a.nrb;
     if (p >= a.P) return;  // whole block
-    // pass 1: the F rows in order; pass 2: the listed rows J of G (rlist)
-    const int nr = kIdx ? count_of(a.n_rows, p, a.Rmax) : a.rcount[p];
+    // the rows: in order (pass 1) or the listed ones rlist[p][0 .. rcount[p])
+    // (pass 2: J; the 3-term passes behind a 1-term one: the rows it left)
+    const int *rl = a.rlist ? a.rlist + (size_t)p * a.Rmax : nullptr;
+    const int nr = rl ? a.rcount[p] : count_of(a.n_rows, p, a.Rmax);
+    if (a.fbdiag && rb == 0 && threadIdx.x == 0 && nr > 0)
+        atomicAdd(&g_featnn_fallback_rows[a.fbdiag - 1], (unsigned long long)nr);
     if (rb * W * RT * 32 >= nr) return;  // whole block: no rows here
     const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
     const int m = count_of(a.n_cols, p, a.Cmax);
@@ -1381,13 +1459,14 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     asm("" : "+v"(keep));  // a VGPR operand: one v_and_or_b32 per code with the SGPR tile number
     // the row operand built from the f32 rows (one 128-byte row per lane, the
     // operands exactly as the pack stores them: the packed row image is not read)
-    f16x8 A[RT][NM];
+    f16x8 A[RT][NB];
+    float rex[RT];  // kOne: the row's |x - f16(x)| (rounded up)
     {
         const float sc = __uint_as_float(a.sc[p]);
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
             const int k = (qt0 + t) * 32 + (l & 31);
-            const int row = kIdx ? k : (k < nr ? a.rlist[(size_t)p * a.Rmax + k] : 0);
+            const int row = rl ? (k < nr ? rl[k] : 0) : k;
             float x[16 * S];
             const float *xr = a.Xr + ((size_t)p * a.Rmax + row) * a.D;
             if (k < nr && a.D == 16 * S && ((uintptr_t)xr & 15) == 0) {
@@ -1403,8 +1482,28 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
 #pragma unroll
                 for (int q = 0; q < 16 * S; ++q) x[q] = 0.0f;  // rows past the count write nothing
             }
-            row_frags<S>(x, a.D, h, kIdx ? 0 : 1, a.cs, A[t]);
-            if (h == 0) A[t][NM - 1][kIdx ? 6 : 7] = (_Float16)1.0f;  // the bias (see above)
+            f16x8 fr[NM];
+            row_frags<S>(x, a.D, h, a.role, a.cs, fr);
+#pragma unroll
+            for (int c = 0; c < NB; ++c) A[t][c] = fr[kOne ? (c < S ? c : 2 * S) : c];
+            // the bias (see above): 1.0 (3-term) or 64 (1-term) opposite the image's 2^15
+            const _Float16 bv = (_Float16)(kOne ? 64.0f : 1.0f);
+            if (h == 0) {
+                if (a.role == 0) A[t][NB - 1][6] = bv;
+                else A[t][NB - 1][7] = bv;
+            }
+            if constexpr (kOne) {
+                double ea = 0.0;
+#pragma unroll
+                for (int q = 0; q < 16 * S; ++q) {
+                    const double e = (double)(x[q] - (float)(_Float16)x[q]);
+                    ea = ea + e * e;
+                }
+                rex[t] = split_err_norm(ea);
+                asm volatile("" : "+v"(rex[t]));  // here, not sunk to its use after the loop (the rows stay live)
+            } else {
+                rex[t] = 0.0f;
+            }
         }
     }
     unsigned b1[RT][16], b2[RT][16];
@@ -1414,8 +1513,10 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         for (int r = 0; r < 16; ++r) { b1[t][r] = 0x7f800000u; b2[t][r] = 0x7f800000u; }
     const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
     auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NM; c += W) {
-            const f16x8 *src = bsrc + ((size_t)grp * G * NM + c) * 64;
+        for (int c = wid; c < G * NB; c += W) {
+            const int g = c / NB, cc = c - g * NB;
+            const int sch = kOne ? (cc < S ? cc : 2 * S) : cc;  // the stored chunk
+            const f16x8 *src = bsrc + ((size_t)(grp * G + g) * NM + sch) * 64;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)src,
                 (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
@@ -1440,6 +1541,9 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
             asm("" : "+v"(b2[t][r]));  // no b2 min chain across steps (it held 32 more VGPRs and spilled)
         }
     };
+    // executed chunk c -> the register / LDS chunk holding its operands
+    auto ach = [](int c) { return kOne ? c : amap(c, S); };
+    auto bch = [](int c) { return kOne ? c : bmap(c, S); };
     f32x16 acc[RT][2];
     // the first phase A finds a harmless pending epilogue: +inf with code 0
 #pragma unroll
@@ -1448,6 +1552,9 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         for (int r = 0; r < 16; ++r) acc[1][c][r] = __builtin_inff();
     unsigned pend = 0u;
     const f32x16 zero = {};
+    // VALU per phase (two tiles' epilogues): 80; spread over the phase's MFMAs
+    constexpr int kVA = PCR_VA;
+    constexpr int kVB = PCR_VB;
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1458,11 +1565,11 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         // the step's B fragments, read in MFMA order (the first MFMAs wait for
         // the first reads only): the group's first step reads them at its
         // start, every later step at the end of the previous step's phase B
-        f16x8 Bf[2][NM];
+        f16x8 Bf[2][NB];
 #pragma unroll
-        for (int c = 0; c < NM; ++c)
+        for (int c = 0; c < NB; ++c)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[(u * NM + c) * 64];
+            for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[(u * NB + c) * 64];
 #pragma unroll
         for (int st = 0; st < G / 2; ++st) {
             const unsigned ct = (unsigned)(grp * G + 2 * st);
@@ -1471,15 +1578,15 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
             for (int c = 0; c < NX; ++c)
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
-                    acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0][amap(c, S)], Bf[u][bmap(c, S)],
+                    acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0][ach(c)], Bf[u][bch(c)],
                                                                        c == 0 ? zero : acc[0][u], 0, 0, 0);
             epilogue(acc[1], 1, pend);
-            if (st == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NM, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, kRow8Head, 0);
+            if (st == 0) SGB(0x100, 2 * NB, 0);
+            SGB(0x002, kRow8Head, 0);
 #pragma unroll
             for (int i = 0; i < 2 * NX; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, (80 - kRow8Head + 2 * NX - 1) / (2 * NX), 0);
+                SGB(0x008, 1, 0);
+                SGB(0x002, kVA, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             // phase B
@@ -1487,23 +1594,23 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
             for (int c = 0; c < NX; ++c)
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
-                    acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[1][amap(c, S)], Bf[u][bmap(c, S)],
+                    acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[1][ach(c)], Bf[u][bch(c)],
                                                                        c == 0 ? zero : acc[1][u], 0, 0, 0);
             epilogue(acc[0], 0, ct);
             if (st + 1 < G / 2) {  // the next step's fragments, behind this phase's last MFMA
 #pragma unroll
-                for (int c = 0; c < NM; ++c)
+                for (int c = 0; c < NB; ++c)
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[((2 * st + 2 + u) * NM + c) * 64];
+                    for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[((2 * st + 2 + u) * NB + c) * 64];
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            SGB(0x008, 2, 0);
 #pragma unroll
             for (int i = 0; i < 2 * NX - 2; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                SGB(0x002, kVB, 0);
+                SGB(0x008, 1, 0);
             }
-            if (st + 1 < G / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NM, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+            if (st + 1 < G / 2) SGB(0x100, 2 * NB, 0);
+            SGB(0x002, 16, 0);
             __builtin_amdgcn_sched_barrier(0);
             pend = ct;
         }
@@ -1521,6 +1628,7 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     // +inf).  Stride 17: the stores and the row reads spread over the banks.
     uint2 *tl = reinterpret_cast<uint2 *>(Bs) + (size_t)wid * 64 * 17;
     const int R = l & 31, hR = (R >> 2) & 1, rR = (R & 3) + 4 * (R >> 3), j0 = 16 * h;
+    const double sub = kOne ? sub_term(a.D) : 0.0;
 #pragma unroll
     for (int t = 0; t < RT; ++t) {  // every wave runs both (the barriers), rows past nr write nothing
         const int qt = qt0 + t;
@@ -1548,35 +1656,64 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         }
         const float mb1 = __uint_as_float(B1), mb2 = __uint_as_float(B2);
         const int mi1 = (int)(B1 & ctmask) * 32 + jw;
-        const int row = qt * 32 + R;
-        if (h != 0 || row >= nr) continue;
-        if constexpr (!kIdx) {  // pass 2: the row's biased top-2 values and its bound, by original row
-            const int j = a.rlist[(size_t)p * a.Rmax + row];
-            const double e2 = 0.5 * (bound5((double)a.rnr[(size_t)p * a.ntr * 32 + j],
-                                            (double)__uint_as_float(a.cmax[p]), 16 * NX, a.D) +
-                                     4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kRowBias);
-            a.wq[(size_t)p * a.Rmax + j] = make_float4(m == 0 ? __builtin_inff() : mb1, m == 0 ? __builtin_inff() : mb2,
-                                                       (float)(e2 * (1.0 + 1e-6)), 0.0f);
+        const int k = qt * 32 + R;
+        if (h != 0 || k >= nr) continue;
+        const int row = rl ? rl[k] : k;  // the original row index
+        // this row's screen error bound (2x, as bound5): the split's or the 1-term's,
+        // plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled
+        const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+        const double Gm = (double)__uint_as_float(a.cmax[p]);
+        const double bnd = (kOne ? bound1(qn, (double)rex[t] + sub, Gm,
+                                          (double)__uint_as_float(a.cemax[p]) + sub, 16 * NX)
+                                 : bound5(qn, Gm, 16 * NX, a.D)) +
+                           4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kBias;
+        if constexpr (!kIdx) {  // pass 2: the row's biased top-2 values, its bound and the bias, by original row
+            const double e2 = 0.5 * bnd;
+            a.wq[(size_t)p * a.Rmax + row] = make_float4(m == 0 ? __builtin_inff() : mb1, m == 0 ? __builtin_inff() : mb2,
+                                                         (float)(e2 * (1.0 + 1e-6)), (float)kBias);
+            // 1-term: a column whose gap the resolve could not use goes to the
+            // 3-term screen (a.list; the 3-term pass lists nothing)
+            if (kOne && m != 0 && a.list &&
+                !((double)mb2 - (double)mb1 > 2.0 * e2 * (1.0 + 1e-6) + 1e-6 * (double)mb1))
+                a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
             continue;
         }
         const size_t o = (size_t)p * a.Rmax + row;
         if (m == 0) {
             a.nn[o] = 0;
+            if (a.nns) a.nns[o] = 0;
             a.v[o] = __builtin_inf();
             a.e[o] = 0.0f;
             continue;
         }
-        const double Gm = (double)__uint_as_float(a.cmax[p]);
-        const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
-        // bound5 plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled like bound5
-        const double bnd = bound5(qn, Gm, 16 * NX, a.D) + 4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kRowBias;
         const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
-        a.v[o] = (double)mb1 - kRowBias;  // exact (both multiples of mb1's ulp)
+        a.v[o] = (double)mb1 - kBias;  // exact (both multiples of mb1's ulp)
         a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-        // uncertified rows too: the screened argmin, which the exact rescan
-        // overwrites (featmut_jbuild, beside that rescan, may read either)
+        // the certificate: the top-2 gap against twice the per-value bound, or
+        // (1-term) against a bound on the DIFFERENCE of two values' errors.  Only
+        // columns j screened within 2 err of the winner j1 can overtake it, and
+        // for those the dot-product errors differ by at most
+        //   2 |e_x| |y_j - y_j1| + 2 |f16(x)| (|e_yj| + |e_yj1|),
+        // |y_j - y_j1| <= sqrt(D_j) + sqrt(D_j1) <= sqrt(b1 + 3 err) + sqrt(b1 + err)
+        // (b1 the winner's screened value): the row's nearest columns are much
+        // closer together than 2 max|y|.  ~20 % fewer rows to the 3-term screen.
+        double thr = bnd;
+        if constexpr (kOne) {
+            const double ex = (double)rex[t] + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
+            const double dot = 2.0 * (ex * Gm + (qn + ex) * E);       // bound1's dot-product share
+            const double rest = 0.5 * bnd - dot;                        // accumulation, norms, bias
+            const double er = 0.5 * bnd + pk * __builtin_fabs((double)mb2);
+            const double b1v = __builtin_fmax((double)mb1 - kBias, 0.0);
+            const double win = 2.0 * rest + 2.0 * ex * (__builtin_sqrt(b1v + 3.0 * er) + __builtin_sqrt(b1v + er)) +
+                               4.0 * (qn + ex) * E;
+            thr = __builtin_fmin(bnd, win * (1.0 + 1e-9));
+        }
+        // uncertified rows too: the screened argmin, which the 3-term pass or
+        // the exact rescan overwrites; J is built from the copy in nns, which
+        // nothing overwrites while featmut_jbuild reads it
         a.nn[o] = mi1;
-        if (!((double)mb2 - (double)mb1 > bnd + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
+        if (a.nns) a.nns[o] = mi1;
+        if (!((double)mb2 - (double)mb1 > thr + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
             a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
     }
 }
@@ -1589,9 +1726,11 @@ struct MutArgs {
     int *jlist, *nj;  // [P][Mmax], [P]: the rows of pass 2, ascending
     const double *v12;
     const float *e12;
-    const float4 *wq;
-    double wbias;     // the bias in wq's values (featnn_row8: kRowBias; featnn_row7: 0)
+    const float4 *wq;   // (w1, w2, e2, the bias in w1 / w2)
     const unsigned *fmax;
+    const int32_t *nns; // the screened argmins J is built from (never overwritten by the rescans)
+    const float *F, *G; // the f32 clouds and the scale the packs used: the exact distance of a
+    const unsigned *mx; // candidate whose screened value is too coarse for its column's gap
     int *flag;        // [P][Nmax + 1]: mutual 0 / 1, 2 = decided by the exact column
     int *list21, *cnt21;
     const int32_t *nn21x;
@@ -1610,7 +1749,7 @@ __global__ __launch_bounds__(1024) void featmut_jbuild(MutArgs a) {
     int *u = kLds ? jsh : ug;
     int *ps = kLds ? jsh : a.pos + (size_t)p * (a.Mmax + 1);
     int *jl = a.jlist + (size_t)p * a.Mmax;
-    const int32_t *nn = a.nn12 + (size_t)p * a.Nmax;
+    const int32_t *nn = a.nns + (size_t)p * a.Nmax;
     for (int j = threadIdx.x; j < m; j += 1024) u[j] = 0;
     __syncthreads();
     if constexpr (kLds) {
@@ -1662,14 +1801,34 @@ __global__ __launch_bounds__(256) void featmut_resolve(MutArgs a) {
         if (atomicCAS(uj, 0, 3) == 0) a.list21[(size_t)p * a.Mmax + atomicAdd(a.cnt21 + p, 1)] = j;
     } else if (j >= 0 && j < m) {
         const size_t oj = (size_t)p * a.Mmax + j;
-        const float4 q = a.wq[oj];  // featnn_row8's pass 2 stores biased values (exact in f64)
-        const double w1 = (double)q.x - a.wbias, w2 = (double)q.y - a.wbias, e2 = (double)q.z;
+        const float4 q = a.wq[oj];  // biased values (exact in f64), the bound, the bias
+        const double w1 = (double)q.x - (double)q.w, w2 = (double)q.y - (double)q.w, e2 = (double)q.z;
         const double vi = a.v12[oi];
         // slack: the f64 sums of a rescanned value vs the exact real distance
         const double sl = 1e-9 * (__builtin_fabs(w1) + __builtin_fabs(vi));
+        bool done = false;
         if (w2 - w1 > 2.0 * (e2 + e1 + sl)) {
             f = (vi <= w1 + e2 + e1 + sl) ? 1 : 0;
-        } else {
+            done = true;
+        } else if (e1 != 0.0) {
+            // the row's screened value is too coarse for this column's gap (the
+            // 1-term screen's bound): its exact distance, the oracle's f64 sum in
+            // the rescan's units, decides when the gap alone allows
+            const float *fr = a.F + oi * a.D, *gr = a.G + oj * a.D;
+            double acc = 0.0;
+            for (int k = 0; k < a.D; ++k) {
+                const double df = (double)fr[k] - (double)gr[k];
+                acc = acc + df * df;
+            }
+            const double sc = (double)__uint_as_float(a.mx[p]);
+            const double vx = acc * sc * sc;
+            const double slx = 1e-9 * (__builtin_fabs(w1) + __builtin_fabs(vx));
+            if (w2 - w1 > 2.0 * (e2 + slx)) {
+                f = (vx <= w1 + e2 + slx) ? 1 : 0;
+                done = true;
+            }
+        }
+        if (!done) {
             f = 2;
             if (atomicCAS(uj, 1, 2) == 1)
                 a.list21[(size_t)p * a.Mmax + atomicAdd(a.cnt21 + p, 1)] = j;
@@ -1721,6 +1880,8 @@ struct V5Buf {
     float *fnr, *gnr;
     unsigned *gmax, *fmax, *mx;
     int *cnt12, *cnt21, *list12, *list21;
+    unsigned *gemax, *femax;  // per pair max |x - f16(x)| of the column (G) / row (F) images
+    int *fbc12, *fbc21, *fbl12, *fbl21;  // the rows a 1-term screen left for the 3-term one
 };
 
 static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
@@ -1742,7 +1903,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     const size_t ap = (size_t)P * ntn * NM * 64, bp = (size_t)P * ntm * NM * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
-        16 * (ap + bp) + 4 * (nn_n + nn_m + 5 * (size_t)P + (size_t)P * (Nmax + Mmax) + 18 * (size_t)P);
+        16 * (ap + bp) + 4 * (nn_n + nn_m + 9 * (size_t)P + 2 * (size_t)P * (Nmax + Mmax) + 18 * (size_t)P);
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     v.Ap = (f16x8 *)ws;
@@ -1750,14 +1911,22 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.fnr = (float *)(v.Bp + bp);
     v.gnr = v.fnr + nn_n;
     // [0,P): max|y|  [P,2P): max|x|  [2P,3P): the scale used  [3P,4P): cnt12  [4P,5P): cnt21
+    // [5P,6P): gemax  [6P,7P): femax  [7P,8P): fbc12  [8P,9P): fbc21 (feat_sample clears
+    // all but the scale)
     v.gmax = (unsigned *)(v.gnr + nn_m);
     v.fmax = v.gmax + P;
     v.mx = v.gmax + 2 * P;
     v.cnt12 = (int *)(v.gmax + 3 * P);
     v.cnt21 = v.cnt12 + P;
-    v.list12 = v.cnt21 + P;                    // per pair, stride Nmax
+    v.gemax = v.gmax + 5 * P;
+    v.femax = v.gmax + 6 * P;
+    v.fbc12 = (int *)(v.gmax + 7 * P);
+    v.fbc21 = v.fbc12 + P;
+    v.list12 = v.fbc21 + P;                    // per pair, stride Nmax
     v.list21 = v.list12 + (size_t)P * Nmax;    // per pair, stride Mmax
-    unsigned *mxp = (unsigned *)(v.list21 + (size_t)P * Mmax);  // [P][2][zr] partial maxima (repair)
+    v.fbl12 = v.list21 + (size_t)P * Mmax;     // per pair, stride Nmax
+    v.fbl21 = v.fbl12 + (size_t)P * Nmax;      // per pair, stride Mmax
+    unsigned *mxp = (unsigned *)(v.fbl21 + (size_t)P * Mmax);  // [P][2][zr] partial maxima (repair)
     unsigned *smax = mxp + 2 * (size_t)P * 8;                     // [P] sample maxima
     int *bad = (int *)(smax + P);                                  // [P] repair flags
     prof_begin(s, kProfFeatPack);
@@ -1774,7 +1943,8 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
             PCR_LAUNCH_CHECK();
         }
         const int gy = rep ? R : P;
-        PackIO io{{F, G}, {n_src, n_tgt}, {Nmax, Mmax}, {ntn, ntm}, {v.Ap, v.Bp}, {v.fnr, v.gnr}, {v.fmax, v.gmax}};
+        PackIO io{{F, G}, {n_src, n_tgt}, {Nmax, Mmax}, {ntn, ntm}, {v.Ap, v.Bp}, {v.fnr, v.gnr}, {v.fmax, v.gmax},
+                  {v.femax, v.gemax}};
         const dim3 grid(cdiv(std::max(ntn, ntm), 4), gy, 2);
         if (D == 32) hipLaunchKernelGGL(feat_pack5r<32>, grid, dim3(256), 0, s, io, v.sp, pc);  // register-resident
         else hipLaunchKernelGGL(feat_pack5, grid, dim3(256), 0, s, io, D, v.S, v.sp, pc);
@@ -1908,6 +2078,27 @@ constexpr int row_group(int S) { return S <= 2 ? 8 : 4; }
 // S <= 2 is featnn_row8; other S: row_tiles
 static int pass_tiles(int S, bool pass2) { return (S == 2 && pass2) ? 1 : row_tiles(S); }
 
+// one featnn_row8 launch over a grid for all Rmax rows (list mode: the blocks
+// past the pair's count exit at once)
+template <bool kIdx, bool kOne>
+static int launch_row8(const RowArgs5 &r0, int S, hipStream_t s) {
+    RowArgs5 r = r0;
+    r.nrb = cdiv(cdiv(r.Rmax, 32), 8 * 2);  // 8 waves x 2 row tiles per workgroup
+    const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
+    PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
+    if (S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G, kIdx, kOne>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    else hipLaunchKernelGGL((featnn_row8<2, kRow8G, kIdx, kOne>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+// the 1-term screens in front of the 3-term ones (S <= 2): on by default,
+// PCR_FEAT_ONE=0 for the round-5 path (A/B, the parity tests; read per call)
+static bool feat_one_term() {
+    const char *e = getenv("PCR_FEAT_ONE");
+    return !(e && e[0] == '0');
+}
+
 // one row screen launch (pass 1: kIdx, F rows; pass 2: the J rows of G)
 template <bool kIdx>
 static int launch_row7(const RowArgs5 &r, int S, hipStream_t s, int rt) {
@@ -1942,9 +2133,9 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     if (rc != PCR_OK) return rc;
     const int ntn = v.ntn, ntm = v.ntm;
     // scratch: v12 [P][Nmax] f64 | e12 [P][Nmax] f32 | wq [P][Mmax] float4 | used, pos
-    // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P]
+    // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P] | nns [P][Nmax]
     const size_t pn = (size_t)P * Nmax, pm = (size_t)P * Mmax;
-    const size_t bytes = 8 * pn + 4 * pn + 16 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P + 16;
+    const size_t bytes = 8 * pn + 4 * pn + 16 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P + 4 * pn + 16;
     bool fresh = false;
     char *ws = (char *)workspace(33, bytes + 256, &fresh);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
@@ -1959,6 +2150,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     ma.flag = nn21x + pm;
     ma.nj = ma.flag + pn + P;
     int *zero = ma.nj + P;
+    int32_t *nns = zero + P;
+    const bool one = v.S <= 2 && feat_one_term();
     // a constant zero count per pair (read only): cleared when the slot is new
     // or was last used for fewer pairs
     static thread_local const void *z_ptr = nullptr;
@@ -1971,7 +2164,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     ma.nn12 = nn12; ma.n_src = n_src; ma.n_tgt = n_tgt; ma.Nmax = Nmax; ma.Mmax = Mmax;
     ma.mutual = mutual; ma.ransac_n = ransac_n; ma.Kt = 16 * v.NX; ma.D = D; ma.ntm = ntm;
     ma.v12 = v12; ma.e12 = e12; ma.wq = wq; ma.fmax = v.fmax;
-    ma.wbias = v.S <= 2 ? kRowBias : 0.0;
+    ma.nns = v.S <= 2 ? nns : nn12;  // featnn_row7 (S > 2) writes no copy
+    ma.F = F; ma.G = G; ma.mx = v.mx;
     ma.list21 = v.list21; ma.cnt21 = v.cnt21; ma.nn21x = nn21x;
     ma.corres = corres; ma.n_corres = n_corres;
     // pass 1: F rows x all G columns
@@ -1984,24 +2178,31 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.nn = nn12; r.v = v12; r.e = e12; r.list = v.list12; r.count = v.cnt12;
     r.wq = nullptr;
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
+    r.cemax = v.gemax; r.nns = nns; r.fbdiag = 0; r.rbmajor = 0;
     if (prep_event && prep_at == 2) {
         PCR_HIP_CHECK(hipEventRecord(prep_event, s));
         if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
         prep_fn = nullptr;
     }
     prof_begin(s, kProfFeatScreen);
-    if (v.S <= 2) {  // two column tiles per step (featnn_row8)
-        r.nrb = cdiv(cdiv(Nmax, 32), v.W * 2);
-        const long long nblk = 8LL * r.nrb * cdiv(P, 8);  // XCD-aware 1-D grid
-        PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
-        if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G, true>), dim3((unsigned)nblk), dim3(512), 0, s, r);
-        else hipLaunchKernelGGL((featnn_row8<2, kRow8G, true>), dim3((unsigned)nblk), dim3(512), 0, s, r);
-        PCR_LAUNCH_CHECK();
+    if (one) {  // two column tiles per step (featnn_row8), 1-term; the rows it leaves to the 3-term
+        r.list = v.fbl12; r.count = v.fbc12;
+        if ((rc = launch_row8<true, true>(r, v.S, s)) != PCR_OK) return rc;
+        prof_end(s, kProfFeatScreen);
+        RowArgs5 r1 = r;
+        r1.rlist = v.fbl12; r1.rcount = v.fbc12; r1.list = v.list12; r1.count = v.cnt12; r1.fbdiag = 1;
+        r1.rbmajor = 1;
+        prof_begin(s, kProfFeatScreen1b);
+        if ((rc = launch_row8<true, false>(r1, v.S, s)) != PCR_OK) return rc;
+        prof_end(s, kProfFeatScreen1b);
+    } else if (v.S <= 2) {  // the 3-term screen only
+        if ((rc = launch_row8<true, false>(r, v.S, s)) != PCR_OK) return rc;
+        prof_end(s, kProfFeatScreen);
     } else {
         rc = launch_row7<true>(r, v.S, s, rt1);
         if (rc != PCR_OK) return rc;
+        prof_end(s, kProfFeatScreen);
     }
-    prof_end(s, kProfFeatScreen);
     if (prep_event && prep_at == 1) {
         PCR_HIP_CHECK(hipEventRecord(prep_event, s));
         if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
@@ -2029,8 +2230,15 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     if (rc != PCR_OK) return rc;
     if (rs != s) PCR_HIP_CHECK(hipEventRecord(ev_join, rs));
     if (mutual) {
+        // the LDS form when its dynamic (Mmax + 1) ints fit beside the kernel's
+        // static LDS (the block scan's wave totals) in 64 KB
         const size_t jsm = sizeof(int) * ((size_t)Mmax + 1);
-        if (jsm <= 64 * 1024) {
+        static size_t jstatic = [] {
+            hipFuncAttributes fa{};
+            return hipFuncGetAttributes(&fa, (const void *)featmut_jbuild<true>) == hipSuccess
+                       ? fa.sharedSizeBytes : (size_t)1024;
+        }();
+        if (jsm + jstatic <= 64 * 1024) {
             PCR_HIP_CHECK(hipFuncSetAttribute((const void *)featmut_jbuild<true>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
             hipLaunchKernelGGL(featmut_jbuild<true>, dim3(P), dim3(1024), jsm, s, ma);
@@ -2046,21 +2254,29 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         const int rt2 = pass_tiles(v.S, true);
         r2.ntr = ntm; r2.ntc = ntn; r2.nrb = cdiv(cdiv(Mmax, 32), v.W * rt2);
         r2.nn = nullptr; r2.v = nullptr; r2.e = nullptr; r2.list = nullptr; r2.count = nullptr;
+        r2.nns = nullptr;
         r2.wq = wq;
         r2.Xr = G; r2.sc = v.mx; r2.role = 1; r2.cs = v.sp.cs;
+        r2.cemax = v.femax;
         prof_begin(s, kProfFeatScreen2);
-        if (v.S <= 2) {  // two column tiles per step, values only (featnn_row8<.., false>)
-            r2.nrb = cdiv(cdiv(Mmax, 32), v.W * 2);
-            const long long nblk = 8LL * r2.nrb * cdiv(P, 8);
-            PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
-            if (v.S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G, false>), dim3((unsigned)nblk), dim3(512), 0, s, r2);
-            else hipLaunchKernelGGL((featnn_row8<2, kRow8G, false>), dim3((unsigned)nblk), dim3(512), 0, s, r2);
-            PCR_LAUNCH_CHECK();
+        if (one) {  // values only, 1-term; the columns whose gap it cannot use go to the 3-term
+            r2.list = v.fbl21; r2.count = v.fbc21;
+            if ((rc = launch_row8<false, true>(r2, v.S, s)) != PCR_OK) return rc;
+            prof_end(s, kProfFeatScreen2);
+            RowArgs5 r2b = r2;
+            r2b.rlist = v.fbl21; r2b.rcount = v.fbc21; r2b.list = nullptr; r2b.count = nullptr; r2b.fbdiag = 2;
+            r2b.rbmajor = 1;
+            prof_begin(s, kProfFeatScreen2b);
+            if ((rc = launch_row8<false, false>(r2b, v.S, s)) != PCR_OK) return rc;
+            prof_end(s, kProfFeatScreen2b);
+        } else if (v.S <= 2) {
+            if ((rc = launch_row8<false, false>(r2, v.S, s)) != PCR_OK) return rc;
+            prof_end(s, kProfFeatScreen2);
         } else {
             rc = launch_row7<false>(r2, v.S, s, rt2);
             if (rc != PCR_OK) return rc;
+            prof_end(s, kProfFeatScreen2);
         }
-        prof_end(s, kProfFeatScreen2);
         if (rs != s) PCR_HIP_CHECK(hipStreamWaitEvent(s, ev_join, 0));
         hipLaunchKernelGGL(featmut_resolve, dim3(cdiv(Nmax, 256), P), dim3(256), 0, s, ma);
         PCR_LAUNCH_CHECK();
@@ -2171,6 +2387,20 @@ extern "C" int pcr_correspondences(const int32_t *nn12, const int32_t *nn21, int
     PCR_REQUIRE(nn12 && nn21 && corres && n_corres, PCR_ERR_ARG, "correspondences: null pointer");
     return pcr::corres_impl(nn12, nn21, n_src, n_tgt, P, Nmax, Mmax, mutual_filter, ransac_n,
                             corres, n_corres, pcr::as_stream(stream));
+}
+
+extern "C" int pcr_featnn_fallback_rows(int64_t *rows12, int64_t *cols21, int32_t reset) {
+    pcr::clear_error();
+    unsigned long long v[2] = {0, 0};
+    PCR_HIP_CHECK(hipDeviceSynchronize());
+    PCR_HIP_CHECK(hipMemcpyFromSymbol(v, HIP_SYMBOL(pcr::g_featnn_fallback_rows), sizeof(v)));
+    if (rows12) *rows12 = (int64_t)v[0];
+    if (cols21) *cols21 = (int64_t)v[1];
+    if (reset) {
+        const unsigned long long z[2] = {0, 0};
+        PCR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pcr::g_featnn_fallback_rows), z, sizeof(z)));
+    }
+    return PCR_OK;
 }
 
 extern "C" int pcr_featnn_rescan_rows(int64_t *rows12, int64_t *rows21, int32_t reset) {

@@ -151,3 +151,61 @@ def test_feature_correspondences_repair_mixed_batch(oracle, d):
         assert np.array_equal(_np(nn12)[p], e12), p
         assert int(_np(nc)[p]) == len(exp), p
         assert np.array_equal(_np(co)[p, :len(exp)], exp), p
+
+
+def _twins(rng, n, d, sep, twin_src):
+    """Near-tie descriptors for the 1-term screen: every target has a twin
+    `sep` away (relative ~1e-3 of a distance: inside the 1-term f16 screen's
+    error bound, far outside the 3-term split's), so the row screen cannot
+    order the twins and leaves nearly every row to the 3-term screen; with
+    twin_src the sources are twinned too, which does the same to the columns
+    of pass 2."""
+    a = rng.standard_normal((n, d)).astype(np.float32)
+    b = (a + 0.5 * rng.standard_normal((n, d))).astype(np.float32)
+    tw = (b + sep * rng.standard_normal((n, d))).astype(np.float32)
+    ft = np.concatenate([b, tw])[rng.permutation(2 * n)]
+    if twin_src:
+        a = np.concatenate([a, (a + sep * rng.standard_normal((n, d))).astype(np.float32)])
+    return a, ft
+
+
+@pytest.mark.parametrize("twin_src", [False, True])
+def test_one_term_fallback_near_ties(oracle, monkeypatch, twin_src):
+    """The 1-term screens' fallback (featnn_row8<.., kOne = false> over the rows
+    and J columns the 1-term screens could not certify) on near-tie descriptors:
+    the fallback runs (pcr_featnn_fallback_rows), and nn12 / the mutual set are
+    bit-exact vs the oracle and equal the 3-term-only path (PCR_FEAT_ONE=0)."""
+    from pointcloudregistration_amd import _lib
+    rng = np.random.default_rng(61)
+    fs, ft = _twins(rng, 700, 32, 1e-2, twin_src)
+    _lib.featnn_fallback_rows(reset=True)
+    co, nc, nn12 = reg.feature_correspondences(fs[None], ft[None])
+    r12, c21 = _lib.featnn_fallback_rows(reset=True)
+    assert r12 > len(fs) // 2, r12
+    if twin_src:
+        assert c21 > 0, c21
+    e12 = oracle.featnn(fs, ft)
+    exp = oracle.corres(e12, oracle.featnn(ft, fs), True, 3)
+    assert np.array_equal(_np(nn12)[0], e12)
+    assert int(_np(nc)[0]) == len(exp)
+    assert np.array_equal(_np(co)[0, :len(exp)], exp)
+    monkeypatch.setenv("PCR_FEAT_ONE", "0")
+    co3, nc3, nn3 = reg.feature_correspondences(fs[None], ft[None])
+    assert _lib.featnn_fallback_rows(reset=True) == (0, 0)
+    assert np.array_equal(_np(nn3), _np(nn12)) and int(_np(nc3)[0]) == len(exp)
+    assert np.array_equal(_np(co3)[0, :len(exp)], exp)
+
+
+@pytest.mark.parametrize("name", ["synthetic_4096", "dup_rows", "dynamic_range", "offset", "nan_rows",
+                                  "near_twins", "subnormal", "tail_above_sample", "d1"])
+def test_feature_correspondences_three_term_only(oracle, monkeypatch, name):
+    """The round-5 path (the 3-term split screens alone, PCR_FEAT_ONE=0) stays
+    bit-exact: it is what the 1-term screens fall back to."""
+    monkeypatch.setenv("PCR_FEAT_ONE", "0")
+    fs, ft = CASES[name]
+    co, nc, nn12 = reg.feature_correspondences(fs[None], ft[None])
+    e12 = oracle.featnn(fs, ft)
+    exp = oracle.corres(e12, oracle.featnn(ft, fs), True, 3)
+    assert np.array_equal(_np(nn12)[0], e12)
+    assert int(_np(nc)[0]) == len(exp)
+    assert np.array_equal(_np(co)[0, :len(exp)], exp)

@@ -39,9 +39,10 @@ def main():
     run()
     torch.cuda.synchronize()
     _lib.profile_enable(True)
-    for pid in range(9):
+    for pid in range(_lib.PROF_SLOTS):
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
+    _lib.featnn_fallback_rows(reset=True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(a.iters):
@@ -50,13 +51,16 @@ def main():
     torch.cuda.synchronize()
     prof = {name: _lib.profile_read(pid)[0] / a.iters for name, pid in
             (("screen", _lib.PROF_FEAT_SCREEN), ("rescan", _lib.PROF_FEAT_RESCAN),
-             ("pack", _lib.PROF_FEAT_PACK), ("screen2", _lib.PROF_FEAT_SCREEN2))}
+             ("pack", _lib.PROF_FEAT_PACK), ("screen2", _lib.PROF_FEAT_SCREEN2),
+             ("screen1b", _lib.PROF_FEAT_SCREEN1B), ("screen2b", _lib.PROF_FEAT_SCREEN2B))}
     rows = _lib.featnn_rescan_rows(reset=True)
+    fb = _lib.featnn_fallback_rows(reset=True)
     flops = 2.0 * a.pairs * a.n * a.n * a.d
     print(json.dumps({"pairs": a.pairs, "mode": a.mode,
                       "n": a.n, "d": a.d, "ms_total": ev0.elapsed_time(ev1) / a.iters,
                       "ms": prof, "screen_alg_tflops": flops / prof["screen"] / 1e9,
-                      "rescan_rows": [r / a.iters for r in rows]}))
+                      "rescan_rows": [r / a.iters for r in rows],
+                      "fallback_rows": [r / a.iters for r in fb]}))
 
 
 if __name__ == "__main__":
