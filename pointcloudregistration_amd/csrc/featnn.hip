@@ -68,9 +68,13 @@ __global__ __launch_bounds__(1024) void corres_build(const int32_t *nn12, const 
 //   split: x = hi + lo + e_x, hi = f16(x), lo = f16(x - hi): |e_x| <= 2^-22|x|
 //          + 2^-14 (the 2^-14 covers f16 subnormals even if flushed).
 //   operands (k order, each D-segment padded to S = ceil(D/16) chunks of 16):
-//          A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c | 0]
-//          B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo | 2^15]
-//          (k = 6 of the norm chunk: featnn_row8 sets the row's to 2.0)
+//          A_i = [-2hi | -2hi | -2lo | nx_hi nx_mid nx_lo | c c c | 0 | 2^15]
+//          B_j = [  hi |   lo |   hi | c c c | ny_hi ny_mid ny_lo | 2^15 | 0]
+//          (norm chunk k = 6 / k = 7: the bias slots.  The G image (role 1)
+//          stores 2^15 at k = 6, the F image (role 0) at k = 7; featnn_row8
+//          patches the row operand's opposite slot in registers -- 1.0 at k = 6
+//          for pass 1 (F rows), k = 7 for pass 2 (G rows), 64 for the 1-term
+//          screens -- see kRowBias / kRowBias1)
 //          nx = |x|^2 / c split into three f16 parts, c = 2^cs fits f16.
 //          Executed: NX = 3S + 1 k-chunks (one MFMA each).  Stored: NM = 2S + 1
 //          -- A as [-2hi | -2lo | norms], B as [hi | lo | norms]; the MFMA of

@@ -605,9 +605,6 @@ __global__ __launch_bounds__(kThreads) void icp_kernel(IArgs a) {
     }
 }
 
-// set while an ICP call's launches are being issued: a call that returned an
-// error in between leaves it set, and the next call re-zeroes the barrier slot
-thread_local bool t_icp_failed = false;
 
 const void *icp_fn(bool lds) {
     return lds ? (const void *)icp_kernel<true> : (const void *)icp_kernel<false>;
@@ -695,6 +692,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
     a.P3 = (double *)ws;
     a.cst = (int4 *)workspace(38, sizeof(int4) * (size_t)P * nm + 64);
     PCR_REQUIRE(a.cst, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
+    bool *icp_dirty = nullptr;
     if (a.G > 1 || two_phase) {
         const int gp = two_phase ? a.gmax2 : a.G;  // partial slots per pair
         char *cw = (char *)workspace(10, sizeof(XPart) * 2 * (size_t)gp * (size_t)P + 64);
@@ -708,12 +706,18 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         size_t nb = 16384;
         while (nb < 4 * (size_t)P) nb <<= 1;
         // A launch that failed after some of its workgroups arrived could leave
-        // arrivals behind: the call after any failed one re-zeroes.
+        // arrivals behind: the call after any failed one in this (device,
+        // context) re-zeroes.
         bool fresh = false;
         a.bar = (unsigned *)workspace(39, sizeof(unsigned) * nb, &fresh);
         PCR_REQUIRE(a.bar, PCR_ERR_NOMEM, "icp: %s", pcr_last_error());
-        if (fresh || t_icp_failed) PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * nb, s));
-        t_icp_failed = false;
+        // the slot's dirty flag (per device and workspace context, as the slot
+        // itself) is set while a call's launches are being issued: a call that
+        // returned an error in between leaves it set for the next one here
+        icp_dirty = workspace_dirty(39);
+        PCR_REQUIRE(icp_dirty, PCR_ERR_ARG, "icp: no workspace slot");
+        if (fresh || *icp_dirty) PCR_HIP_CHECK(hipMemsetAsync(a.bar, 0, sizeof(unsigned) * nb, s));
+        *icp_dirty = false;
     } else {
         a.part = nullptr;
         a.bar = nullptr;
@@ -735,7 +739,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         PCR_HIP_CHECK(hipMemsetAsync(a.ctl + 1, 0, sizeof(int), s));  // none listed
     }
     prof_begin(s, kProfIcp);
-    t_icp_failed = true;  // until every launch below went in
+    if (icp_dirty) *icp_dirty = true;  // until every launch below went in
     if (!two_phase) {
         void *args[] = {&a};
         PCR_HIP_CHECK(coop_launch(fn, P, a.G, kThreads, args, sm, s));
@@ -753,7 +757,7 @@ int icp_impl(const float *src, const float *tgt, int P, int Nmax, int Mmax, cons
         PCR_HIP_CHECK(hipLaunchCooperativeKernel(fn, dim3(grid2), dim3(kThreads), args, (unsigned)sm, s));
         PCR_LAUNCH_CHECK();
     }
-    t_icp_failed = false;
+    if (icp_dirty) *icp_dirty = false;
     prof_end(s, kProfIcp);
     if (want_timing) {  // debug: phase split in shader clocks, mean over pairs, to stderr
         std::vector<unsigned long long> h(12 * (size_t)P);

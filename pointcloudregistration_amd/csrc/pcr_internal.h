@@ -17,6 +17,9 @@ void clear_error();
 // stream never see their scratch freed.  Mutex-guarded.  *fresh (optional) tells
 // whether the buffer was (re)allocated by this call (contents undefined).
 void *workspace(int slot, size_t bytes, bool *fresh = nullptr);
+// a flag kept beside the calling thread's (device, context) buffer of `slot`
+// (false at first): set by an owner whose launches may not all have gone in
+bool *workspace_dirty(int slot);
 
 // Chamfer NN (nnd.hip / nnd_grid.hip): the size rule of pcr_nnd_forward, and
 // its grid path; _xf forms set 0 as T (x) src (transform_kernel's rounding),

@@ -25,6 +25,7 @@ namespace {
 struct Slot {
     void *ptr = nullptr;
     size_t bytes = 0;
+    bool dirty = false;  // workspace_dirty: the owner's last use did not complete
 };
 constexpr int kMaxDevices = 64;
 constexpr int kMaxSlots = 40;
@@ -42,6 +43,14 @@ int g_conc = 1;
 // slot grew still points at its old buffer)
 std::vector<std::pair<int, void *>> g_retired;
 }  // namespace
+
+bool *workspace_dirty(int slot) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices || slot < 0 || slot >= kMaxSlots)
+        return nullptr;
+    std::lock_guard<std::mutex> lk(g_mu);
+    return &g_slots[dev][t_ctx][slot].dirty;
+}
 
 void *workspace(int slot, size_t bytes, bool *fresh) {
     if (fresh) *fresh = false;

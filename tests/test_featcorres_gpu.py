@@ -209,3 +209,61 @@ def test_feature_correspondences_three_term_only(oracle, monkeypatch, name):
     assert np.array_equal(_np(nn12)[0], e12)
     assert int(_np(nc)[0]) == len(exp)
     assert np.array_equal(_np(co)[0, :len(exp)], exp)
+
+
+def _used_flags(P, Nmax, Mmax):
+    """featmut_jbuild / featmut_resolve's per-column flags of the last
+    pcr_feature_correspondences call (its scratch, pcr_featmut_debug_copy):
+    [P][Mmax + 1] ints after v12 (f64) | e12 (f32) | wq (float4, 16-aligned)."""
+    import torch
+    from pointcloudregistration_amd import _lib
+    off = ((12 * P * Nmax + 15) // 16) * 16 + 16 * P * Mmax
+    n = P * (Mmax + 1)
+    buf = torch.empty(off + 4 * n, dtype=torch.uint8, device="cuda")
+    _lib.call("pcr_featmut_debug_copy", buf.data_ptr(), buf.numel(), _lib.stream_handle())
+    torch.cuda.synchronize()
+    return _np(buf[off:].view(torch.int32)).reshape(P, Mmax + 1)
+
+
+@pytest.mark.parametrize("P", [1, 192])
+def test_resolve_outside_j(oracle, P):
+    """featmut_resolve's branch for a rescanned row whose exact argmin is outside
+    J (J is built from the screened argmins, beside the exact row rescan, which
+    runs on a side stream at P >= 192): near-twin targets make the screened
+    argmin the exact loser for about half the rows.  The branch runs (columns
+    flagged 3 in the resolve's scratch) at P = 1 and at P = 192, and every pair
+    is bit-exact vs the oracle."""
+    rng = np.random.default_rng(500 + P)
+    N, K, D = 160, 20, 32
+    M = 2 * N + K
+    fs = rng.standard_normal((P, N, D)).astype(np.float32)
+    ft = np.empty((P, M, D), np.float32)
+    for p in range(P):
+        tw = np.repeat(fs[p], 2, axis=0) + (rng.standard_normal((2 * N, D)) * 1e-6).astype(np.float32)
+        ft[p] = np.concatenate([tw, rng.standard_normal((K, D)).astype(np.float32)])[rng.permutation(M)]
+    co, nc, nn12 = reg.feature_correspondences(fs, ft)
+    used = _used_flags(P, N, M)
+    outside = (used[:, :M] == 3).sum(axis=1)
+    assert outside.min() > 0, outside
+    nn12, nc, co = _np(nn12), _np(nc), _np(co)
+    for p in range(P):
+        e12 = oracle.featnn(fs[p], ft[p])
+        exp = oracle.corres(e12, oracle.featnn(ft[p], fs[p]), True, 3)
+        assert np.array_equal(nn12[p], e12), p
+        assert int(nc[p]) == len(exp), p
+        assert np.array_equal(co[p, :len(exp)], exp), p
+
+
+def test_mutual_mmax_16383(oracle):
+    """Mmax = 16383: J's build no longer fits its LDS form beside the block
+    scan's static LDS (4 (Mmax + 1) + 64 > 64 KB) and takes the HBM form."""
+    rng = np.random.default_rng(16383)
+    fs = rng.standard_normal((300, 32)).astype(np.float32)
+    ft = rng.standard_normal((16383, 32)).astype(np.float32)
+    ft[:300] = fs + (0.1 * rng.standard_normal((300, 32))).astype(np.float32)
+    co, nc, nn12 = reg.feature_correspondences(fs[None], ft[None])
+    e12 = oracle.featnn(fs, ft)
+    exp = oracle.corres(e12, oracle.featnn(ft, fs), True, 3)
+    assert np.array_equal(_np(nn12)[0], e12)
+    assert int(_np(nc)[0]) == len(exp)
+    assert np.array_equal(_np(co)[0, :len(exp)], exp)
