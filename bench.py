@@ -35,6 +35,7 @@ PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak
 # 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md "Peak BF16/FP16 MFMA ~2.5 PF dense")
 PEAK_F16_MFMA_TFLOPS = 2516.6
 PEAK_HBM_GBS = 8000.0
+PEAK_LDS_GBS = 256 * 256 * 2.4   # 256 CUs x 256 B/clk (ds_read_b64/b128) x 2.4 GHz, in GB/s
 
 
 def parse():
@@ -840,7 +841,7 @@ def _chamfer_roofline(prof, P, N, samples):
     slots = 1024 * WAVES_PER_SIMD
     floor_ms = -(-waves // slots) * trips_w * L2_HIT_CYC / (CLOCK_GHZ_PEAK * 1e9) * 1e3
     floors = {"l2_latency_ms": floor_ms}
-    sq, src = _pmc_sq("nng_query<1>")
+    sq, src = _pmc_sq("nng_query<1>", P)
     if sq and "SQ_INSTS_VALU" in sq:
         f64 = sum(sq.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                              "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
@@ -903,29 +904,29 @@ def grid_candidates(src, tgt, T, d, slot_num=2):
 
 # Per 32 x 32 tile and wave, the inner loop of the shipped build's screens
 # (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 8
-# column tiles = 16 tiles, D = 32 -> NX = 7 k-chunks of 16):
-#  pass 1 featnn_row8<2,8,true>:  7 v_mfma_f32_32x32x16_f16, 40.1 VALU per tile
-#    (16 v_and_or_b32 tagging the u32 distance bits with the column code, and the
-#    pairs top-2 update: 8 v_med3 + 8 v_min3_u32 + 8 v_min_u32), 2.5 ds_read_b128,
-#    1.4 SALU, 0.25 s_nop;
-#  pass 2 featnn_row8<2,8,false>: 7 MFMA, 24.1 VALU (values only: no tag), 2.5 LDS,
-#    0.44 s_nop.
+# column tiles = 16 tiles, D = 32 -> the 1-term screen executes S + 1 = 3
+# k-chunks of 16: [f16(x) (2 chunks) | norms (1)]):
+#  featnn_row9<2,8,*> (passes 1 and 2, the same loop): 3 v_mfma_f32_32x32x16_f16,
+#    10.6 VALU per tile (the group-min sweep: 124 v_min3_u32 + 16 v_min + 8 x
+#    (v_max, v_cmp, v_cndmask) + 6 other per 16 tiles), 1.5 ds_read_b128,
+#    0.94 SALU, 0.69 s_nop;
 # SIMD issue cycles (MI355X guide, 'vector-instruction ISSUE cost'): an MFMA holds
-# vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the two waves of a
-# SIMD share that port.  The MFMA pipe needs 7 x 32 = 224 cycles per tile.
-SCREEN_TILE_ISSUE = {"mfma": 7 * 8, "valu": 642 / 16 * 4, "lds": 40 / 16 * 4, "s_nop": 4 / 16 * 4}
-SCREEN2_TILE_ISSUE = {"mfma": 7 * 8, "valu": 386 / 16 * 4, "lds": 40 / 16 * 4, "s_nop": 7 / 16 * 4}
+# vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the waves of a SIMD
+# share that port.  The MFMA pipe needs 3 x 32 = 96 cycles per tile.
+SCREEN_TILE_ISSUE = {"mfma": 3 * 8, "valu": 170 / 16 * 4, "lds": 24 / 16 * 4, "s_nop": 11 / 16 * 4}
+SCREEN_TILE_MFMA = 3
 
 
-def _screen_issue_model(tiles, ms, table):
+def _screen_issue_model(tiles, ms, table, mfma=SCREEN_TILE_MFMA):
     """Floor of a feature screen launch: per tile the larger of its vector-issue
-    cycles and the MFMA pipe's 224, on 1,024 SIMDs at 2.4 GHz."""
+    cycles and the MFMA pipe's (32 cycles per MFMA), on 1,024 SIMDs at 2.4 GHz."""
     issue = sum(table.values())
-    cyc = max(issue, 7 * 32)
+    pipe = mfma * 32
+    cyc = max(issue, pipe)
     floor_ms = tiles * cyc / 1024 / (CLOCK_GHZ_PEAK * 1e9) * 1e3
     return {"issue_cycles_per_tile": issue, "breakdown": table, "tiles_per_launch": tiles,
-            "mfma_pipe_cycles_per_tile": 7 * 32,
-            "binding": "vector issue" if issue > 7 * 32 else "MFMA pipe",
+            "mfma_pipe_cycles_per_tile": pipe,
+            "binding": "vector issue" if issue > pipe else "MFMA pipe",
             "floor_ms_at_2p4ghz": floor_ms, "model_frac": floor_ms / ms if ms else None}
 
 
@@ -943,24 +944,40 @@ def _newest(pattern):
     return best
 
 
-def _pmc_sq(kernel):
-    """Per-launch SQ instruction counters of `kernel` (tools/pmc_sq.sh on this
-    bench, the newest profiles/rNN/vMM_sq_pmc.json), or None."""
-    f = _newest("sq_pmc.json")
-    if f is None:
+def _pmc_sq(kernel, pairs):
+    """Per-launch SQ instruction counters of `kernel` for a launch over `pairs`
+    pairs: tools/pmc_sq.sh on this bench at the same pair count (the newest
+    profiles/rNN/vMM_sq_pmc_<P>pairs.json; vMM_sq_pmc.json is the 256-pair
+    run), or else the newest counters of another pair count scaled by the
+    pair ratio (the sweeps' work is per pair).  Returns (counters, source)."""
+    best = None
+    for pat, pp in ((f"sq_pmc_{pairs}pairs.json", pairs), ("sq_pmc.json", 256)):
+        f = _newest(pat)
+        if f is not None:
+            best = (f, pp)
+            break
+    if best is None:
         return None, None
+    f, pp = best
     try:
         with open(f) as fh:
-            ks = json.load(fh)["kernels"]
+            d = json.load(fh)
+        ks = d["kernels"]
+        pp = int(d.get("pairs", pp))
     except (OSError, ValueError, KeyError):
         return None, None
     for k, v in ks.items():
         if kernel in k:
-            return v.get("counters", v), os.path.relpath(f, ROOT)
+            c = dict(v.get("counters", v))
+            src = os.path.relpath(f, ROOT)
+            if pp != pairs:
+                c = {n: x * pairs / pp for n, x in c.items()}
+                src += f" (scaled {pairs}/{pp} pairs)"
+            return c, src
     return None, None
 
 
-def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
+def _sweep_roofline(name, kernel, prof, sweeps, N, cbar, P):
     """Roofline line of a grid-sweep kernel (RANSAC verification a7 / ICP a8).
     Its candidate gathers are served from the pair's LDS copy of the target grid,
     so the bound is VALU issue: the kernel's own executed VALU instructions (PMC
@@ -977,12 +994,16 @@ def _sweep_roofline(name, kernel, prof, sweeps, N, cbar):
     per_sweep = N * 12 + N * cbar * 12 + N / 8
     nbytes = sweeps * per_sweep
     gbs = nbytes / (per * 1e-3) / 1e9
-    sq, src = _pmc_sq(kernel)
+    sq, src = _pmc_sq(kernel, P)
     out = {"bound": "valu-issue", "kernel": kernel, "kernel_ms_per_launch": per, "launches": n,
            "sweeps_per_launch": sweeps, "c_bar": cbar,
            "lds_served": {"algorithmic_bytes_per_launch": nbytes, "achieved_gbs": gbs,
+                          "peak_gbs": PEAK_LDS_GBS, "frac": gbs / PEAK_LDS_GBS,
                           "note": f"{name}: candidate gathers read the pair's LDS copy of its "
-                                  "target grid; HBM sees the points once per launch"},
+                                  "target grid; HBM sees the points once per launch.  frac: "
+                                  "SURVEY 8d's algorithmic bytes per sweep against the chip's LDS "
+                                  "rate (256 CUs x 256 B/clk x 2.4 GHz, MI355X guide 'LDS')"},
+           "algorithmic_frac": gbs / PEAK_LDS_GBS,
            "traffic": _pmc_traffic(kernel), "frac": None}
     if sq and "SQ_INSTS_VALU" in sq:
         # the largest launch's counts (`*_max`; RANSAC launches its sweep twice a
@@ -1246,6 +1267,7 @@ def main():
     for pid in range(_lib.PROF_SLOTS):
         _lib.profile_read(pid, reset=True)
     _lib.featnn_rescan_rows(reset=True)
+    _lib.featnn_fallback_rows(reset=True)
     pwall, _ = run_timed(step, args.steps, 0, world)
     if S > 1:
         _lib.call("pcr_set_concurrency", 1)
@@ -1254,9 +1276,11 @@ def main():
              ("ransac_validate", _lib.PROF_RANSAC_VALIDATE), ("ransac_hyp", _lib.PROF_RANSAC_HYP),
              ("icp", _lib.PROF_ICP), ("feat_rescan", _lib.PROF_FEAT_RESCAN),
              ("feat_pack", _lib.PROF_FEAT_PACK), ("nnd_grid_query", _lib.PROF_NND_GRID),
-             ("feature_screen2", _lib.PROF_FEAT_SCREEN2))}
+             ("feature_screen2", _lib.PROF_FEAT_SCREEN2), ("feature_screen1b", _lib.PROF_FEAT_SCREEN1B),
+             ("feature_screen2b", _lib.PROF_FEAT_SCREEN2B), ("feat_regroup", _lib.PROF_FEAT_REGROUP))}
     _lib.profile_enable(False)
     rescan_rows = _lib.featnn_rescan_rows(reset=True)
+    fallback_rows = _lib.featnn_fallback_rows(reset=True)
 
     # stage split of one extra (untimed) step
     pipe.run(time_stages=True)
@@ -1264,27 +1288,28 @@ def main():
     stages = dict(zip(("feature_match", "corres+ransac", "icp", "transform", "chamfer"),
                       pipe.stage_ms()))
 
-    # dominant kernel: pass 1 of the feature screen, featnn_row8 (one launch = the
-    # source->target row screen of all P pairs, index packed in).  Algorithmic
-    # work: the P*N*M*D MACs of the distance matrix = 2*P*N*M*D flops,
-    # which pass 1 computes in full; pass 2 re-screens only the target rows J that
-    # some source chose (the mutual check), so the screen STAGE (pass 1 + pass 2)
-    # is also reported against the same algorithmic flops.  Both run on the f16
-    # MFMA with a 3-term split: 16*NCH k-steps per tile (NCH = ceil((3D+6)/16))
-    # instead of D -> executed flops.
+    # dominant kernel: pass 1 of the feature screen, featnn_row9 (one launch = the
+    # source->target row screen of all P pairs).  Algorithmic work:
+    # the P*N*M*D MACs of the distance matrix = 2*P*N*M*D flops, which pass 1
+    # computes in full; pass 2 re-screens only the target rows J that some
+    # source chose (the mutual check), so the screen STAGE (pass 1 + pass 2 +
+    # their regroups and 3-term fallbacks) is also reported against the same
+    # algorithmic flops.  The 1-term screen executes 16*(ceil(D/16)+1) k-steps
+    # per tile (the f16 values and one norm chunk) instead of D.
     ms_tot, launches = prof["feature_screen"]
     per_launch_ms = ms_tot / max(launches, 1)
     ms2_tot, launches2 = prof["feature_screen2"]
     per2_ms = ms2_tot / max(launches2, 1)
     flops_launch = 2.0 * P * N * N * D
-    kexec = 16 * -(-(3 * D + 6) // 16)
+    kexec = 16 * (-(-D // 16) + 1)
     achieved = flops_launch / (per_launch_ms * 1e-3) / 1e12
     executed = achieved * kexec / D
     nn12 = torch.sort(pipe.nn12, dim=1).values
     jrows = ((nn12[:, 1:] != nn12[:, :-1]).sum(1) + 1).cpu().numpy().astype(np.int64)
     tiles1 = P * (-(-N // 32)) * (-(-N // 32))
     tiles2 = int(sum(-(-int(j) // 32) for j in jrows)) * (-(-N // 32))
-    stage_ms = per_launch_ms + per2_ms
+    extra_ms = sum(prof[k][0] for k in ("feature_screen1b", "feature_screen2b", "feat_regroup")) / args.steps
+    stage_ms = per_launch_ms + per2_ms + extra_ms
     stage_tf = flops_launch / (stage_ms * 1e-3) / 1e12
 
     recs = rec.cpu().numpy()
@@ -1319,8 +1344,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32 xyz/features; f64 RANSAC/ICP; f16x3-split MFMA screen (certified bound) "
-                 "+ f64 exact re-rank",
+        "dtype": "f32 xyz/features; f64 RANSAC/ICP; 1-term f16 MFMA screen (certified bound), "
+                 "f16x3-split MFMA screen for the rows it leaves, f64 exact re-rank",
         "data": f"synthetic: procedural surface pairs, ROPNet-style augmentation, D={D} "
                 f"descriptors (noise {args.feat_noise}), generated per rank (seeds 1000+pair)",
         "config": {"workload": "C4: batch of augmented TOF/PC pairs (featNN+RANSAC+ICP+Chamfer)",
@@ -1331,37 +1356,44 @@ def main():
                    "inputs": "resident in HBM (see host_resident for the PCIe-inclusive rate)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_F16_MFMA_TFLOPS,
-                     "traffic": _pmc_traffic("featnn_row8<", "true"),
+                     "traffic": _pmc_traffic("featnn_row9<", "true>"),
                      "traffic_source": f"{_traffic_source()} (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this bench; FETCH_SIZE x2 per the "
                                        "gfx950 note)",
-                     "kernel": "featnn_row8<2,8,true> (pass 1: v_mfma_f32_32x32x16_f16, f16x3 "
-                               "split, row top-2 on biased u32 bits tagged with the column code)",
+                     "kernel": "featnn_row9<2,8,true> (pass 1: 1-term f16 screen on "
+                               "v_mfma_f32_32x32x16_f16 with the operands transposed -- a lane "
+                               "holds one row -- and a group-min sweep; featnn_regroup9 recovers "
+                               "the winning group's column and second value)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,
                      "executed_mfma_tflops": executed,
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS,
                      "issue_model": _screen_issue_model(tiles1, per_launch_ms, SCREEN_TILE_ISSUE),
-                     "pass2": {"kernel": "featnn_row8<2,8,false> (target rows J = unique(nn12), "
+                     "pass2": {"kernel": "featnn_row9<2,8,false> (target rows J = unique(nn12), "
                                          "values only)",
                                "kernel_ms_per_launch": per2_ms, "launches": launches2,
                                "j_rows_mean": float(jrows.mean()),
                                "flops_per_launch": 2.0 * float(jrows.sum()) * N * D,
-                               "traffic": _pmc_traffic("featnn_row8<", "false"),
-                               "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN2_TILE_ISSUE)},
+                               "traffic": _pmc_traffic("featnn_row9<", "false>"),
+                               "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN_TILE_ISSUE)},
                      "screen_stage": {"ms_per_launch": stage_ms, "achieved": stage_tf,
                                       "frac": stage_tf / PEAK_F16_MFMA_TFLOPS,
-                                      "note": "pass 1 + pass 2 against the distance matrix's "
+                                      "parts_ms_per_step": {k: prof[k][0] / args.steps for k in (
+                                          "feature_screen", "feature_screen2", "feat_regroup",
+                                          "feature_screen1b", "feature_screen2b")},
+                                      "note": "pass 1 + pass 2 + their regroups + the 3-term "
+                                              "fallback screens against the distance matrix's "
                                               "2*P*N*M*D algorithmic flops"}},
         "roofline_chamfer": _chamfer_roofline(prof["nnd_grid_query"], P, N, chamfer_samples),
         "roofline_ransac": _sweep_roofline("a7 RANSAC verification", "ransac_sweep_kernel",
-                                           prof["ransac_validate"], validated, N, cb_r),
-        "roofline_icp": _sweep_roofline("a8 ICP", "icp_kernel", prof["icp"], icp_sweeps, N, cb_i),
+                                           prof["ransac_validate"], validated, N, cb_r, P),
+        "roofline_icp": _sweep_roofline("a8 ICP", "icp_kernel", prof["icp"], icp_sweeps, N, cb_i, P),
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
         "profiled_ms_per_step": pwall / args.steps * 1e3,  # the steps kernels_ms_per_step came from
         "step_graph": graphed,  # the headline steps were replays of the captured step
         "featnn_rescan_rows_per_step": [r / args.steps for r in rescan_rows],
+        "featnn_fallback_rows_per_step": [r / args.steps for r in fallback_rows],
         "stages_ms": stages,
         "accuracy": {"rre_deg_median": float(np.median(rre)), "rre_deg_max": float(np.max(rre)),
                      "rte_median": float(np.median(rte)), "rte_max": float(np.max(rte)),

@@ -64,7 +64,8 @@ int pcr_coop_probe(int32_t *out, int32_t blocks, int32_t cooperative, pcr_stream
 /* Optional per-kernel timing with HIP events recorded on the launch stream
  * around the hot kernels (id 0 feature screen (pass 1), 1 nnd forward, 2 RANSAC verify,
  * 3 ICP, 4 RANSAC hypotheses, 5 feature rescan, 6 feature pack, 7 nnd grid query,
- * 8 feature screen pass 2, 9 / 10 the 3-term screens behind passes 1 / 2).  pcr_profile_read synchronizes the pending
+ * 8 feature screen pass 2, 9 / 10 the 3-term screens behind passes 1 / 2, 11 the 1-term
+ * screens' regroup and finish, featnn_regroup9 / featnn_finish9).  pcr_profile_read synchronizes the pending
  * events and returns the accumulated milliseconds and launch count. */
 void pcr_profile_enable(int32_t on);
 int pcr_profile_read(int32_t id, double *total_ms, int64_t *count, int32_t reset);

@@ -167,7 +167,8 @@ def exported_symbols():
 PROF_FEAT_SCREEN, PROF_NND_FWD, PROF_RANSAC_VALIDATE, PROF_ICP, PROF_RANSAC_HYP = 0, 1, 2, 3, 4
 PROF_FEAT_RESCAN, PROF_FEAT_PACK, PROF_NND_GRID, PROF_FEAT_SCREEN2 = 5, 6, 7, 8
 PROF_FEAT_SCREEN1B, PROF_FEAT_SCREEN2B = 9, 10   # the 3-term screens behind the 1-term ones
-PROF_SLOTS = 11   # pcr_internal.h kProfSlots
+PROF_FEAT_REGROUP = 11   # featnn_regroup9 + featnn_finish9 (both passes)
+PROF_SLOTS = 12   # pcr_internal.h kProfSlots
 
 
 # bumped by every shutdown(): a HIP graph captured before it points at freed

@@ -268,6 +268,7 @@ struct PackIO {
     float *nrm[2];
     unsigned *nmax[2];
     unsigned *emax[2];  // per pair: max over the cloud's rows of |x s - f16(x s)| (the 1-term screen's bound)
+    float *rex[2];      // per row: its |x s - f16(x s)| (rounded up; featnn_regroup9's bound)
 };
 
 // |x - f16(x)| of one row (x already scaled), rounded up: e^2 summed exactly
@@ -397,7 +398,10 @@ __global__ __launch_bounds__(256) void feat_pack5(PackIO io, int D, int S, Split
         // L2: ~80 us per launch whatever the batch.  Max of the bit patterns: the
         // same word per-lane atomics would leave, NaN included.
         const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
-        if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+        if (h == 0) {
+            nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+            io.rex[role][(size_t)p * ntiles * 32 + t * 32 + rr] = valid ? split_err_norm(ea) : 0.0f;
+        }
         block_max_atomic(__float_as_uint(r), wmax, nmax + p);
         __syncthreads();
         block_max_atomic(valid ? __float_as_uint(split_err_norm(ea)) : 0u, wmax, io.emax[role] + p);
@@ -511,7 +515,10 @@ __global__ __launch_bounds__(256) void feat_pack5r(PackIO io, Split5 sp, PackCtl
         }
         // the pair's max norm: one atomic per WORKGROUP (see feat_pack5)
         const float r = (h == 0 && valid) ? (float)__builtin_sqrt(acc) : 0.0f;
-        if (h == 0) nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+        if (h == 0) {
+            nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
+            io.rex[role][(size_t)p * ntiles * 32 + t * 32 + rr] = valid ? split_err_norm(ea) : 0.0f;
+        }
         block_max_atomic(__float_as_uint(r), wmax, nmax + p);
         __syncthreads();
         block_max_atomic(valid ? __float_as_uint(split_err_norm(ea)) : 0u, wmax, io.emax[role] + p);
@@ -1065,6 +1072,12 @@ struct RowArgs5 {
     int32_t *nns;               // pass 1: a copy of the screened argmin for featmut_jbuild (nullable)
     int fbdiag;                 // 1 / 2: count the listed rows in g_featnn_fallback_rows[0 / 1]
     int rbmajor;                // featnn_row8: blocks ordered row block first (short lists, below)
+    const float *rre;           // the rows' |x - f16(x)| from the pack, [P][ntr * 32]
+    // featnn_row9's buckets (rows by winning step): [P][steps] counts and
+    // [P][steps][bcap] entries (row, B1, B2, lane half of the winning group)
+    int *bcnt, bcap;
+    uint4 *blist;
+    uint4 *rec;                 // featnn_regroup9 -> featnn_finish9, by row: (column, B1, B2, skip)
 };
 
 // rows (pass 1) and J columns (pass 2) the 1-term screens left to the 3-term
@@ -1425,6 +1438,72 @@ __device__ __forceinline__ double bound1(double q, double ex, double G, double E
 }
 __device__ __forceinline__ double sub_term(int D) { return 6.103515625e-05 * __builtin_sqrt((double)D); }  // 2^-14 sqrt(D)
 
+// The certification and outputs of one screened row (featnn_row8's tail, and
+// featnn_finish9's): B1 / B2 the row's smallest and second smallest biased
+// value patterns, mi1 the column of B1, rexv the row's |x - f16(x)| (1-term),
+// pk the relative truncation of the values' low bits (the column code of
+// featnn_row8 pass 1; 0 when the values carry no code).  Returns whether the
+// row goes to a.list (the caller appends it)
+template <bool kIdx, bool kOne, int NX>
+__device__ __forceinline__ bool row_tail(const RowArgs5 &a, int p, int row, int m, unsigned B1, unsigned B2,
+                                         int mi1, float rexv, double pk) {
+    constexpr double kBias = kOne ? kRowBias1 : kRowBias;
+    const double sub = kOne ? sub_term(a.D) : 0.0;
+    const float mb1 = __uint_as_float(B1), mb2 = __uint_as_float(B2);
+    // this row's screen error bound (2x, as bound5): the split's or the 1-term's,
+    // plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled
+    const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+    const double Gm = (double)__uint_as_float(a.cmax[p]);
+    const double bnd = (kOne ? bound1(qn, (double)rexv + sub, Gm,
+                                      (double)__uint_as_float(a.cemax[p]) + sub, 16 * NX)
+                             : bound5(qn, Gm, 16 * NX, a.D)) +
+                       4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kBias;
+    if constexpr (!kIdx) {  // pass 2: the row's biased top-2 values, its bound and the bias, by original row
+        const double e2 = 0.5 * bnd;
+        a.wq[(size_t)p * a.Rmax + row] = make_float4(m == 0 ? __builtin_inff() : mb1, m == 0 ? __builtin_inff() : mb2,
+                                                     (float)(e2 * (1.0 + 1e-6)), (float)kBias);
+        // 1-term: a column whose gap the resolve could not use goes to the
+        // 3-term screen (a.list; the 3-term pass lists nothing)
+        return kOne && m != 0 && a.list &&
+               !((double)mb2 - (double)mb1 > 2.0 * e2 * (1.0 + 1e-6) + 1e-6 * (double)mb1);
+    }
+    const size_t o = (size_t)p * a.Rmax + row;
+    if (m == 0) {
+        a.nn[o] = 0;
+        if (a.nns) a.nns[o] = 0;
+        a.v[o] = __builtin_inf();
+        a.e[o] = 0.0f;
+        return false;
+    }
+    a.v[o] = (double)mb1 - kBias;  // exact (both multiples of mb1's ulp)
+    a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
+    // the certificate: the top-2 gap against twice the per-value bound, or
+    // (1-term) against a bound on the DIFFERENCE of two values' errors.  Only
+    // columns j screened within 2 err of the winner j1 can overtake it, and
+    // for those the dot-product errors differ by at most
+    //   2 |e_x| |y_j - y_j1| + 2 |f16(x)| (|e_yj| + |e_yj1|),
+    // |y_j - y_j1| <= sqrt(D_j) + sqrt(D_j1) <= sqrt(b1 + 3 err) + sqrt(b1 + err)
+    // (b1 the winner's screened value): the row's nearest columns are much
+    // closer together than 2 max|y|.  ~20 % fewer rows to the 3-term screen.
+    double thr = bnd;
+    if constexpr (kOne) {
+        const double ex = (double)rexv + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
+        const double dot = 2.0 * (ex * Gm + (qn + ex) * E);       // bound1's dot-product share
+        const double rest = 0.5 * bnd - dot;                        // accumulation, norms, bias
+        const double er = 0.5 * bnd + pk * __builtin_fabs((double)mb2);
+        const double b1v = __builtin_fmax((double)mb1 - kBias, 0.0);
+        const double win = 2.0 * rest + 2.0 * ex * (__builtin_sqrt(b1v + 3.0 * er) + __builtin_sqrt(b1v + er)) +
+                           4.0 * (qn + ex) * E;
+        thr = __builtin_fmin(bnd, win * (1.0 + 1e-9));
+    }
+    // uncertified rows too: the screened argmin, which the 3-term pass or
+    // the exact rescan overwrites; J is built from the copy in nns, which
+    // nothing overwrites while featmut_jbuild reads it
+    a.nn[o] = mi1;
+    if (a.nns) a.nns[o] = mi1;
+    return !((double)mb2 - (double)mb1 > thr + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)));
+}
+
 template <int S, int G, bool kIdx, bool kOne>
 __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     constexpr int W = 8, RT = 2;                   // waves per workgroup, row tiles per wave
@@ -1632,7 +1711,6 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     // +inf).  Stride 17: the stores and the row reads spread over the banks.
     uint2 *tl = reinterpret_cast<uint2 *>(Bs) + (size_t)wid * 64 * 17;
     const int R = l & 31, hR = (R >> 2) & 1, rR = (R & 3) + 4 * (R >> 3), j0 = 16 * h;
-    const double sub = kOne ? sub_term(a.D) : 0.0;
 #pragma unroll
     for (int t = 0; t < RT; ++t) {  // every wave runs both (the barriers), rows past nr write nothing
         const int qt = qt0 + t;
@@ -1658,68 +1736,409 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
             B1 = take ? o1 : B1;
             jw = take ? oj : jw;
         }
-        const float mb1 = __uint_as_float(B1), mb2 = __uint_as_float(B2);
         const int mi1 = (int)(B1 & ctmask) * 32 + jw;
         const int k = qt * 32 + R;
         if (h != 0 || k >= nr) continue;
         const int row = rl ? rl[k] : k;  // the original row index
-        // this row's screen error bound (2x, as bound5): the split's or the 1-term's,
-        // plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled
-        const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
-        const double Gm = (double)__uint_as_float(a.cmax[p]);
-        const double bnd = (kOne ? bound1(qn, (double)rex[t] + sub, Gm,
-                                          (double)__uint_as_float(a.cemax[p]) + sub, 16 * NX)
-                                 : bound5(qn, Gm, 16 * NX, a.D)) +
-                           4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kBias;
-        if constexpr (!kIdx) {  // pass 2: the row's biased top-2 values, its bound and the bias, by original row
-            const double e2 = 0.5 * bnd;
-            a.wq[(size_t)p * a.Rmax + row] = make_float4(m == 0 ? __builtin_inff() : mb1, m == 0 ? __builtin_inff() : mb2,
-                                                         (float)(e2 * (1.0 + 1e-6)), (float)kBias);
-            // 1-term: a column whose gap the resolve could not use goes to the
-            // 3-term screen (a.list; the 3-term pass lists nothing)
-            if (kOne && m != 0 && a.list &&
-                !((double)mb2 - (double)mb1 > 2.0 * e2 * (1.0 + 1e-6) + 1e-6 * (double)mb1))
-                a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
-            continue;
-        }
-        const size_t o = (size_t)p * a.Rmax + row;
-        if (m == 0) {
-            a.nn[o] = 0;
-            if (a.nns) a.nns[o] = 0;
-            a.v[o] = __builtin_inf();
-            a.e[o] = 0.0f;
-            continue;
-        }
-        const double pk = __builtin_ldexp(1.0, a.ctbits - 23);
-        a.v[o] = (double)mb1 - kBias;  // exact (both multiples of mb1's ulp)
-        a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
-        // the certificate: the top-2 gap against twice the per-value bound, or
-        // (1-term) against a bound on the DIFFERENCE of two values' errors.  Only
-        // columns j screened within 2 err of the winner j1 can overtake it, and
-        // for those the dot-product errors differ by at most
-        //   2 |e_x| |y_j - y_j1| + 2 |f16(x)| (|e_yj| + |e_yj1|),
-        // |y_j - y_j1| <= sqrt(D_j) + sqrt(D_j1) <= sqrt(b1 + 3 err) + sqrt(b1 + err)
-        // (b1 the winner's screened value): the row's nearest columns are much
-        // closer together than 2 max|y|.  ~20 % fewer rows to the 3-term screen.
-        double thr = bnd;
-        if constexpr (kOne) {
-            const double ex = (double)rex[t] + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
-            const double dot = 2.0 * (ex * Gm + (qn + ex) * E);       // bound1's dot-product share
-            const double rest = 0.5 * bnd - dot;                        // accumulation, norms, bias
-            const double er = 0.5 * bnd + pk * __builtin_fabs((double)mb2);
-            const double b1v = __builtin_fmax((double)mb1 - kBias, 0.0);
-            const double win = 2.0 * rest + 2.0 * ex * (__builtin_sqrt(b1v + 3.0 * er) + __builtin_sqrt(b1v + er)) +
-                               4.0 * (qn + ex) * E;
-            thr = __builtin_fmin(bnd, win * (1.0 + 1e-9));
-        }
-        // uncertified rows too: the screened argmin, which the 3-term pass or
-        // the exact rescan overwrites; J is built from the copy in nns, which
-        // nothing overwrites while featmut_jbuild reads it
-        a.nn[o] = mi1;
-        if (a.nns) a.nns[o] = mi1;
-        if (!((double)mb2 - (double)mb1 > thr + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2))))
+        if (row_tail<kIdx, kOne, NX>(a, p, row, m, B1, B2, mi1, rex[t], __builtin_ldexp(1.0, a.ctbits - 23)))
             a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Round 6: the 1-term screens without a per-value index (featnn_row9, then
+// featnn_regroup9).  featnn_row8 spends 2.5 VALU per screened value -- the
+// column code OR-ed into the low bits (1) and the running top-2 (1.5) -- i.e.
+// 40 VALU per 32 x 32 tile beside 3 MFMAs (96 pipe cycles): the 1-term pass
+// is VALU-issue bound (~190 issue cycles per tile).  featnn_row9 swaps the
+// MFMA's operands (the column fragments as A, the row's as B: the tile's
+// transpose), so a lane holds ONE row and 16 columns of each column tile
+// (register r: column 8 (r / 4) + 4 h + (r % 4), h the lane half).  A lane's
+// 32 values of a step (two column tiles) form a group, and the sweep keeps
+// per lane only
+//   B1 -- the smallest value,
+//   B2 -- the second smallest GROUP minimum,
+//   I  -- the step of B1's group:
+// 16 v_min3 + 5 VALU per step and row tile (10.5 per tile): the loop is
+// MFMA-pipe bound.  The lane halves merge at the end (a row's other half is
+// another set of groups).  What the sweep does not know -- the argmin's column
+// and the second smallest value INSIDE the winning group -- featnn_regroup9
+// recovers by re-running the identical MFMA chain (same operands, same order:
+// bit-identical values) for the winning step only: a pair's rows bucketed by
+// that step, one 32-row tile per bucket segment (~1 % of the sweep's MFMAs).
+// Then second = min(B2, the group's own second) exactly, the values carry no
+// code bits (pk = 0), and the certification and outputs are featnn_row8's
+// (row_tail).
+// ---------------------------------------------------------------------------
+
+// The 1-term row operand of one row (lane half h) built from its f32 values,
+// exactly as the packs store its [f16 segment | norms] chunks (row_frags), with
+// the bias patch 64 opposite the column image's 2^15 (see featnn_row8): one
+// 128-byte line per row where the packed image spreads it over S + 1 lines --
+// the regroup gathers rows.  The sweep and the regroup both build it here, so
+// their MFMA chains agree bit for bit.
+template <int S>
+__device__ __forceinline__ void row_operand1(const RowArgs5 &a, int p, int row, bool valid, int h,
+                                             f16x8 (&A)[S + 1]) {
+    const float sc = __uint_as_float(a.sc[p]);
+    float x[16 * S];
+    const float *xr = a.Xr + ((size_t)p * a.Rmax + row) * a.D;
+    if (valid && a.D == 16 * S && ((uintptr_t)xr & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < 4 * S; ++q) {
+            const float4 v = reinterpret_cast<const float4 *>(xr)[q];
+            x[4 * q] = v.x * sc; x[4 * q + 1] = v.y * sc; x[4 * q + 2] = v.z * sc; x[4 * q + 3] = v.w * sc;
+        }
+    } else if (valid) {
+#pragma unroll
+        for (int q = 0; q < 16 * S; ++q) x[q] = q < a.D ? xr[q] * sc : 0.0f;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16 * S; ++q) x[q] = 0.0f;
+    }
+    f16x8 fr[2 * S + 1];
+    row_frags<S>(x, a.D, h, a.role, a.cs, fr);
+#pragma unroll
+    for (int c = 0; c < S + 1; ++c) A[c] = fr[c < S ? c : 2 * S];
+    if (h == 0) {
+        if (a.role == 0) A[S][6] = (_Float16)64.0f;
+        else A[S][7] = (_Float16)64.0f;
+    }
+}
+
+__device__ __forceinline__ unsigned fbits(float v) { return __float_as_uint(v); }
+
+// min of a lane's 32 values of one step (two column tiles): three v_min3 chains
+__device__ __forceinline__ unsigned group_min32(const f32x16 &x, const f32x16 &y) {
+    unsigned c0 = umin2(umin2(fbits(x[0]), fbits(x[1])), fbits(x[2]));
+    unsigned c1 = umin2(umin2(fbits(x[11]), fbits(x[12])), fbits(x[13]));
+    unsigned c2 = umin2(umin2(fbits(y[6]), fbits(y[7])), fbits(y[8]));
+#pragma unroll
+    for (int r = 3; r < 11; r += 2) c0 = umin2(umin2(c0, fbits(x[r])), fbits(x[r + 1]));
+    c1 = umin2(umin2(c1, fbits(x[14])), fbits(x[15]));
+#pragma unroll
+    for (int r = 0; r < 6; r += 2) c1 = umin2(umin2(c1, fbits(y[r])), fbits(y[r + 1]));
+#pragma unroll
+    for (int r = 9; r < 15; r += 2) c2 = umin2(umin2(c2, fbits(y[r])), fbits(y[r + 1]));
+    c2 = umin2(c2, fbits(y[15]));
+    return umin2(umin2(c0, c1), c2);
+}
+
+// kIdx: pass 1 / pass 2 (the same code; two names for the profiles)
+template <int S, int G, bool kIdx>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void featnn_row9(RowArgs5 a) {
+    constexpr int W = 8, RT = 2;          // waves per workgroup, row tiles per wave
+    constexpr int NM = 2 * S + 1;         // stored k-chunks of the packed images
+    constexpr int NB = S + 1;             // executed chunks: [f16 segment | norms]
+    constexpr int kB = G * NB * 64;       // f16x8 per B buffer
+    static_assert(G % 2 == 0 && S <= 2, "column tiles in pairs");
+    __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int ppx = (a.P + 7) >> 3;
+    const int p = a.rbmajor ? (slot % ppx) * 8 + xcd : (slot / a.nrb) * 8 + xcd;
+    const int rb = a.rbmajor ? slot / ppx : slot - (slot / a.nrb) * a.nrb;
+    if (p >= a.P) return;  // whole block
+    const int *rl = a.rlist ? a.rlist + (size_t)p * a.Rmax : nullptr;
+    const int nr = rl ? a.rcount[p] : count_of(a.n_rows, p, a.Rmax);
+    if (rb * W * RT * 32 >= nr) return;  // whole block: no rows here
+    const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const int m = count_of(a.n_cols, p, a.Cmax);
+    const int qt0 = (rb * W + wid) * RT;  // this wave's first row tile
+    const int ntc = (m + 31) >> 5;
+    const int ngroups = (ntc + G - 1) / G;
+    f16x8 A[RT][NB];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+        const int k = (qt0 + t) * 32 + (l & 31);
+        row_operand1<S>(a, p, rl ? (k < nr ? rl[k] : 0) : k, k < nr, h, A[t]);
+    }
+    unsigned B1[RT], B2[RT], I[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) { B1[t] = 0x7f800000u; B2[t] = 0x7f800000u; I[t] = 0u; }
+    const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
+    auto issue = [&](int grp, int bufi) {
+        for (int c = wid; c < G * NB; c += W) {
+            const int g = c / NB, cc = c - g * NB;
+            const int sch = cc < S ? cc : 2 * S;  // the stored chunk
+            const f16x8 *src = bsrc + ((size_t)(grp * G + g) * NM + sch) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)src,
+                (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
+        }
+    };
+    // row tile t's group of step st: the values of column tiles 2 st, 2 st + 1
+    auto epilogue = [&](const f32x16 (&x)[2], int t, unsigned st) {
+        const unsigned mn = group_min32(x[0], x[1]);
+        const unsigned n2 = umin2(umax2(B1[t], mn), B2[t]);  // 2nd smallest of {B1, B2, mn}
+        I[t] = mn < B1[t] ? st : I[t];
+        B1[t] = umin2(B1[t], mn);
+        B2[t] = n2;
+    };
+    f32x16 acc[RT][2];
+    // the first phase A finds a harmless pending epilogue: +inf
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[1][c][r] = __builtin_inff();
+    unsigned pend = 0u;
+    const f32x16 zero = {};
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngroups; ++grp) {
+        const int buf = grp & 1;
+        if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
+        const f16x8 *Bb = Bs + buf * kB + l;
+        f16x8 Bf[2][NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[(u * NB + c) * 64];
+#pragma unroll
+        for (int st = 0; st < G / 2; ++st) {
+            const unsigned stp = (unsigned)(grp * (G / 2) + st);
+            // phase A: row tile 0's MFMAs beside row tile 1's previous epilogue
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[0][c],
+                                                                       c == 0 ? zero : acc[0][u], 0, 0, 0);
+            epilogue(acc[1], 1, pend);
+            if (st == 0) SGB(0x100, 2 * NB, 0);
+            SGB(0x002, 3, 0);
+#pragma unroll
+            for (int i = 0; i < 2 * NB; ++i) {
+                SGB(0x008, 1, 0);
+                SGB(0x002, 3, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // phase B: row tile 1's MFMAs beside row tile 0's epilogue
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[1][c],
+                                                                       c == 0 ? zero : acc[1][u], 0, 0, 0);
+            epilogue(acc[0], 0, stp);
+            if (st + 1 < G / 2) {  // the next step's fragments, behind this phase's MFMAs
+#pragma unroll
+                for (int c = 0; c < NB; ++c)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[((2 * st + 2 + u) * NB + c) * 64];
+            }
+            SGB(0x008, 2, 0);
+#pragma unroll
+            for (int i = 0; i < 2 * NB - 2; ++i) {
+                SGB(0x002, 4, 0);
+                SGB(0x008, 1, 0);
+            }
+            if (st + 1 < G / 2) SGB(0x100, 2 * NB, 0);
+            SGB(0x002, 8, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            pend = stp;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    epilogue(acc[1], 1, pend);
+    // the row's two lane halves: the smaller B1 wins (the lower half on a tie:
+    // a zero gap, uncertified either way); the second smallest of the union.
+    // The row goes to its winning step's bucket as (row, B1, B2, half); a row
+    // past a full bucket goes to the 3-term screen's list instead (and its
+    // record is marked for featnn_finish9 to skip)
+    const int nst = a.ntc >> 1;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+        const unsigned o1 = (unsigned)__shfl_xor((int)B1[t], 32, 64);
+        const unsigned o2 = (unsigned)__shfl_xor((int)B2[t], 32, 64);
+        const unsigned oi = (unsigned)__shfl_xor((int)I[t], 32, 64);
+        const unsigned s2 = umin2(umax2(B1[t], o1), umin2(B2[t], o2));
+        const bool mine = B1[t] < o1 || (B1[t] == o1 && h == 0);
+        const unsigned w1 = mine ? B1[t] : o1;
+        const unsigned wst = min(mine ? I[t] : oi, (unsigned)(nst - 1));
+        const int k = (qt0 + t) * 32 + (l & 31);
+        if (h == 0 && k < nr) {
+            const int row = rl ? rl[k] : k;
+            const size_t bk = (size_t)p * nst + wst;
+            const int rank = atomicAdd(a.bcnt + bk, 1);
+            if (rank < a.bcap) {
+                a.blist[bk * a.bcap + rank] = make_uint4((unsigned)row, w1, s2, mine ? 0u : 1u);
+            } else {
+                a.rec[(size_t)p * a.Rmax + row] = make_uint4(0u, 0u, 0u, 1u);
+                a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
+            }
+        }
+    }
+}
+
+// featnn_row9's second half (one launch per pass).  A pair's tiles: each
+// bucket's rows in 32-row tiles, in bucket order.  Grid (blocks per pair, P):
+// a block puts the pair's tiles-per-bucket prefix in LDS once, its waves take
+// tiles w, w + 4 gridDim.x, ... (a few each); one MFMA chain over a tile's
+// two column tiles (from the packed image) gives every row of the tile its
+// winning group's 32 values again (its operand rebuilt from the f32 row, as
+// the sweep built it), and the row's (column, B1, B2) record goes to
+// featnn_finish9.  (Run inside the sweep, on a workgroup's own 512 rows, the
+// regroup cost more: pass 1 2.0 ms against 1.29 + 0.2 -- ~126 chains of ~4
+// rows per workgroup and the registers it kept live.)
+constexpr int kRegroupMaxSteps = 4096;
+template <int S, bool kIdx>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void featnn_regroup9(RowArgs5 a) {
+    constexpr int NM = 2 * S + 1, NB = S + 1;
+    __shared__ int ts[kRegroupMaxSteps + 1], cn[kRegroupMaxSteps];
+    __shared__ int wsum[4];
+    // XCD-aware: a pair's blocks on one XCD (its rows and column image in that L2)
+    const int nbp = gridDim.x / (8 * ((a.P + 7) >> 3));  // blocks per pair
+    const int bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const int p = (slot / nbp) * 8 + xcd, bx = slot % nbp;
+    if (p >= a.P) return;
+    const int t = threadIdx.x, wid = t >> 6, l = t & 63, h = l >> 5;
+    const int nst = a.ntc >> 1;
+    const int *bc = a.bcnt + (size_t)p * nst;
+    // exclusive prefix of the tiles per bucket: each wave scans a quarter
+    const int seg = (nst + 3) >> 2, s0 = min(nst, wid * seg), s1 = min(nst, s0 + seg);
+    int run = 0;
+    for (int c0 = s0; c0 < s1; c0 += 64) {
+        const int i = c0 + l;
+        const int ci = i < s1 ? min(bc[i], a.bcap) : 0;
+        const int ti = (ci + 31) >> 5;
+        int x = ti;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (l >= o) x += y;
+        }
+        if (i < s1) {
+            ts[i] = run + x - ti;
+            cn[i] = ci;
+        }
+        run += __shfl(x, 63, 64);
+    }
+    if (l == 0) wsum[wid] = run;
+    __syncthreads();
+    int add = 0;
+    for (int ww = 0; ww < wid; ++ww) add += wsum[ww];
+    for (int i = s0 + l; i < s1; i += 64) ts[i] += add;
+    if (t == 0) ts[nst] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    const int ntiles = ts[nst];
+    const f16x8 *bimg = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
+    const uint4 *bl = a.blist + (size_t)p * nst * a.bcap;
+    const f32x16 zero = {};
+    // tile q's bucket, its rows' entries (the next tile's loaded while this one runs)
+    auto locate = [&](int q, int &b, bool &valid, uint4 &e) {
+        int lo = 0, hi = nst;  // ts[lo] <= q < ts[hi]
+        while (hi - lo > 1) {
+            const int md = (lo + hi) >> 1;
+            if (ts[md] <= q) lo = md;
+            else hi = md;
+        }
+        b = lo;
+        const int o = (q - ts[b]) * 32 + (l & 31);
+        valid = o < cn[b];
+        e = valid ? bl[(size_t)b * a.bcap + o] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    const int qs = nbp * 4;
+    int q = bx * 4 + wid, b = 0;
+    bool valid = false;
+    uint4 e = make_uint4(0u, 0u, 0u, 0u);
+    if (q < ntiles) locate(q, b, valid, e);
+    for (; q < ntiles; q += qs) {
+        int bn = 0;
+        bool vn = false;
+        uint4 en = make_uint4(0u, 0u, 0u, 0u);
+        if (q + qs < ntiles) locate(q + qs, bn, vn, en);
+        const int row = (int)e.x;
+        f16x8 Bf[2][NB];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int c = 0; c < NB; ++c) Bf[u][c] = bimg[((size_t)(2 * b + u) * NM + (c < S ? c : 2 * S)) * 64];
+        f16x8 A[NB];
+        row_operand1<S>(a, p, row, valid, h, A);
+        f32x16 acc[2];
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[c], c == 0 ? zero : acc[u], 0, 0, 0);
+        if (valid && (int)e.w == h) {
+            // the winner's column (the first in column order among equal
+            // patterns) and the group's second smallest value
+            unsigned t2 = 0xffffffffu;
+            int pos = -1;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const unsigned v = fbits(acc[u][r]);
+                    const bool hit = pos < 0 && v == e.y;
+                    t2 = hit ? t2 : umin2(t2, v);
+                    pos = hit ? 32 * (2 * b + u) + 8 * (r >> 2) + 4 * h + (r & 3) : pos;
+                }
+            // a winner not found again (it cannot be: the same chain) is left uncertified
+            const unsigned B2 = pos < 0 ? e.y : umin2(e.z, t2);
+            a.rec[(size_t)p * a.Rmax + row] = make_uint4((unsigned)(pos < 0 ? 64 * b : pos), e.y, B2, 0u);
+        }
+        b = bn; valid = vn; e = en;
+    }
+}
+
+// the rows' certification and outputs (row_tail) in row order, from the
+// regroup's (column, B1, B2) records: coalesced, where the regroup visits rows
+// in bucket order.  A record marked 1 is a row the sweep gave to the 3-term
+// screen (a full bucket).  1024 rows per block, the listed ones appended with
+// one global atomic per block: one counter per pair, the P counters in a few
+// cache lines -- per-row atomics from this short kernel serialised there
+// (~4 cycles each, 0.15 ms for C4's 73k rows).
+template <int S, bool kIdx>
+__global__ __launch_bounds__(256) void featnn_finish9(RowArgs5 a) {
+    constexpr int R = 4;
+    __shared__ int wcnt[4], base;
+    const int p = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int *rl = a.rlist ? a.rlist + (size_t)p * a.Rmax : nullptr;
+    const int nr = rl ? a.rcount[p] : count_of(a.n_rows, p, a.Rmax);
+    const int k0 = blockIdx.x * 256 * R;
+    if (k0 >= nr) return;  // whole block
+    const int m = count_of(a.n_cols, p, a.Cmax);
+    int rows[R];
+    bool put[R];
+    uint4 rc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int k = k0 + i * 256 + t;
+        rows[i] = k < nr ? (rl ? rl[k] : k) : -1;
+        rc[i] = rows[i] >= 0 ? a.rec[(size_t)p * a.Rmax + rows[i]] : make_uint4(0u, 0u, 0u, 1u);
+    }
+    int mine = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        put[i] = false;
+        if (rc[i].w == 0u)
+            put[i] = row_tail<kIdx, true, S + 1>(a, p, rows[i], m, rc[i].y, rc[i].z, (int)rc[i].x,
+                                                 a.rre[(size_t)p * a.ntr * 32 + rows[i]], 0.0);
+        mine += put[i] ? 1 : 0;
+    }
+    // block-wide exclusive offsets of the listed rows
+    int x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (l >= o) x += y;
+    }
+    if (l == 63) wcnt[w] = x;
+    __syncthreads();
+    if (t == 0) {
+        const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        base = tot ? atomicAdd(a.count + p, tot) : 0;
+    }
+    __syncthreads();
+    int off = base + x - mine;
+    for (int ww = 0; ww < w; ++ww) off += wcnt[ww];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+        if (put[i]) a.list[(size_t)p * a.Rmax + off++] = rows[i];
 }
 
 struct MutArgs {
@@ -1886,6 +2305,7 @@ struct V5Buf {
     int *cnt12, *cnt21, *list12, *list21;
     unsigned *gemax, *femax;  // per pair max |x - f16(x)| of the column (G) / row (F) images
     int *fbc12, *fbc21, *fbl12, *fbl21;  // the rows a 1-term screen left for the 3-term one
+    float *fre, *gre;                    // per row |x - f16(x)| of F / G (scaled, rounded up)
 };
 
 static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
@@ -1907,17 +2327,19 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     const size_t ap = (size_t)P * ntn * NM * 64, bp = (size_t)P * ntm * NM * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
-        16 * (ap + bp) + 4 * (nn_n + nn_m + 9 * (size_t)P + 2 * (size_t)P * (Nmax + Mmax) + 18 * (size_t)P);
+        16 * (ap + bp) + 4 * (2 * (nn_n + nn_m) + 9 * (size_t)P + 2 * (size_t)P * (Nmax + Mmax) + 18 * (size_t)P);
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     v.Ap = (f16x8 *)ws;
     v.Bp = v.Ap + ap;
     v.fnr = (float *)(v.Bp + bp);
     v.gnr = v.fnr + nn_n;
+    v.fre = v.gnr + nn_m;
+    v.gre = v.fre + nn_n;
     // [0,P): max|y|  [P,2P): max|x|  [2P,3P): the scale used  [3P,4P): cnt12  [4P,5P): cnt21
     // [5P,6P): gemax  [6P,7P): femax  [7P,8P): fbc12  [8P,9P): fbc21 (feat_sample clears
     // all but the scale)
-    v.gmax = (unsigned *)(v.gnr + nn_m);
+    v.gmax = (unsigned *)(v.gre + nn_m);
     v.fmax = v.gmax + P;
     v.mx = v.gmax + 2 * P;
     v.cnt12 = (int *)(v.gmax + 3 * P);
@@ -1948,7 +2370,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
         }
         const int gy = rep ? R : P;
         PackIO io{{F, G}, {n_src, n_tgt}, {Nmax, Mmax}, {ntn, ntm}, {v.Ap, v.Bp}, {v.fnr, v.gnr}, {v.fmax, v.gmax},
-                  {v.femax, v.gemax}};
+                  {v.femax, v.gemax}, {v.fre, v.gre}};
         const dim3 grid(cdiv(std::max(ntn, ntm), 4), gy, 2);
         if (D == 32) hipLaunchKernelGGL(feat_pack5r<32>, grid, dim3(256), 0, s, io, v.sp, pc);  // register-resident
         else hipLaunchKernelGGL(feat_pack5, grid, dim3(256), 0, s, io, D, v.S, v.sp, pc);
@@ -2096,6 +2518,42 @@ static int launch_row8(const RowArgs5 &r0, int S, hipStream_t s) {
     return PCR_OK;
 }
 
+// PCR_FEAT_ROW9=0: the round-6 featnn_row8 1-term passes (A/B; read per call)
+static bool feat_row9() {
+    const char *e = getenv("PCR_FEAT_ROW9");
+    return !(e && e[0] == '0');
+}
+
+template <bool kIdx>
+static int launch_row9(const RowArgs5 &r0, int S, hipStream_t s) {
+    RowArgs5 r = r0;
+    r.nrb = cdiv(cdiv(r.Rmax, 32), 8 * 2);  // 8 waves x 2 row tiles per workgroup
+    const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
+    PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
+    if (S == 1) hipLaunchKernelGGL((featnn_row9<1, kRow8G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    else hipLaunchKernelGGL((featnn_row9<2, kRow8G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+template <bool kIdx>
+static int launch_regroup9(const RowArgs5 &r, int S, hipStream_t s) {
+    // a pair has at most one tile per 32 rows plus one per bucket: ~3 per
+    // wave; 1-D, a pair's blocks on one XCD
+    const int nbp = cdiv(cdiv(r.Rmax, 32) + r.ntc / 2, 12);
+    const dim3 grid((unsigned)(8LL * nbp * cdiv(r.P, 8)));
+    const dim3 fgrid(cdiv(r.Rmax, 1024), r.P);
+    if (S == 1) {
+        hipLaunchKernelGGL((featnn_regroup9<1, kIdx>), grid, dim3(256), 0, s, r);
+        hipLaunchKernelGGL((featnn_finish9<1, kIdx>), fgrid, dim3(256), 0, s, r);
+    } else {
+        hipLaunchKernelGGL((featnn_regroup9<2, kIdx>), grid, dim3(256), 0, s, r);
+        hipLaunchKernelGGL((featnn_finish9<2, kIdx>), fgrid, dim3(256), 0, s, r);
+    }
+    PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
 // the 1-term screens in front of the 3-term ones (S <= 2): on by default,
 // PCR_FEAT_ONE=0 for the round-5 path (A/B, the parity tests; read per call)
 static bool feat_one_term() {
@@ -2139,7 +2597,16 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     // scratch: v12 [P][Nmax] f64 | e12 [P][Nmax] f32 | wq [P][Mmax] float4 | used, pos
     // [P][Mmax+1] | jlist, nn21x [P][Mmax] | flag [P][Nmax+1] | nj, zero [P] | nns [P][Nmax]
     const size_t pn = (size_t)P * Nmax, pm = (size_t)P * Mmax;
-    const size_t bytes = 8 * pn + 4 * pn + 16 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P + 4 * pn + 16;
+    // featnn_row9's buckets (a pass's rows by winning step): 4x a bucket's mean
+    // row count, at least 64 rows; a fuller bucket sends rows to the 3-term screen
+    const int nst1 = ntm / 2, nst2 = ntn / 2;
+    const int cap1 = std::max(64, 4 * cdiv(Nmax, nst1)), cap2 = std::max(64, 4 * cdiv(Mmax, nst2));
+    const size_t pb = (size_t)P * std::max(nst1, nst2);
+    const size_t pl = (size_t)P * std::max((size_t)nst1 * cap1, (size_t)nst2 * cap2);
+    const size_t pr = (size_t)P * std::max(Nmax, Mmax);
+    const size_t bytes = 8 * pn + 4 * pn + 16 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P + 4 * pn + 16 +
+                         16 * (pl + pr) + 4 * pb + 16;
+
     bool fresh = false;
     char *ws = (char *)workspace(33, bytes + 256, &fresh);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_corres: %s", pcr_last_error());
@@ -2155,7 +2622,12 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     ma.nj = ma.flag + pn + P;
     int *zero = ma.nj + P;
     int32_t *nns = zero + P;
+    uint4 *blist = reinterpret_cast<uint4 *>(((uintptr_t)(nns + pn) + 15) & ~(uintptr_t)15);
+    uint4 *rec = blist + pl;
+    int *bcnt = reinterpret_cast<int *>(rec + pr);
     const bool one = v.S <= 2 && feat_one_term();
+    // (the regroup keeps a pair's per-step prefix in LDS)
+    const bool use9 = one && feat_row9() && std::max(ntm, ntn) / 2 <= kRegroupMaxSteps;
     // a constant zero count per pair (read only): cleared when the slot is new
     // or was last used for fewer pairs
     static thread_local const void *z_ptr = nullptr;
@@ -2183,6 +2655,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.wq = nullptr;
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
     r.cemax = v.gemax; r.nns = nns; r.fbdiag = 0; r.rbmajor = 0;
+    r.rre = v.fre; r.bcnt = bcnt; r.blist = blist; r.bcap = cap1; r.rec = rec;
     if (prep_event && prep_at == 2) {
         PCR_HIP_CHECK(hipEventRecord(prep_event, s));
         if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
@@ -2191,8 +2664,17 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     prof_begin(s, kProfFeatScreen);
     if (one) {  // two column tiles per step (featnn_row8), 1-term; the rows it leaves to the 3-term
         r.list = v.fbl12; r.count = v.fbc12;
-        if ((rc = launch_row8<true, true>(r, v.S, s)) != PCR_OK) return rc;
-        prof_end(s, kProfFeatScreen);
+        if (use9) {  // featnn_row9's sweep, then the winners' groups again (regroup + finish)
+            PCR_HIP_CHECK(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)P * nst1, s));
+            if ((rc = launch_row9<true>(r, v.S, s)) != PCR_OK) return rc;
+            prof_end(s, kProfFeatScreen);
+            prof_begin(s, kProfFeatRegroup);
+            if ((rc = launch_regroup9<true>(r, v.S, s)) != PCR_OK) return rc;
+            prof_end(s, kProfFeatRegroup);
+        } else {
+            if ((rc = launch_row8<true, true>(r, v.S, s)) != PCR_OK) return rc;
+            prof_end(s, kProfFeatScreen);
+        }
         RowArgs5 r1 = r;
         r1.rlist = v.fbl12; r1.rcount = v.fbc12; r1.list = v.list12; r1.count = v.cnt12; r1.fbdiag = 1;
         r1.rbmajor = 1;
@@ -2265,8 +2747,18 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         prof_begin(s, kProfFeatScreen2);
         if (one) {  // values only, 1-term; the columns whose gap it cannot use go to the 3-term
             r2.list = v.fbl21; r2.count = v.fbc21;
-            if ((rc = launch_row8<false, true>(r2, v.S, s)) != PCR_OK) return rc;
-            prof_end(s, kProfFeatScreen2);
+            if (use9) {
+                r2.rre = v.gre; r2.bcap = cap2;
+                PCR_HIP_CHECK(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)P * nst2, s));
+                if ((rc = launch_row9<false>(r2, v.S, s)) != PCR_OK) return rc;
+                prof_end(s, kProfFeatScreen2);
+                prof_begin(s, kProfFeatRegroup);
+                if ((rc = launch_regroup9<false>(r2, v.S, s)) != PCR_OK) return rc;
+                prof_end(s, kProfFeatRegroup);
+            } else {
+                if ((rc = launch_row8<false, true>(r2, v.S, s)) != PCR_OK) return rc;
+                prof_end(s, kProfFeatScreen2);
+            }
             RowArgs5 r2b = r2;
             r2b.rlist = v.fbl21; r2b.rcount = v.fbc21; r2b.list = nullptr; r2b.count = nullptr; r2b.fbdiag = 2;
             r2b.rbmajor = 1;

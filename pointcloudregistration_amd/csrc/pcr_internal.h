@@ -53,7 +53,8 @@ int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which =
 // per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)
 enum ProfId { kProfFeatScreen = 0, kProfNndFwd = 1, kProfRansacValidate = 2, kProfIcp = 3,
               kProfRansacHyp = 4, kProfFeatRescan = 5, kProfFeatPack = 6, kProfNndGrid = 7,
-              kProfFeatScreen2 = 8, kProfFeatScreen1b = 9, kProfFeatScreen2b = 10, kProfSlots = 11 };
+              kProfFeatScreen2 = 8, kProfFeatScreen1b = 9, kProfFeatScreen2b = 10, kProfFeatRegroup = 11,
+              kProfSlots = 12 };
 void prof_begin(hipStream_t s, int id);
 void prof_end(hipStream_t s, int id);
 

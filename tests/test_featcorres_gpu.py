@@ -267,3 +267,38 @@ def test_mutual_mmax_16383(oracle):
     assert np.array_equal(_np(nn12)[0], e12)
     assert int(_np(nc)[0]) == len(exp)
     assert np.array_equal(_np(co)[0, :len(exp)], exp)
+
+
+def test_row9_path_runs_and_row8_path_equal(oracle, monkeypatch):
+    """The shipped 1-term passes are featnn_row9 + featnn_regroup9 (the regroup's
+    profile slot counts its two launches, one per pass); PCR_FEAT_ROW9=0 selects
+    the round-6 featnn_row8 1-term passes, which give the same nn12 and set."""
+    from pointcloudregistration_amd import _lib
+    fs, ft = CASES["synthetic_4096"]
+    _lib.profile_enable(True)
+    _lib.profile_read(_lib.PROF_FEAT_REGROUP, reset=True)
+    co, nc, nn12 = reg.feature_correspondences(fs[None], ft[None])
+    _, launches = _lib.profile_read(_lib.PROF_FEAT_REGROUP, reset=True)
+    _lib.profile_enable(False)
+    assert launches == 2, launches
+    monkeypatch.setenv("PCR_FEAT_ROW9", "0")
+    co8, nc8, nn8 = reg.feature_correspondences(fs[None], ft[None])
+    e12 = oracle.featnn(fs, ft)
+    exp = oracle.corres(e12, oracle.featnn(ft, fs), True, 3)
+    for c, n, nn in ((co, nc, nn12), (co8, nc8, nn8)):
+        assert np.array_equal(_np(nn)[0], e12)
+        assert int(_np(n)[0]) == len(exp)
+        assert np.array_equal(_np(c)[0, :len(exp)], exp)
+
+
+@pytest.mark.parametrize("name", ["dup_rows", "dynamic_range", "near_twins", "nan_rows", "d1"])
+def test_feature_correspondences_row8_one_term(oracle, monkeypatch, name):
+    """The featnn_row8 1-term passes (PCR_FEAT_ROW9=0) stay bit-exact."""
+    monkeypatch.setenv("PCR_FEAT_ROW9", "0")
+    fs, ft = CASES[name]
+    co, nc, nn12 = reg.feature_correspondences(fs[None], ft[None])
+    e12 = oracle.featnn(fs, ft)
+    exp = oracle.corres(e12, oracle.featnn(ft, fs), True, 3)
+    assert np.array_equal(_np(nn12)[0], e12)
+    assert int(_np(nc)[0]) == len(exp)
+    assert np.array_equal(_np(co)[0, :len(exp)], exp)

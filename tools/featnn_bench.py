@@ -52,7 +52,8 @@ def main():
     prof = {name: _lib.profile_read(pid)[0] / a.iters for name, pid in
             (("screen", _lib.PROF_FEAT_SCREEN), ("rescan", _lib.PROF_FEAT_RESCAN),
              ("pack", _lib.PROF_FEAT_PACK), ("screen2", _lib.PROF_FEAT_SCREEN2),
-             ("screen1b", _lib.PROF_FEAT_SCREEN1B), ("screen2b", _lib.PROF_FEAT_SCREEN2B))}
+             ("screen1b", _lib.PROF_FEAT_SCREEN1B), ("screen2b", _lib.PROF_FEAT_SCREEN2B),
+             ("regroup", _lib.PROF_FEAT_REGROUP))}
     rows = _lib.featnn_rescan_rows(reset=True)
     fb = _lib.featnn_fallback_rows(reset=True)
     flops = 2.0 * a.pairs * a.n * a.n * a.d

@@ -11,11 +11,12 @@ export TMPDIR=/tmp
 # the profiler)
 export PCR_ICP_TAIL=0
 OUT=${1:-gpurun_out/pmc_sq}
+PAIRS=${PAIRS:-256}   # the bench's pair count (bench.py reads profiles/rNN/vMM_sq_pmc[_<P>pairs].json)
 mkdir -p "$OUT"
 run() {
   local name=$1; shift
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --no-host-resident > "$OUT/$name.log" 2>&1
+    -- python3 bench.py --pairs $PAIRS --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --no-host-resident > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   return $rc
@@ -25,11 +26,12 @@ timeout -s KILL 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || true
 if grep -q SQ_INSTS_VALU_FMA_F64 "$OUT/avail.txt"; then
   run b SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 || exit 1
 fi
-python3 - "$OUT" > "$OUT/summary.json" <<'PY'
+python3 - "$OUT" "$PAIRS" > "$OUT/summary.json" <<'PY'
 import json, subprocess, sys
 raw = json.loads(subprocess.check_output([sys.executable, "tools/sq_summary.py", sys.argv[1]]))
 print(json.dumps({"note": "tools/pmc_sq.sh: per-launch averages of SQ counters over "
-                  "bench.py --steps 2 (wave-level instruction counts, whole chip)",
+                  f"bench.py --pairs {sys.argv[2]} --steps 2 (wave-level instruction counts, whole chip)",
+                  "pairs": int(sys.argv[2]),
                   "kernels": {k: {"counters": v} for k, v in raw.items()}}, indent=1))
 PY
 cat "$OUT/summary.json" | head -40
