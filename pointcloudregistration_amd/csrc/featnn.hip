@@ -1078,6 +1078,11 @@ struct RowArgs5 {
     int *bcnt, bcap;
     uint4 *blist;
     uint4 *rec;                 // featnn_regroup9 -> featnn_finish9, by row: (column, B1, B2, skip)
+    // featnn_row8 list mode over column slices (csl > 1: short lists at small
+    // batches): slice sl's partial (B1, B2, column) per listed row position k,
+    // [P][csl][Rmax], merged by featnn_slicemerge
+    int csl;
+    uint4 *part;
 };
 
 // rows (pass 1) and J columns (pass 2) the 1-term screens left to the 3-term
@@ -1522,21 +1527,26 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     // row-block-major: pair-major placed the working blocks 16 apart in an
     // XCD's dispatch order, and they piled onto a few of its CUs (3x slower)
     const int ppx = (a.P + 7) >> 3;
+    // row-block-major blocks also split the columns into a.csl slices (list
+    // mode at small batches: a pair's short list is one block per slice)
+    const int rbs = a.rbmajor ? slot / ppx : 0, csl = a.rbmajor ? a.csl : 1, sl = rbs % csl;
     const int p = a.rbmajor ? (slot % ppx) * 8 + xcd : (slot / a.nrb) * 8 + xcd;
-    const int rb = a.rbmajor ? slot / ppx : slot - (slot / a.nrb) * a.nrb;
+    const int rb = a.rbmajor ? rbs / csl : slot - (slot / a.nrb) * a.nrb;
     if (p >= a.P) return;  // whole block
     // the rows: in order (pass 1) or the listed ones rlist[p][0 .. rcount[p])
     // (pass 2: J; the 3-term passes behind a 1-term one: the rows it left)
     const int *rl = a.rlist ? a.rlist + (size_t)p * a.Rmax : nullptr;
     const int nr = rl ? a.rcount[p] : count_of(a.n_rows, p, a.Rmax);
-    if (a.fbdiag && rb == 0 && threadIdx.x == 0 && nr > 0)
+    if (a.fbdiag && rb == 0 && sl == 0 && threadIdx.x == 0 && nr > 0)
         atomicAdd(&g_featnn_fallback_rows[a.fbdiag - 1], (unsigned long long)nr);
     if (rb * W * RT * 32 >= nr) return;  // whole block: no rows here
     const int wid = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
     const int m = count_of(a.n_cols, p, a.Cmax);
     const int qt0 = (rb * W + wid) * RT;  // this wave's first row tile
     const int ntc = (m + 31) >> 5;
-    const int ngroups = (ntc + G - 1) / G;
+    const int ngall = (ntc + G - 1) / G;
+    // this slice's column groups [g0, ngroups)
+    const int g0 = (int)((long long)ngall * sl / csl), ngroups = (int)((long long)ngall * (sl + 1) / csl);
     const unsigned ctmask = (1u << a.ctbits) - 1u;
     unsigned keep = ~ctmask;
     asm("" : "+v"(keep));  // a VGPR operand: one v_and_or_b32 per code with the SGPR tile number
@@ -1638,11 +1648,11 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
     // VALU per phase (two tiles' epilogues): 80; spread over the phase's MFMAs
     constexpr int kVA = PCR_VA;
     constexpr int kVB = PCR_VB;
-    issue(0, 0);
+    if (g0 < ngroups) issue(g0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int grp = 0; grp < ngroups; ++grp) {
-        const int buf = grp & 1;
+    for (int grp = g0; grp < ngroups; ++grp) {
+        const int buf = (grp - g0) & 1;
         if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
         const f16x8 *Bb = Bs + buf * kB + l;
         // the step's B fragments, read in MFMA order (the first MFMAs wait for
@@ -1740,9 +1750,36 @@ __global__ __launch_bounds__(512) void featnn_row8(RowArgs5 a) {
         const int k = qt * 32 + R;
         if (h != 0 || k >= nr) continue;
         const int row = rl ? rl[k] : k;  // the original row index
+        if (csl > 1) {  // this slice's partial, merged by featnn_slicemerge
+            a.part[((size_t)p * csl + sl) * a.Rmax + k] = make_uint4(B1, B2, (unsigned)mi1, 0u);
+            continue;
+        }
         if (row_tail<kIdx, kOne, NX>(a, p, row, m, B1, B2, mi1, rex[t], __builtin_ldexp(1.0, a.ctbits - 23)))
             a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
     }
+}
+
+// featnn_row8's column slices (list mode, csl > 1) merged: per listed row the
+// smallest B1 over the slices (the values carry the column tile code: no two
+// are equal across slices), B2 the second smallest of the union, then the
+// row's certification and outputs as the unsliced kernel's tail
+template <int S, bool kIdx>
+__global__ __launch_bounds__(256) void featnn_slicemerge(RowArgs5 a) {
+    constexpr int NX = 3 * S + 1;
+    const int p = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+    const int *rl = a.rlist + (size_t)p * a.Rmax;
+    if (k >= a.rcount[p]) return;
+    unsigned B1 = 0x7f800000u, B2 = 0x7f800000u, mi = 0u;
+    for (int s2 = 0; s2 < a.csl; ++s2) {
+        const uint4 q = a.part[((size_t)p * a.csl + s2) * a.Rmax + k];
+        B2 = umin2(umin2(B2, q.y), umax2(B1, q.x));
+        mi = q.x < B1 ? q.z : mi;
+        B1 = umin2(B1, q.x);
+    }
+    const int row = rl[k];
+    if (row_tail<kIdx, false, NX>(a, p, row, count_of(a.n_cols, p, a.Cmax), B1, B2, (int)mi, 0.0f,
+                                  __builtin_ldexp(1.0, a.ctbits - 23)))
+        a.list[(size_t)p * a.Rmax + atomicAdd(a.count + p, 1)] = row;
 }
 
 // ---------------------------------------------------------------------------
@@ -2510,13 +2547,25 @@ template <bool kIdx, bool kOne>
 static int launch_row8(const RowArgs5 &r0, int S, hipStream_t s) {
     RowArgs5 r = r0;
     r.nrb = cdiv(cdiv(r.Rmax, 32), 8 * 2);  // 8 waves x 2 row tiles per workgroup
-    const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
+    const int csl = r.rbmajor ? r.csl : 1;
+    const long long nblk = 8LL * r.nrb * csl * cdiv(r.P, 8);  // XCD-aware 1-D grid
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
     if (S == 1) hipLaunchKernelGGL((featnn_row8<1, kRow8G, kIdx, kOne>), dim3((unsigned)nblk), dim3(512), 0, s, r);
     else hipLaunchKernelGGL((featnn_row8<2, kRow8G, kIdx, kOne>), dim3((unsigned)nblk), dim3(512), 0, s, r);
     PCR_LAUNCH_CHECK();
+    if (csl > 1) {
+        const dim3 mg(cdiv(r.Rmax, 256), r.P);
+        if (S == 1) hipLaunchKernelGGL((featnn_slicemerge<1, kIdx>), mg, dim3(256), 0, s, r);
+        else hipLaunchKernelGGL((featnn_slicemerge<2, kIdx>), mg, dim3(256), 0, s, r);
+        PCR_LAUNCH_CHECK();
+    }
     return PCR_OK;
 }
+
+// column slices of the 3-term screens' list mode: a pair's short list is
+// one workgroup per slice -- at 256 pairs one slice (the chip is full), at
+// 32 pairs 8 (one block per pair left 224 CUs idle: ~0.2 ms per launch)
+static int list_slices(int P) { return std::max(1, std::min(8, 256 / std::max(P, 1))); }
 
 // PCR_FEAT_ROW9=0: the round-6 featnn_row8 1-term passes (A/B; read per call)
 static bool feat_row9() {
@@ -2604,8 +2653,10 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     const size_t pb = (size_t)P * std::max(nst1, nst2);
     const size_t pl = (size_t)P * std::max((size_t)nst1 * cap1, (size_t)nst2 * cap2);
     const size_t pr = (size_t)P * std::max(Nmax, Mmax);
+    const int fsl = list_slices(P);
+    const size_t pt = fsl > 1 ? (size_t)fsl * pr : 0;  // the sliced 3-term screens' partials
     const size_t bytes = 8 * pn + 4 * pn + 16 * pm + 8 * (pm + P) + 8 * pm + 4 * (pn + P) + 8 * (size_t)P + 4 * pn + 16 +
-                         16 * (pl + pr) + 4 * pb + 16;
+                         16 * (pl + pr + pt) + 4 * pb + 16;
 
     bool fresh = false;
     char *ws = (char *)workspace(33, bytes + 256, &fresh);
@@ -2624,7 +2675,8 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     int32_t *nns = zero + P;
     uint4 *blist = reinterpret_cast<uint4 *>(((uintptr_t)(nns + pn) + 15) & ~(uintptr_t)15);
     uint4 *rec = blist + pl;
-    int *bcnt = reinterpret_cast<int *>(rec + pr);
+    uint4 *part = rec + pr;
+    int *bcnt = reinterpret_cast<int *>(part + pt);
     const bool one = v.S <= 2 && feat_one_term();
     // (the regroup keeps a pair's per-step prefix in LDS)
     const bool use9 = one && feat_row9() && std::max(ntm, ntn) / 2 <= kRegroupMaxSteps;
@@ -2656,6 +2708,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
     r.cemax = v.gemax; r.nns = nns; r.fbdiag = 0; r.rbmajor = 0;
     r.rre = v.fre; r.bcnt = bcnt; r.blist = blist; r.bcap = cap1; r.rec = rec;
+    r.csl = 1; r.part = part;
     if (prep_event && prep_at == 2) {
         PCR_HIP_CHECK(hipEventRecord(prep_event, s));
         if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
@@ -2677,7 +2730,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         }
         RowArgs5 r1 = r;
         r1.rlist = v.fbl12; r1.rcount = v.fbc12; r1.list = v.list12; r1.count = v.cnt12; r1.fbdiag = 1;
-        r1.rbmajor = 1;
+        r1.rbmajor = 1; r1.csl = fsl;
         prof_begin(s, kProfFeatScreen1b);
         if ((rc = launch_row8<true, false>(r1, v.S, s)) != PCR_OK) return rc;
         prof_end(s, kProfFeatScreen1b);
@@ -2761,7 +2814,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
             }
             RowArgs5 r2b = r2;
             r2b.rlist = v.fbl21; r2b.rcount = v.fbc21; r2b.list = nullptr; r2b.count = nullptr; r2b.fbdiag = 2;
-            r2b.rbmajor = 1;
+            r2b.rbmajor = 1; r2b.csl = fsl;
             prof_begin(s, kProfFeatScreen2b);
             if ((rc = launch_row8<false, false>(r2b, v.S, s)) != PCR_OK) return rc;
             prof_end(s, kProfFeatScreen2b);
