@@ -88,9 +88,13 @@ constexpr int kCUs = 256;
         }                                                                              \
     } while (0)
 
+// PCR_SYNC_CHECK=1 (debug): also synchronise after every checked launch, so a
+// kernel fault is reported at its own launch site
+namespace pcr { bool sync_check(); }
 #define PCR_LAUNCH_CHECK()                                                             \
     do {                                                                               \
         hipError_t e_ = hipGetLastError();                                             \
+        if (e_ == hipSuccess && pcr::sync_check()) e_ = hipDeviceSynchronize();        \
         if (e_ != hipSuccess) {                                                        \
             pcr::set_error("kernel launch failed at %s:%d: %s", __FILE__, __LINE__,    \
                            hipGetErrorString(e_));                                     \

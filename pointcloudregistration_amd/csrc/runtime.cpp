@@ -21,6 +21,14 @@ void set_error(const char *fmt, ...) {
 
 void clear_error() { g_err[0] = '\0'; }
 
+bool sync_check() {
+    static const bool on = [] {
+        const char *e = getenv("PCR_SYNC_CHECK");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 namespace {
 struct Slot {
     void *ptr = nullptr;
