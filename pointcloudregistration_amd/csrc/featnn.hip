@@ -1078,6 +1078,7 @@ struct RowArgs5 {
     int *bcnt, bcap;
     uint4 *blist;
     uint4 *rec;                 // featnn_regroup9 -> featnn_finish9, by row: (column, B1, B2, skip)
+    int *llist, *lcount;        // featnn_finish9: where its failing rows go (nullable)
     // featnn_row8 list mode over column slices (csl > 1: short lists at small
     // batches): slice sl's partial (B1, B2, column) per listed row position k,
     // [P][csl][Rmax], merged by featnn_slicemerge
@@ -1507,6 +1508,30 @@ __device__ __forceinline__ bool row_tail(const RowArgs5 &a, int p, int row, int 
     a.nn[o] = mi1;
     if (a.nns) a.nns[o] = mi1;
     return !((double)mb2 - (double)mb1 > thr + pk * (__builtin_fabs((double)mb1) + __builtin_fabs((double)mb2)));
+}
+
+// featnn_row9's early test: a row whose gap between its smallest value and
+// the second smallest GROUP minimum -- an upper bound on its true second
+// value -- already fails the 1-term certificate (row_tail's, pk = 0) fails it
+// whatever the winning group's own second: it goes to the 3-term screen right
+// after the sweep (beside the regroup) instead of through the regroup.
+template <bool kIdx, int NX>
+__device__ __forceinline__ bool one_term_fails(const RowArgs5 &a, int p, int row, unsigned B1, unsigned B2g,
+                                               float rexv) {
+    const double sub = sub_term(a.D);
+    const double mb1 = (double)__uint_as_float(B1), mb2 = (double)__uint_as_float(B2g);
+    const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
+    const double Gm = (double)__uint_as_float(a.cmax[p]);
+    const double ex = (double)rexv + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
+    const double bnd = bound1(qn, ex, Gm, E, 16 * NX) + 4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kRowBias1;
+    if constexpr (!kIdx) return !(mb2 - mb1 > bnd * (1.0 + 1e-6) + 1e-6 * mb1);
+    const double dot = 2.0 * (ex * Gm + (qn + ex) * E);
+    const double rest = 0.5 * bnd - dot;
+    const double er = 0.5 * bnd;
+    const double b1v = __builtin_fmax(mb1 - kRowBias1, 0.0);
+    const double win = 2.0 * rest + 2.0 * ex * (__builtin_sqrt(b1v + 3.0 * er) + __builtin_sqrt(b1v + er)) +
+                       4.0 * (qn + ex) * E;
+    return !(mb2 - mb1 > __builtin_fmin(bnd, win * (1.0 + 1e-9)));
 }
 
 template <int S, int G, bool kIdx, bool kOne>
@@ -1982,8 +2007,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     // the row's two lane halves: the smaller B1 wins (the lower half on a tie:
     // a zero gap, uncertified either way); the second smallest of the union.
     // The row goes to its winning step's bucket as (row, B1, B2, half); a row
-    // past a full bucket goes to the 3-term screen's list instead (and its
-    // record is marked for featnn_finish9 to skip)
+    // that one_term_fails, or past a full bucket, goes to the 3-term screen's
+    // list instead (and its record is marked for featnn_finish9 to skip)
     const int nst = a.ntc >> 1;
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -1998,7 +2023,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         if (h == 0 && k < nr) {
             const int row = rl ? rl[k] : k;
             const size_t bk = (size_t)p * nst + wst;
-            const int rank = atomicAdd(a.bcnt + bk, 1);
+            const bool early = one_term_fails<kIdx, S + 1>(a, p, row, w1, s2, a.rre[(size_t)p * a.ntr * 32 + row]);
+            const int rank = early ? a.bcap : atomicAdd(a.bcnt + bk, 1);
             if (rank < a.bcap) {
                 a.blist[bk * a.bcap + rank] = make_uint4((unsigned)row, w1, s2, mine ? 0u : 1u);
             } else {
@@ -2023,15 +2049,18 @@ constexpr int kRegroupMaxSteps = 4096;
 template <int S, bool kIdx>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void featnn_regroup9(RowArgs5 a) {
     constexpr int NM = 2 * S + 1, NB = S + 1;
-    __shared__ int ts[kRegroupMaxSteps + 1], cn[kRegroupMaxSteps];
+    // the pair's per-step tile prefix and row counts, 2 (steps + 1) ints of
+    // dynamic LDS (a static 4097-entry pair held 32 KB and four blocks per CU)
+    extern __shared__ int rg_lds[];
     __shared__ int wsum[4];
+    const int nst = a.ntc >> 1;
+    int *ts = rg_lds, *cn = rg_lds + nst + 1;
     // XCD-aware: a pair's blocks on one XCD (its rows and column image in that L2)
     const int nbp = gridDim.x / (8 * ((a.P + 7) >> 3));  // blocks per pair
     const int bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
     const int p = (slot / nbp) * 8 + xcd, bx = slot % nbp;
     if (p >= a.P) return;
     const int t = threadIdx.x, wid = t >> 6, l = t & 63, h = l >> 5;
-    const int nst = a.ntc >> 1;
     const int *bc = a.bcnt + (size_t)p * nst;
     // exclusive prefix of the tiles per bucket: each wave scans a quarter
     const int seg = (nst + 3) >> 2, s0 = min(nst, wid * seg), s1 = min(nst, s0 + seg);
@@ -2125,7 +2154,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 // the rows' certification and outputs (row_tail) in row order, from the
 // regroup's (column, B1, B2) records: coalesced, where the regroup visits rows
 // in bucket order.  A record marked 1 is a row the sweep gave to the 3-term
-// screen (a full bucket).  1024 rows per block, the listed ones appended with
+// screen.  A row that fails here -- its winning group's own second value
+// closed the gap, rare -- goes to a.llist: pass 1 the exact rescan's list (the
+// 3-term screen runs beside this kernel), pass 2 none (the resolve sends a
+// column whose top-2 gap is too small to the exact column rescan).  1024 rows per block, the listed ones appended with
 // one global atomic per block: one counter per pair, the P counters in a few
 // cache lines -- per-row atomics from this short kernel serialised there
 // (~4 cycles each, 0.15 ms for C4's 73k rows).
@@ -2168,14 +2200,15 @@ __global__ __launch_bounds__(256) void featnn_finish9(RowArgs5 a) {
     __syncthreads();
     if (t == 0) {
         const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        base = tot ? atomicAdd(a.count + p, tot) : 0;
+        base = tot && a.llist ? atomicAdd(a.lcount + p, tot) : 0;
     }
     __syncthreads();
+    if (!a.llist) return;
     int off = base + x - mine;
     for (int ww = 0; ww < w; ++ww) off += wcnt[ww];
 #pragma unroll
     for (int i = 0; i < R; ++i)
-        if (put[i]) a.list[(size_t)p * a.Rmax + off++] = rows[i];
+        if (put[i]) a.llist[(size_t)p * a.Rmax + off++] = rows[i];
 }
 
 struct MutArgs {
@@ -2592,14 +2625,53 @@ static int launch_regroup9(const RowArgs5 &r, int S, hipStream_t s) {
     const int nbp = cdiv(cdiv(r.Rmax, 32) + r.ntc / 2, 12);
     const dim3 grid((unsigned)(8LL * nbp * cdiv(r.P, 8)));
     const dim3 fgrid(cdiv(r.Rmax, 1024), r.P);
+    const size_t sm = sizeof(int) * (2 * (size_t)(r.ntc / 2) + 1);
     if (S == 1) {
-        hipLaunchKernelGGL((featnn_regroup9<1, kIdx>), grid, dim3(256), 0, s, r);
+        hipLaunchKernelGGL((featnn_regroup9<1, kIdx>), grid, dim3(256), sm, s, r);
         hipLaunchKernelGGL((featnn_finish9<1, kIdx>), fgrid, dim3(256), 0, s, r);
     } else {
-        hipLaunchKernelGGL((featnn_regroup9<2, kIdx>), grid, dim3(256), 0, s, r);
+        hipLaunchKernelGGL((featnn_regroup9<2, kIdx>), grid, dim3(256), sm, s, r);
         hipLaunchKernelGGL((featnn_finish9<2, kIdx>), fgrid, dim3(256), 0, s, r);
     }
     PCR_LAUNCH_CHECK();
+    return PCR_OK;
+}
+
+// a 3-term fallback screen (list mode), in its profile slot
+template <bool kIdx>
+static int launch_fallback(const RowArgs5 &r, int S, hipStream_t q, int slot) {
+    prof_begin(q, slot);
+    const int rc = launch_row8<kIdx, false>(r, S, q);
+    prof_end(q, slot);
+    return rc;
+}
+
+// side(q) then main() on s; with PCR_FEAT_BESIDE=1, side(q) on the second
+// side stream beside main() on s, joined back into s.  Measured (featnn_bench,
+// mutual): 256 pairs 3.42 ms either way, 32 pairs 0.778 beside vs 0.755 ms in
+// order -- the 3-term screen and the regroup compete for the same CUs, so the
+// default is in order
+template <class Side, class Main>
+static int beside(hipStream_t s, Side side, Main main) {
+    static const bool off = [] {
+        const char *e = getenv("PCR_FEAT_BESIDE");
+        return !(e && e[0] == '1');
+    }();
+    hipStream_t q = s;
+    hipEvent_t ef = nullptr, ej = nullptr;
+    int rc = off ? PCR_OK : side_stream(&q, &ef, &ej, 2);
+    if (rc != PCR_OK) return rc;
+    if (q != s) {
+        PCR_HIP_CHECK(hipEventRecord(ef, s));
+        PCR_HIP_CHECK(hipStreamWaitEvent(q, ef, 0));
+    }
+    if ((rc = side(q)) != PCR_OK) return rc;
+    if (q != s) PCR_HIP_CHECK(hipEventRecord(ej, q));
+    prof_begin(s, kProfFeatRegroup);
+    rc = main();
+    prof_end(s, kProfFeatRegroup);
+    if (rc != PCR_OK) return rc;
+    if (q != s) PCR_HIP_CHECK(hipStreamWaitEvent(s, ej, 0));
     return PCR_OK;
 }
 
@@ -2708,7 +2780,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
     r.cemax = v.gemax; r.nns = nns; r.fbdiag = 0; r.rbmajor = 0;
     r.rre = v.fre; r.bcnt = bcnt; r.blist = blist; r.bcap = cap1; r.rec = rec;
-    r.csl = 1; r.part = part;
+    r.csl = 1; r.part = part; r.llist = nullptr; r.lcount = nullptr;
     if (prep_event && prep_at == 2) {
         PCR_HIP_CHECK(hipEventRecord(prep_event, s));
         if (prep_fn && (rc = prep_fn(prep_ctx)) != PCR_OK) return rc;
@@ -2717,23 +2789,24 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     prof_begin(s, kProfFeatScreen);
     if (one) {  // two column tiles per step (featnn_row8), 1-term; the rows it leaves to the 3-term
         r.list = v.fbl12; r.count = v.fbc12;
+        RowArgs5 r1 = r;
+        r1.rlist = v.fbl12; r1.rcount = v.fbc12; r1.list = v.list12; r1.count = v.cnt12; r1.fbdiag = 1;
+        r1.rbmajor = 1; r1.csl = fsl;
         if (use9) {  // featnn_row9's sweep, then the winners' groups again (regroup + finish)
             PCR_HIP_CHECK(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)P * nst1, s));
             if ((rc = launch_row9<true>(r, v.S, s)) != PCR_OK) return rc;
             prof_end(s, kProfFeatScreen);
-            prof_begin(s, kProfFeatRegroup);
-            if ((rc = launch_regroup9<true>(r, v.S, s)) != PCR_OK) return rc;
-            prof_end(s, kProfFeatRegroup);
+            // the 3-term screen of the rows the sweep listed, beside the regroup
+            RowArgs5 rg = r;
+            rg.llist = v.list12; rg.lcount = v.cnt12;
+            if ((rc = beside(s, [&](hipStream_t q) { return launch_fallback<true>(r1, v.S, q, kProfFeatScreen1b); },
+                             [&] { return launch_regroup9<true>(rg, v.S, s); })) != PCR_OK)
+                return rc;
         } else {
             if ((rc = launch_row8<true, true>(r, v.S, s)) != PCR_OK) return rc;
             prof_end(s, kProfFeatScreen);
+            if ((rc = launch_fallback<true>(r1, v.S, s, kProfFeatScreen1b)) != PCR_OK) return rc;
         }
-        RowArgs5 r1 = r;
-        r1.rlist = v.fbl12; r1.rcount = v.fbc12; r1.list = v.list12; r1.count = v.cnt12; r1.fbdiag = 1;
-        r1.rbmajor = 1; r1.csl = fsl;
-        prof_begin(s, kProfFeatScreen1b);
-        if ((rc = launch_row8<true, false>(r1, v.S, s)) != PCR_OK) return rc;
-        prof_end(s, kProfFeatScreen1b);
     } else if (v.S <= 2) {  // the 3-term screen only
         if ((rc = launch_row8<true, false>(r, v.S, s)) != PCR_OK) return rc;
         prof_end(s, kProfFeatScreen);
@@ -2800,24 +2873,24 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
         prof_begin(s, kProfFeatScreen2);
         if (one) {  // values only, 1-term; the columns whose gap it cannot use go to the 3-term
             r2.list = v.fbl21; r2.count = v.fbc21;
+            RowArgs5 r2b = r2;
+            r2b.rlist = v.fbl21; r2b.rcount = v.fbc21; r2b.list = nullptr; r2b.count = nullptr; r2b.fbdiag = 2;
+            r2b.rbmajor = 1; r2b.csl = fsl;
             if (use9) {
                 r2.rre = v.gre; r2.bcap = cap2;
                 PCR_HIP_CHECK(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)P * nst2, s));
                 if ((rc = launch_row9<false>(r2, v.S, s)) != PCR_OK) return rc;
                 prof_end(s, kProfFeatScreen2);
-                prof_begin(s, kProfFeatRegroup);
-                if ((rc = launch_regroup9<false>(r2, v.S, s)) != PCR_OK) return rc;
-                prof_end(s, kProfFeatRegroup);
+                RowArgs5 rg2 = r2;
+                rg2.llist = nullptr; rg2.lcount = nullptr;
+                if ((rc = beside(s, [&](hipStream_t q) { return launch_fallback<false>(r2b, v.S, q, kProfFeatScreen2b); },
+                                 [&] { return launch_regroup9<false>(rg2, v.S, s); })) != PCR_OK)
+                    return rc;
             } else {
                 if ((rc = launch_row8<false, true>(r2, v.S, s)) != PCR_OK) return rc;
                 prof_end(s, kProfFeatScreen2);
+                if ((rc = launch_fallback<false>(r2b, v.S, s, kProfFeatScreen2b)) != PCR_OK) return rc;
             }
-            RowArgs5 r2b = r2;
-            r2b.rlist = v.fbl21; r2b.rcount = v.fbc21; r2b.list = nullptr; r2b.count = nullptr; r2b.fbdiag = 2;
-            r2b.rbmajor = 1; r2b.csl = fsl;
-            prof_begin(s, kProfFeatScreen2b);
-            if ((rc = launch_row8<false, false>(r2b, v.S, s)) != PCR_OK) return rc;
-            prof_end(s, kProfFeatScreen2b);
         } else if (v.S <= 2) {
             if ((rc = launch_row8<false, false>(r2, v.S, s)) != PCR_OK) return rc;
             prof_end(s, kProfFeatScreen2);

@@ -47,7 +47,8 @@ inline hipStream_t as_stream(pcr_stream_t s) { return reinterpret_cast<hipStream
 // destroyed by pcr_shutdown.  which = the event pair: 0 the pipeline's grid
 // prep, 1 the feature stage's exact row rescan (beside pass 2).  One stream for
 // both: a second stream per context moved other streams' hardware queues (the
-// process has 4) and cost the s8d job 18 %.
+// process has 4) and cost the s8d job 18 %.  Pair 2 is on a second stream,
+// created on its first use: the 3-term screens beside the 1-term regroups.
 int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which = 0);
 
 // per-kernel HIP-event timing on the launch stream (enabled by pcr_profile_enable)

@@ -95,8 +95,8 @@ thread_local void *prep_ctx = nullptr;
 // ---- side stream of a (device, workspace context) -------------------------
 namespace {
 struct Side {
-    hipStream_t s = nullptr;
-    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t s = nullptr, s2 = nullptr;  // pairs 0, 1 on s; pair 2 on s2
+    hipEvent_t e[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 Side g_side[kMaxDevices][kMaxCtx];
 }  // namespace
@@ -108,24 +108,27 @@ int side_stream(hipStream_t *s, hipEvent_t *e_in, hipEvent_t *e_out, int which) 
         set_error("side_stream: no current device");
         return PCR_ERR_HIP;
     }
-    if (which < 0 || which > 1) {
+    if (which < 0 || which > 2) {
         set_error("side_stream: no event pair %d", which);
         return PCR_ERR_ARG;
     }
     std::lock_guard<std::mutex> lk(g_mu);
     Side &d = g_side[dev][t_ctx];
     if (!d.s) {
-        if (hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&d.e[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.e[1], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.e[2], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.e[3], hipEventDisableTiming) != hipSuccess) {
+        bool ok = hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < 6 && ok; ++i) ok = hipEventCreateWithFlags(&d.e[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
             (void)hipGetLastError();
             set_error("side_stream: stream / event creation failed");
             return PCR_ERR_HIP;
         }
     }
-    *s = d.s;
+    if (which == 2 && !d.s2 && hipStreamCreateWithFlags(&d.s2, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("side_stream: stream creation failed");
+        return PCR_ERR_HIP;
+    }
+    *s = which == 2 ? d.s2 : d.s;
     *e_in = d.e[2 * which];
     *e_out = d.e[2 * which + 1];
     return PCR_OK;
@@ -343,7 +346,12 @@ extern "C" int pcr_shutdown(void) {
                 if (hipSetDevice(dev) == hipSuccess) {
                     (void)hipStreamSynchronize(sd.s);
                     (void)hipStreamDestroy(sd.s);
-                    for (hipEvent_t e : sd.e) (void)hipEventDestroy(e);
+                    if (sd.s2) {
+                        (void)hipStreamSynchronize(sd.s2);
+                        (void)hipStreamDestroy(sd.s2);
+                    }
+                    for (hipEvent_t e : sd.e)
+                        if (e) (void)hipEventDestroy(e);
                 }
                 sd = pcr::Side{};
             }
