@@ -2621,8 +2621,14 @@ static int launch_row9(const RowArgs5 &r0, int S, hipStream_t s) {
 template <bool kIdx>
 static int launch_regroup9(const RowArgs5 &r, int S, hipStream_t s) {
     // a pair has at most one tile per 32 rows plus one per bucket: ~3 per
-    // wave; 1-D, a pair's blocks on one XCD
-    const int nbp = cdiv(cdiv(r.Rmax, 32) + r.ntc / 2, 12);
+    // wave (PCR_REGROUP_TPB: tiles per 4-wave block); 1-D, a pair's blocks on
+    // one XCD
+    static const int tpb = [] {
+        const char *e = getenv("PCR_REGROUP_TPB");
+        const int v = e ? atoi(e) : 12;
+        return v >= 4 ? v : 12;
+    }();
+    const int nbp = cdiv(cdiv(r.Rmax, 32) + r.ntc / 2, tpb);
     const dim3 grid((unsigned)(8LL * nbp * cdiv(r.P, 8)));
     const dim3 fgrid(cdiv(r.Rmax, 1024), r.P);
     const size_t sm = sizeof(int) * (2 * (size_t)(r.ntc / 2) + 1);
