@@ -2620,13 +2620,13 @@ static int launch_row9(const RowArgs5 &r0, int S, hipStream_t s) {
 
 template <bool kIdx>
 static int launch_regroup9(const RowArgs5 &r, int S, hipStream_t s) {
-    // a pair has at most one tile per 32 rows plus one per bucket: ~3 per
-    // wave (PCR_REGROUP_TPB: tiles per 4-wave block); 1-D, a pair's blocks on
-    // one XCD
+    // a pair has at most one tile per 32 rows plus one per bucket: ~6 per
+    // wave (PCR_REGROUP_TPB: tiles per 4-wave block; 4 / 6 / 12 / 24 measured
+    // 0.36 / 0.34 / 0.30 / 0.29 ms per C4 step); 1-D, a pair's blocks on one XCD
     static const int tpb = [] {
         const char *e = getenv("PCR_REGROUP_TPB");
-        const int v = e ? atoi(e) : 12;
-        return v >= 4 ? v : 12;
+        const int v = e ? atoi(e) : 24;
+        return v >= 4 ? v : 24;
     }();
     const int nbp = cdiv(cdiv(r.Rmax, 32) + r.ntc / 2, tpb);
     const dim3 grid((unsigned)(8LL * nbp * cdiv(r.P, 8)));
