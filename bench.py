@@ -728,31 +728,45 @@ def _traffic_file():
     return _newest("pmc_traffic.json")
 
 
+# the pair count of the launches the traffic counters are quoted for (set by
+# main: tools/pmc_traffic.sh profiles the default 256-pair bench)
+_TRAFFIC_PAIRS = {"launch": 256}
+
+
 def _pmc_traffic(kernel, *more):
     """HBM bytes per launch (fetch + write) of the kernel whose name holds `kernel`
     (and every string of `more`) from the newest committed PMC summary
-    (tools/pmc_traffic.sh on this bench), or None when absent."""
+    (tools/pmc_traffic.sh on this bench, 256 pairs), scaled by the pair ratio
+    when this run's launches cover another pair count, or None when absent."""
     f = _traffic_file()
     if f is None:
         return None
     try:
         with open(f) as fh:
-            ks = json.load(fh)["kernels"]
+            d = json.load(fh)
+        ks = d["kernels"]
+        prof_pairs = int(d.get("pairs", 256))
     except (OSError, ValueError, KeyError):
         return None
+    ratio = _TRAFFIC_PAIRS["launch"] / prof_pairs
     for k, v in ks.items():
         if kernel in k and all(m in k for m in more):
             # the largest launch (RANSAC's gated second round is a near-empty
             # launch of the same kernel; older summaries have the mean only)
             f = v.get("fetch_size_bytes_max", v.get("fetch_size_bytes", 0.0))
             w = v.get("write_size_bytes_max", v.get("write_size_bytes", 0.0))
-            return f + w
+            return (f + w) * ratio
     return None
 
 
 def _traffic_source():
     f = _traffic_file()
-    return os.path.relpath(f, ROOT) if f else None
+    if not f:
+        return None
+    src = os.path.relpath(f, ROOT)
+    if _TRAFFIC_PAIRS["launch"] != 256:
+        src += f" (256-pair counters scaled {_TRAFFIC_PAIRS['launch']}/256)"
+    return src
 
 
 L2_HIT_CYC = 200        # MI355X_MICROARCH.md: global_load_dword L2-hit latency ~180-225 cycles
@@ -1205,6 +1219,7 @@ def main():
     # the job's `pairs` pairs split over the ranks (strong scaling);
     # every rank generates its own shard on the host
     first, P = shard(args.pairs, world, rank)
+    _TRAFFIC_PAIRS["launch"] = P
     if P == 0:
         print(f"bench: rank {rank} has no pairs ({args.pairs} over {world})", file=sys.stderr)
         sys.exit(2)
