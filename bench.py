@@ -918,17 +918,20 @@ def grid_candidates(src, tgt, T, d, slot_num=2):
 
 # Per 32 x 32 tile and wave, the inner loop of the shipped build's screens
 # (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 8
-# column tiles = 16 tiles, D = 32 -> the 1-term screen executes S + 1 = 3
-# k-chunks of 16: [f16(x) (2 chunks) | norms (1)]):
-#  featnn_row9<2,8,*> (passes 1 and 2, the same loop): 3 v_mfma_f32_32x32x16_f16,
-#    10.6 VALU per tile (the group-min sweep: 124 v_min3_u32 + 16 v_min + 8 x
-#    (v_max, v_cmp, v_cndmask) + 6 other per 16 tiles), 1.5 ds_read_b128,
-#    0.94 SALU, 0.69 s_nop;
+# column tiles = 16 tiles, D = 32 -> the 1-term screen executes S = 2 k-chunks
+# of 16, the f16(x) segment, with the columns' |y|^2 + B as the MFMA's C):
+#  featnn_row9<2,8,true> (pass 1): 2 v_mfma_f32_32x32x16_f16, 20.7 VALU per
+#    tile (per 16 tiles: 124 v_min3_u32 + 24 v_min + 8 x (v_max, v_cmp,
+#    v_cndmask) + 128 v_mov_b32_dpp -- the C operand's row broadcasts -- + 23
+#    other), 1.5 LDS reads, 0.5 s_nop;
+#  featnn_row9<2,8,false> (pass 2): the same with the C operand as 4
+#    ds_read_b128 per column tile: 12.6 VALU, 3 LDS reads, 0.4 s_nop.
 # SIMD issue cycles (MI355X guide, 'vector-instruction ISSUE cost'): an MFMA holds
 # vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the waves of a SIMD
-# share that port.  The MFMA pipe needs 3 x 32 = 96 cycles per tile.
-SCREEN_TILE_ISSUE = {"mfma": 3 * 8, "valu": 170 / 16 * 4, "lds": 24 / 16 * 4, "s_nop": 11 / 16 * 4}
-SCREEN_TILE_MFMA = 3
+# share that port.  The MFMA pipe needs 2 x 32 = 64 cycles per tile.
+SCREEN_TILE_ISSUE = {"mfma": 2 * 8, "valu": 331 / 16 * 4, "lds": 24 / 16 * 4, "s_nop": 8 / 16 * 4}
+SCREEN_TILE_ISSUE2 = {"mfma": 2 * 8, "valu": 202 / 16 * 4, "lds": 48 / 16 * 4, "s_nop": 6 / 16 * 4}
+SCREEN_TILE_MFMA = 2
 
 
 def _screen_issue_model(tiles, ms, table, mfma=SCREEN_TILE_MFMA):
@@ -1309,14 +1312,14 @@ def main():
     # computes in full; pass 2 re-screens only the target rows J that some
     # source chose (the mutual check), so the screen STAGE (pass 1 + pass 2 +
     # their regroups and 3-term fallbacks) is also reported against the same
-    # algorithmic flops.  The 1-term screen executes 16*(ceil(D/16)+1) k-steps
-    # per tile (the f16 values and one norm chunk) instead of D.
+    # algorithmic flops.  The 1-term screen executes 16*ceil(D/16) k-steps per
+    # tile (the f16 values; the norms come in as the MFMA's C) instead of D.
     ms_tot, launches = prof["feature_screen"]
     per_launch_ms = ms_tot / max(launches, 1)
     ms2_tot, launches2 = prof["feature_screen2"]
     per2_ms = ms2_tot / max(launches2, 1)
     flops_launch = 2.0 * P * N * N * D
-    kexec = 16 * (-(-D // 16) + 1)
+    kexec = 16 * (-(-D // 16))
     achieved = flops_launch / (per_launch_ms * 1e-3) / 1e12
     executed = achieved * kexec / D
     nn12 = torch.sort(pipe.nn12, dim=1).values
@@ -1377,8 +1380,9 @@ def main():
                                        "gfx950 note)",
                      "kernel": "featnn_row9<2,8,true> (pass 1: 1-term f16 screen on "
                                "v_mfma_f32_32x32x16_f16 with the operands transposed -- a lane "
-                               "holds one row -- and a group-min sweep; featnn_regroup9 recovers "
-                               "the winning group's column and second value)",
+                               "holds one row --, the columns' |y|^2 + B as the MFMA's accumulator "
+                               "input (2 MFMAs per tile) and a group-min sweep; featnn_regroup9 "
+                               "recovers the winning group's column and second value)",
                      "kernel_ms_per_launch": per_launch_ms, "launches": launches,
                      "flops_per_launch": flops_launch,
                      "executed_mfma_tflops": executed,
@@ -1391,7 +1395,7 @@ def main():
                                "j_rows_mean": float(jrows.mean()),
                                "flops_per_launch": 2.0 * float(jrows.sum()) * N * D,
                                "traffic": _pmc_traffic("featnn_row9<", "false>"),
-                               "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN_TILE_ISSUE)},
+                               "issue_model": _screen_issue_model(tiles2, per2_ms, SCREEN_TILE_ISSUE2)},
                      "screen_stage": {"ms_per_launch": stage_ms, "achieved": stage_tf,
                                       "frac": stage_tf / PEAK_F16_MFMA_TFLOPS,
                                       "parts_ms_per_step": {k: prof[k][0] / args.steps for k in (

@@ -269,6 +269,7 @@ struct PackIO {
     unsigned *nmax[2];
     unsigned *emax[2];  // per pair: max over the cloud's rows of |x s - f16(x s)| (the 1-term screen's bound)
     float *rex[2];      // per row: its |x s - f16(x s)| (rounded up; featnn_regroup9's bound)
+    float *ct[2];       // per row: f32(|x s|^2), -1 on padding rows (feat_colterms adds the bias)
 };
 
 // |x - f16(x)| of one row (x already scaled), rounded up: e^2 summed exactly
@@ -401,6 +402,7 @@ __global__ __launch_bounds__(256) void feat_pack5(PackIO io, int D, int S, Split
         if (h == 0) {
             nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
             io.rex[role][(size_t)p * ntiles * 32 + t * 32 + rr] = valid ? split_err_norm(ea) : 0.0f;
+            io.ct[role][(size_t)p * ntiles * 32 + t * 32 + rr] = valid ? (float)acc : -1.0f;
         }
         block_max_atomic(__float_as_uint(r), wmax, nmax + p);
         __syncthreads();
@@ -518,6 +520,7 @@ __global__ __launch_bounds__(256) void feat_pack5r(PackIO io, Split5 sp, PackCtl
         if (h == 0) {
             nrm[(size_t)p * ntiles * 32 + t * 32 + rr] = r;
             io.rex[role][(size_t)p * ntiles * 32 + t * 32 + rr] = valid ? split_err_norm(ea) : 0.0f;
+            io.ct[role][(size_t)p * ntiles * 32 + t * 32 + rr] = valid ? (float)acc : -1.0f;
         }
         block_max_atomic(__float_as_uint(r), wmax, nmax + p);
         __syncthreads();
@@ -1084,11 +1087,41 @@ struct RowArgs5 {
     // [P][csl][Rmax], merged by featnn_slicemerge
     int csl;
     uint4 *part;
+    // featnn_row9: the column cloud's and the row cloud's per-row terms
+    // f32(|.|^2 + B) ([P][ntc * 32], [P][ntr * 32]) and B
+    const float *cct, *rct;
+    const float *cbias;  // [P] B
 };
 
 // rows (pass 1) and J columns (pass 2) the 1-term screens left to the 3-term
 // ones since the last reset (diagnostic, pcr_featnn_fallback_rows)
 __device__ unsigned long long g_featnn_fallback_rows[2];
+
+// featnn_row9's column terms (after the packs and their repairs): the packs
+// stored f32(|x s|^2) per row, -1 on padding rows; here ct = f32(that + B) with
+// B the pair's smallest power of two above both clouds' max |x s|^2 (from the
+// packs' max norms, a rounding's margin added), so every screened value
+// ct_j - 2 x.y_j >= B - |x|^2 > 0 (unsigned order = float order) and ct lies in
+// [B, 2B] (2B - ct exact).  Padding rows: 16 B, above every real value (< 4 B).
+// A pair with a non-finite norm takes B = 2^60 (its rows certify nothing).
+__global__ __launch_bounds__(256) void feat_colterms(float *fct, float *gct, int ntn, int ntm,
+                                                     const unsigned *fmax, const unsigned *gmax, float *cbias) {
+    const int p = blockIdx.y, role = blockIdx.z;
+    const float mf = __builtin_fmaxf(__uint_as_float(fmax[p]), __uint_as_float(gmax[p]));
+    double B = 0x1p60;
+    if (mf < 0x1p50f) {
+        const double m2 = (double)mf * (double)mf * (1.0 + 0x1p-18) + 1.0;
+        const int e = (int)((__double_as_longlong(m2) >> 52) & 0x7ff) - 1023;  // m2 in [2^e, 2^(e+1))
+        B = __builtin_ldexp(1.0, e + 1);
+    }
+    if (blockIdx.x == 0 && role == 0 && threadIdx.x == 0) cbias[p] = (float)B;
+    const int nt = role ? ntm : ntn;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nt * 32) return;
+    float *ct = (role ? gct : fct) + (size_t)p * nt * 32 + i;
+    const float x = *ct;
+    *ct = x < 0.0f ? (float)(16.0 * B) : (float)((double)x + B);
+}
 
 // One row's operand fragments exactly as feat_pack5 / feat_pack5r store them
 // (same scale, same operations in the same order), for lane half h: x the
@@ -1450,24 +1483,43 @@ __device__ __forceinline__ double sub_term(int D) { return 6.103515625e-05 * __b
 // pk the relative truncation of the values' low bits (the column code of
 // featnn_row8 pass 1; 0 when the values carry no code).  Returns whether the
 // row goes to a.list (the caller appends it)
-template <bool kIdx, bool kOne, int NX>
+template <bool kIdx, bool kOne, int NX, bool kCT = false>
 __device__ __forceinline__ bool row_tail(const RowArgs5 &a, int p, int row, int m, unsigned B1, unsigned B2,
-                                         int mi1, float rexv, double pk) {
+                                         int mi1, float rexv, double pk, float ctr = 0.0f) {
     constexpr double kBias = kOne ? kRowBias1 : kRowBias;
+    constexpr double u = 5.9604644775390625e-08;  // 2^-24
     const double sub = kOne ? sub_term(a.D) : 0.0;
     const float mb1 = __uint_as_float(B1), mb2 = __uint_as_float(B2);
     // this row's screen error bound (2x, as bound5): the split's or the 1-term's,
-    // plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled
+    // plus the bias's share of the accumulation error, 2 (Kt + 2) u B, doubled.
+    // kCT (featnn_row9): the values are ct_j - 2 f16(x).f16(y_j) with the column
+    // term ct_j = f32(|y_j|^2 + B) as the MFMA's accumulator input: the f32
+    // accumulation over |C| + |products| <= B + G^2 + 2 (q + ex)(G + E), the f16
+    // dot error as bound1, and ct_j's own roundings (f32 |y|^2, then + B),
+    // u (2 B + G^2).  The row's |x|^2 is not in the values: its own ct (ctr,
+    // rounding u (2 B + q^2)) turns a value into a distance, value - (2 B - ctr)
+    // (exact: Sterbenz).  B: the pair's (feat_colterms).
     const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
     const double Gm = (double)__uint_as_float(a.cmax[p]);
-    const double bnd = (kOne ? bound1(qn, (double)rexv + sub, Gm,
-                                      (double)__uint_as_float(a.cemax[p]) + sub, 16 * NX)
-                             : bound5(qn, Gm, 16 * NX, a.D)) +
-                       4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kBias;
+    double bnd, bias, ebias = 0.0;
+    if constexpr (kCT) {
+        const double ex = (double)rexv + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
+        const double B = (double)a.cbias[p];
+        const double err = 2.0 * (16 * NX + 2) * u * ((B + Gm * Gm) + 2.0 * (qn + ex) * (Gm + E)) +
+                           2.0 * (ex * Gm + (qn + ex) * E) + u * (2.0 * B + Gm * Gm) * (1.0 + 0x1p-20) + 4.0;
+        bnd = 2.0 * err;
+        bias = 2.0 * B - (double)ctr;
+        ebias = u * (2.0 * B + qn * qn) * (1.0 + 0x1p-20);
+    } else {
+        bnd = (kOne ? bound1(qn, (double)rexv + sub, Gm, (double)__uint_as_float(a.cemax[p]) + sub, 16 * NX)
+                    : bound5(qn, Gm, 16 * NX, a.D)) +
+              4.0 * (16 * NX + 2) * u * kBias;
+        bias = kBias;
+    }
     if constexpr (!kIdx) {  // pass 2: the row's biased top-2 values, its bound and the bias, by original row
-        const double e2 = 0.5 * bnd;
+        const double e2 = 0.5 * bnd + ebias;
         a.wq[(size_t)p * a.Rmax + row] = make_float4(m == 0 ? __builtin_inff() : mb1, m == 0 ? __builtin_inff() : mb2,
-                                                     (float)(e2 * (1.0 + 1e-6)), (float)kBias);
+                                                     (float)(e2 * (1.0 + 1e-6)), (float)bias);
         // 1-term: a column whose gap the resolve could not use goes to the
         // 3-term screen (a.list; the 3-term pass lists nothing)
         return kOne && m != 0 && a.list &&
@@ -1481,8 +1533,8 @@ __device__ __forceinline__ bool row_tail(const RowArgs5 &a, int p, int row, int 
         a.e[o] = 0.0f;
         return false;
     }
-    a.v[o] = (double)mb1 - kBias;  // exact (both multiples of mb1's ulp)
-    a.e[o] = (float)((0.5 * bnd + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
+    a.v[o] = (double)mb1 - bias;  // exact (f32 values of a few binades: multiples of mb1's ulp)
+    a.e[o] = (float)((0.5 * bnd + ebias + pk * __builtin_fabs((double)mb1)) * (1.0 + 1e-6));
     // the certificate: the top-2 gap against twice the per-value bound, or
     // (1-term) against a bound on the DIFFERENCE of two values' errors.  Only
     // columns j screened within 2 err of the winner j1 can overtake it, and
@@ -1496,8 +1548,8 @@ __device__ __forceinline__ bool row_tail(const RowArgs5 &a, int p, int row, int 
         const double ex = (double)rexv + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
         const double dot = 2.0 * (ex * Gm + (qn + ex) * E);       // bound1's dot-product share
         const double rest = 0.5 * bnd - dot;                        // accumulation, norms, bias
-        const double er = 0.5 * bnd + pk * __builtin_fabs((double)mb2);
-        const double b1v = __builtin_fmax((double)mb1 - kBias, 0.0);
+        const double er = 0.5 * bnd + ebias + pk * __builtin_fabs((double)mb2);
+        const double b1v = __builtin_fmax((double)mb1 - bias, 0.0);
         const double win = 2.0 * rest + 2.0 * ex * (__builtin_sqrt(b1v + 3.0 * er) + __builtin_sqrt(b1v + er)) +
                            4.0 * (qn + ex) * E;
         thr = __builtin_fmin(bnd, win * (1.0 + 1e-9));
@@ -1512,23 +1564,27 @@ __device__ __forceinline__ bool row_tail(const RowArgs5 &a, int p, int row, int 
 
 // featnn_row9's early test: a row whose gap between its smallest value and
 // the second smallest GROUP minimum -- an upper bound on its true second
-// value -- already fails the 1-term certificate (row_tail's, pk = 0) fails it
+// value -- already fails the certificate (row_tail's kCT one, pk = 0) fails it
 // whatever the winning group's own second: it goes to the 3-term screen right
 // after the sweep (beside the regroup) instead of through the regroup.
 template <bool kIdx, int NX>
 __device__ __forceinline__ bool one_term_fails(const RowArgs5 &a, int p, int row, unsigned B1, unsigned B2g,
-                                               float rexv) {
+                                               float rexv, float ctr) {
+    constexpr double u = 5.9604644775390625e-08;  // 2^-24
     const double sub = sub_term(a.D);
     const double mb1 = (double)__uint_as_float(B1), mb2 = (double)__uint_as_float(B2g);
     const double qn = (double)a.rnr[(size_t)p * a.ntr * 32 + row];
     const double Gm = (double)__uint_as_float(a.cmax[p]);
     const double ex = (double)rexv + sub, E = (double)__uint_as_float(a.cemax[p]) + sub;
-    const double bnd = bound1(qn, ex, Gm, E, 16 * NX) + 4.0 * (16 * NX + 2) * 5.9604644775390625e-08 * kRowBias1;
-    if constexpr (!kIdx) return !(mb2 - mb1 > bnd * (1.0 + 1e-6) + 1e-6 * mb1);
+    const double B = (double)a.cbias[p];
+    const double bnd = 2.0 * (2.0 * (16 * NX + 2) * u * ((B + Gm * Gm) + 2.0 * (qn + ex) * (Gm + E)) +
+                              2.0 * (ex * Gm + (qn + ex) * E) + u * (2.0 * B + Gm * Gm) * (1.0 + 0x1p-20) + 4.0);
+    const double ebias = u * (2.0 * B + qn * qn) * (1.0 + 0x1p-20);
+    if constexpr (!kIdx) return !(mb2 - mb1 > (bnd + 2.0 * ebias) * (1.0 + 1e-6) + 1e-6 * mb1);
     const double dot = 2.0 * (ex * Gm + (qn + ex) * E);
     const double rest = 0.5 * bnd - dot;
-    const double er = 0.5 * bnd;
-    const double b1v = __builtin_fmax(mb1 - kRowBias1, 0.0);
+    const double er = 0.5 * bnd + ebias;
+    const double b1v = __builtin_fmax(mb1 - (2.0 * B - (double)ctr), 0.0);
     const double win = 2.0 * rest + 2.0 * ex * (__builtin_sqrt(b1v + 3.0 * er) + __builtin_sqrt(b1v + er)) +
                        4.0 * (qn + ex) * E;
     return !(mb2 - mb1 > __builtin_fmin(bnd, win * (1.0 + 1e-9)));
@@ -1830,18 +1886,24 @@ __global__ __launch_bounds__(256) void featnn_slicemerge(RowArgs5 a) {
 // that step, one 32-row tile per bucket segment (~1 % of the sweep's MFMAs).
 // Then second = min(B2, the group's own second) exactly, the values carry no
 // code bits (pk = 0), and the certification and outputs are featnn_row8's
-// (row_tail).
+// (row_tail, its kCT bound).
+// The norms are not an MFMA: the columns' terms ct_j = f32(|y_j|^2 + B)
+// (feat_colterms, B the pair's) are the MFMA chain's accumulator input, so a
+// tile costs S = 2 MFMAs instead of S + 1 and the values are ct_j - 2 x.y_j
+// (the row's |x|^2 left out: a constant per row).  A lane's 16 C values per
+// column tile come from the LDS copy of the group's terms or by DPP row
+// broadcasts of one float per lane (see the sweep).
 // ---------------------------------------------------------------------------
 
-// The 1-term row operand of one row (lane half h) built from its f32 values,
-// exactly as the packs store its [f16 segment | norms] chunks (row_frags), with
-// the bias patch 64 opposite the column image's 2^15 (see featnn_row8): one
-// 128-byte line per row where the packed image spreads it over S + 1 lines --
-// the regroup gathers rows.  The sweep and the regroup both build it here, so
-// their MFMA chains agree bit for bit.
+// The 1-term row operand of one row (lane half h) built from its f32 values:
+// its -2 f16(x) chunks exactly as the packs store them (row_frags) -- one
+// 128-byte line per row where the packed image spreads it over S lines: the
+// regroup gathers rows.  The sweep and the regroup both build it here, so
+// their MFMA chains agree bit for bit.  (No norm chunk: featnn_row9 takes the
+// columns' |y|^2 + B as the MFMA's accumulator input and leaves |x|^2 out.)
 template <int S>
 __device__ __forceinline__ void row_operand1(const RowArgs5 &a, int p, int row, bool valid, int h,
-                                             f16x8 (&A)[S + 1]) {
+                                             f16x8 (&A)[S]) {
     const float sc = __uint_as_float(a.sc[p]);
     float x[16 * S];
     const float *xr = a.Xr + ((size_t)p * a.Rmax + row) * a.D;
@@ -1858,14 +1920,31 @@ __device__ __forceinline__ void row_operand1(const RowArgs5 &a, int p, int row, 
 #pragma unroll
         for (int q = 0; q < 16 * S; ++q) x[q] = 0.0f;
     }
-    f16x8 fr[2 * S + 1];
-    row_frags<S>(x, a.D, h, a.role, a.cs, fr);
+    // both lane halves' elements at compile-time indices, then the half's pick
+    // (an index by h is a select chain over the row)
+    auto seg = [&](int k) {
+        const _Float16 hi = (_Float16)x[k];
+        return k < a.D ? (a.role == 0 ? (_Float16)(-2.0f * (float)hi) : hi) : (_Float16)0.0f;
+    };
 #pragma unroll
-    for (int c = 0; c < S + 1; ++c) A[c] = fr[c < S ? c : 2 * S];
-    if (h == 0) {
-        if (a.role == 0) A[S][6] = (_Float16)64.0f;
-        else A[S][7] = (_Float16)64.0f;
+    for (int c = 0; c < S; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const _Float16 v0 = seg(16 * c + j), v1 = seg(16 * c + 8 + j);
+            A[c][j] = h ? v1 : v0;
+        }
+}
+
+// a lane's 16 column terms of column tile ct (register r: column
+// 8 (r / 4) + 4 h + (r % 4)), from 32 floats per tile
+__device__ __forceinline__ f32x16 colterms(const float *tile32, int h) {
+    f32x16 c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float4 v = *reinterpret_cast<const float4 *>(tile32 + 8 * j + 4 * h);
+        c[4 * j] = v.x; c[4 * j + 1] = v.y; c[4 * j + 2] = v.z; c[4 * j + 3] = v.w;
     }
+    return c;
 }
 
 __device__ __forceinline__ unsigned fbits(float v) { return __float_as_uint(v); }
@@ -1891,9 +1970,10 @@ template <int S, int G, bool kIdx>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void featnn_row9(RowArgs5 a) {
     constexpr int W = 8, RT = 2;          // waves per workgroup, row tiles per wave
     constexpr int NM = 2 * S + 1;         // stored k-chunks of the packed images
-    constexpr int NB = S + 1;             // executed chunks: [f16 segment | norms]
-    constexpr int kB = G * NB * 64;       // f16x8 per B buffer
-    static_assert(G % 2 == 0 && S <= 2, "column tiles in pairs");
+    constexpr int NB = S;                 // executed chunks: the f16 segment
+    constexpr int kT = G * NB * 64;       // f16x8 of a B buffer's fragments
+    constexpr int kB = kT + G * 8;        // + the group's column terms (G x 32 floats)
+    static_assert(G % 2 == 0 && S <= 2 && G * 8 <= 64, "column tiles in pairs; one DMA for the terms");
     __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const int ppx = (a.P + 7) >> 3;
@@ -1914,36 +1994,84 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         const int k = (qt0 + t) * 32 + (l & 31);
         row_operand1<S>(a, p, rl ? (k < nr ? rl[k] : 0) : k, k < nr, h, A[t]);
     }
-    unsigned B1[RT], B2[RT], I[RT];
+    // per row tile: B1, B2, I as above; pm the min of the current step's
+    // first column tile (the group's first half)
+    unsigned B1[RT], B2[RT], I[RT], pm[RT];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) { B1[t] = 0x7f800000u; B2[t] = 0x7f800000u; I[t] = 0u; }
+    for (int t = 0; t < RT; ++t) { B1[t] = 0x7f800000u; B2[t] = 0x7f800000u; I[t] = 0u; pm[t] = 0x7f800000u; }
     const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
+    const float *csrc = a.cct + (size_t)p * a.ntc * 32 + 4 * l;
     auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NB; c += W) {
+        for (int c = wid; c < G * NB + 1; c += W) {
+            if (c == G * NB) {  // the group's column terms: G x 128 B, one 16-B piece per lane
+                if (l < G * 8)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void *)(csrc + (size_t)grp * G * 32),
+                        (__attribute__((address_space(3))) void *)(Bs + bufi * kB + kT), 16, 0, 0);
+                continue;
+            }
             const int g = c / NB, cc = c - g * NB;
-            const int sch = cc < S ? cc : 2 * S;  // the stored chunk
-            const f16x8 *src = bsrc + ((size_t)(grp * G + g) * NM + sch) * 64;
+            const f16x8 *src = bsrc + ((size_t)(grp * G + g) * NM + cc) * 64;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)src,
                 (__attribute__((address_space(3))) void *)(Bs + bufi * kB + c * 64), 16, 0, 0);
         }
     };
-    // row tile t's group of step st: the values of column tiles 2 st, 2 st + 1
-    auto epilogue = [&](const f32x16 (&x)[2], int t, unsigned st) {
-        const unsigned mn = group_min32(x[0], x[1]);
+    // min of a lane's 16 values of one column tile and c0 (two v_min3 chains)
+    auto min16 = [](const f32x16 &x, unsigned c0) {
+        unsigned c1 = umin2(umin2(fbits(x[8]), fbits(x[9])), fbits(x[10]));
+        c0 = umin2(umin2(c0, fbits(x[0])), fbits(x[1]));
+        c1 = umin2(umin2(c1, fbits(x[11])), fbits(x[12]));
+        c0 = umin2(umin2(c0, fbits(x[2])), fbits(x[3]));
+        c1 = umin2(umin2(c1, fbits(x[13])), fbits(x[14]));
+        c0 = umin2(umin2(c0, fbits(x[4])), fbits(x[5]));
+        c0 = umin2(umin2(c0, fbits(x[6])), fbits(x[7]));
+        return umin2(umin2(c1, fbits(x[15])), c0);
+    };
+    // row tile t's group of step st closed by its second column tile y
+    auto close = [&](const f32x16 &y, int t, unsigned st) {
+        const unsigned mn = min16(y, pm[t]);
         const unsigned n2 = umin2(umax2(B1[t], mn), B2[t]);  // 2nd smallest of {B1, B2, mn}
         I[t] = mn < B1[t] ? st : I[t];
         B1[t] = umin2(B1[t], mn);
         B2[t] = n2;
     };
+    // A tile's 16 column terms per lane (the MFMA's C): registers [0, 4 KL) as
+    // KL ds_read_b128 of the LDS copy, the rest from ONE float per lane -- lane
+    // l holds column 8 (n / 4) + (n % 4) + 4 h of the tile (n = l % 16), so the
+    // DPP row broadcast of row position r gives every lane its register r's
+    // column (one v_mov_dpp per register).  Measured (C4, featnn_bench alone):
+    // pass 1 1.15 ms with KL = 0, 1.19 with KL = 4 (4 KB of LDS reads per wave
+    // and column tile), the mixes 1.21 - 1.24; pass 2 0.77 with KL = 4 against
+    // 0.80 with KL = 0.
+    const int cl = 8 * ((l & 15) >> 2) + (l & 3) + 4 * h;
+#ifndef PCR_CT_LDS1
+#define PCR_CT_LDS1 0
+#endif
+#ifndef PCR_CT_LDS2
+#define PCR_CT_LDS2 4
+#endif
+    constexpr int KL = kIdx ? PCR_CT_LDS1 : PCR_CT_LDS2;
+    constexpr int kCR = KL + (KL < 4 ? 1 : 0), kCV = 16 - 4 * KL;  // LDS reads / VALU per tile's terms
+    // registers [4 KL, 16) of a tile's terms from the lane's float v
+    auto cterms = [&](f32x16 &c, int v) {
+#define PCR_BC(r) if ((r) >= 4 * KL) c[r] = __int_as_float(__builtin_amdgcn_mov_dpp(v, 0x150 + (r), 0xf, 0xf, false))
+        PCR_BC(0); PCR_BC(1); PCR_BC(2); PCR_BC(3); PCR_BC(4); PCR_BC(5); PCR_BC(6); PCR_BC(7);
+        PCR_BC(8); PCR_BC(9); PCR_BC(10); PCR_BC(11); PCR_BC(12); PCR_BC(13); PCR_BC(14); PCR_BC(15);
+#undef PCR_BC
+    };
+    // Schedule per step (two column tiles u = 0, 1; both row tiles in each
+    // phase), so one tile's 16 column terms are live at a time:
+    //   A: tile u = 0's 4 MFMAs (C = its terms) | the previous step's closes
+    //   B: tile u = 1's 4 MFMAs                  | this step's first halves (pm)
+    // Each phase reads the next phase's fragments and terms behind its MFMAs.
     f32x16 acc[RT][2];
-    // the first phase A finds a harmless pending epilogue: +inf
+    // the first phase A closes a harmless pending group: +inf
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[1][c][r] = __builtin_inff();
+        for (int r = 0; r < 16; ++r) acc[t][1][r] = __builtin_inff();
     unsigned pend = 0u;
-    const f32x16 zero = {};
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1951,59 +2079,75 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         const int buf = grp & 1;
         if (grp + 1 < ngroups) issue(grp + 1, buf ^ 1);
         const f16x8 *Bb = Bs + buf * kB + l;
-        f16x8 Bf[2][NB];
+        const float *Cb = reinterpret_cast<const float *>(Bs + buf * kB + kT);
+        const int *Cv = reinterpret_cast<const int *>(Cb) + cl;
+        auto cnext = [&](int u) {
+            f32x16 c;
 #pragma unroll
-        for (int c = 0; c < NB; ++c)
+            for (int j = 0; j < KL; ++j) {
+                const float4 v = *reinterpret_cast<const float4 *>(Cb + 32 * u + 8 * j + 4 * h);
+                c[4 * j] = v.x; c[4 * j + 1] = v.y; c[4 * j + 2] = v.z; c[4 * j + 3] = v.w;
+            }
+            if constexpr (KL < 4) cterms(c, Cv[32 * u]);
+            return c;
+        };
+        f16x8 Bf[NB];
+        f32x16 Cf;
 #pragma unroll
-            for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[(u * NB + c) * 64];
+        for (int c = 0; c < NB; ++c) Bf[c] = Bb[c * 64];
+        Cf = cnext(0);
+        __builtin_amdgcn_sched_barrier(0);  // the group's first reads: a region of their own
 #pragma unroll
         for (int st = 0; st < G / 2; ++st) {
             const unsigned stp = (unsigned)(grp * (G / 2) + st);
-            // phase A: row tile 0's MFMAs beside row tile 1's previous epilogue
+            // phase A
 #pragma unroll
             for (int c = 0; c < NB; ++c)
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
-                    acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[0][c],
-                                                                       c == 0 ? zero : acc[0][u], 0, 0, 0);
-            epilogue(acc[1], 1, pend);
-            if (st == 0) SGB(0x100, 2 * NB, 0);
-            SGB(0x002, 3, 0);
+                for (int t = 0; t < RT; ++t)
+                    acc[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[c], A[t][c], c == 0 ? Cf : acc[t][0], 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 2 * NB; ++i) {
+            for (int t = 0; t < RT; ++t) close(acc[t][1], t, pend);
+#pragma unroll
+            for (int c = 0; c < NB; ++c) Bf[c] = Bb[((2 * st + 1) * NB + c) * 64];
+            Cf = cnext(2 * st + 1);
+            SGB(0x002, 2, 0);
+#pragma unroll
+            for (int i = 0; i < NB * RT; ++i) {
                 SGB(0x008, 1, 0);
-                SGB(0x002, 3, 0);
+                SGB(0x002, 5, 0);
             }
+            SGB(0x100, NB + kCR, 0);
+            SGB(0x002, 6 + kCV, 0);
             __builtin_amdgcn_sched_barrier(0);
-            // phase B: row tile 1's MFMAs beside row tile 0's epilogue
+            // phase B
 #pragma unroll
             for (int c = 0; c < NB; ++c)
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
-                    acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[1][c],
-                                                                       c == 0 ? zero : acc[1][u], 0, 0, 0);
-            epilogue(acc[0], 0, stp);
-            if (st + 1 < G / 2) {  // the next step's fragments, behind this phase's MFMAs
+                for (int t = 0; t < RT; ++t)
+                    acc[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[c], A[t][c], c == 0 ? Cf : acc[t][1], 0, 0, 0);
 #pragma unroll
-                for (int c = 0; c < NB; ++c)
+            for (int t = 0; t < RT; ++t) pm[t] = min16(acc[t][0], 0x7f800000u);
+            if (st + 1 < G / 2) {
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) Bf[u][c] = Bb[((2 * st + 2 + u) * NB + c) * 64];
+                for (int c = 0; c < NB; ++c) Bf[c] = Bb[((2 * st + 2) * NB + c) * 64];
+                Cf = cnext(2 * st + 2);
             }
-            SGB(0x008, 2, 0);
 #pragma unroll
-            for (int i = 0; i < 2 * NB - 2; ++i) {
-                SGB(0x002, 4, 0);
+            for (int i = 0; i < NB * RT; ++i) {
                 SGB(0x008, 1, 0);
+                SGB(0x002, 4, 0);
             }
-            if (st + 1 < G / 2) SGB(0x100, 2 * NB, 0);
-            SGB(0x002, 8, 0);
+            if (st + 1 < G / 2) SGB(0x100, NB + kCR, 0);
+            if (st + 1 < G / 2 && kCV) SGB(0x002, kCV, 0);
             __builtin_amdgcn_sched_barrier(0);
             pend = stp;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    epilogue(acc[1], 1, pend);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) close(acc[t][1], t, pend);
     // the row's two lane halves: the smaller B1 wins (the lower half on a tie:
     // a zero gap, uncertified either way); the second smallest of the union.
     // The row goes to its winning step's bucket as (row, B1, B2, half); a row
@@ -2021,9 +2165,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         const unsigned wst = min(mine ? I[t] : oi, (unsigned)(nst - 1));
         const int k = (qt0 + t) * 32 + (l & 31);
         if (h == 0 && k < nr) {
-            const int row = rl ? rl[k] : k;
+            // re-read, not kept from the operand build across the sweep (registers)
+            const int row = rl ? reinterpret_cast<const volatile int *>(rl)[k] : k;
             const size_t bk = (size_t)p * nst + wst;
-            const bool early = one_term_fails<kIdx, S + 1>(a, p, row, w1, s2, a.rre[(size_t)p * a.ntr * 32 + row]);
+            const bool early = one_term_fails<kIdx, S>(a, p, row, w1, s2, a.rre[(size_t)p * a.ntr * 32 + row],
+                                                       a.rct[(size_t)p * a.ntr * 32 + row]);
             const int rank = early ? a.bcap : atomicAdd(a.bcnt + bk, 1);
             if (rank < a.bcap) {
                 a.blist[bk * a.bcap + rank] = make_uint4((unsigned)row, w1, s2, mine ? 0u : 1u);
@@ -2048,7 +2194,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
 constexpr int kRegroupMaxSteps = 4096;
 template <int S, bool kIdx>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void featnn_regroup9(RowArgs5 a) {
-    constexpr int NM = 2 * S + 1, NB = S + 1;
+    constexpr int NM = 2 * S + 1, NB = S;
     // the pair's per-step tile prefix and row counts, 2 (steps + 1) ints of
     // dynamic LDS (a static 4097-entry pair held 32 KB and four blocks per CU)
     extern __shared__ int rg_lds[];
@@ -2090,8 +2236,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     __syncthreads();
     const int ntiles = ts[nst];
     const f16x8 *bimg = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
+    const float *ctp = a.cct + (size_t)p * a.ntc * 32;
     const uint4 *bl = a.blist + (size_t)p * nst * a.bcap;
-    const f32x16 zero = {};
     // tile q's bucket, its rows' entries (the next tile's loaded while this one runs)
     auto locate = [&](int q, int &b, bool &valid, uint4 &e) {
         int lo = 0, hi = nst;  // ts[lo] <= q < ts[hi]
@@ -2117,18 +2263,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         if (q + qs < ntiles) locate(q + qs, bn, vn, en);
         const int row = (int)e.x;
         f16x8 Bf[2][NB];
+        f32x16 acc[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < 2; ++u) {
 #pragma unroll
-            for (int c = 0; c < NB; ++c) Bf[u][c] = bimg[((size_t)(2 * b + u) * NM + (c < S ? c : 2 * S)) * 64];
+            for (int c = 0; c < NB; ++c) Bf[u][c] = bimg[((size_t)(2 * b + u) * NM + c) * 64];
+            acc[u] = colterms(ctp + (size_t)(2 * b + u) * 32, h);
+        }
         f16x8 A[NB];
         row_operand1<S>(a, p, row, valid, h, A);
-        f32x16 acc[2];
 #pragma unroll
         for (int c = 0; c < NB; ++c)
 #pragma unroll
             for (int u = 0; u < 2; ++u)
-                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[c], c == 0 ? zero : acc[u], 0, 0, 0);
+                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Bf[u][c], A[c], acc[u], 0, 0, 0);
         if (valid && (int)e.w == h) {
             // the winner's column (the first in column order among equal
             // patterns) and the group's second smallest value
@@ -2185,8 +2333,9 @@ __global__ __launch_bounds__(256) void featnn_finish9(RowArgs5 a) {
     for (int i = 0; i < R; ++i) {
         put[i] = false;
         if (rc[i].w == 0u)
-            put[i] = row_tail<kIdx, true, S + 1>(a, p, rows[i], m, rc[i].y, rc[i].z, (int)rc[i].x,
-                                                 a.rre[(size_t)p * a.ntr * 32 + rows[i]], 0.0);
+            put[i] = row_tail<kIdx, true, S, true>(a, p, rows[i], m, rc[i].y, rc[i].z, (int)rc[i].x,
+                                                   a.rre[(size_t)p * a.ntr * 32 + rows[i]], 0.0,
+                                                   a.rct[(size_t)p * a.ntr * 32 + rows[i]]);
         mine += put[i] ? 1 : 0;
     }
     // block-wide exclusive offsets of the listed rows
@@ -2376,6 +2525,8 @@ struct V5Buf {
     unsigned *gemax, *femax;  // per pair max |x - f16(x)| of the column (G) / row (F) images
     int *fbc12, *fbc21, *fbl12, *fbl21;  // the rows a 1-term screen left for the 3-term one
     float *fre, *gre;                    // per row |x - f16(x)| of F / G (scaled, rounded up)
+    float *fct, *gct;                    // per row f32(|x|^2 + B) of F / G (featnn_row9's column terms)
+    float *cbias;                        // [P] their B (feat_colterms)
 };
 
 static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax, int D,
@@ -2397,7 +2548,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     const size_t ap = (size_t)P * ntn * NM * 64, bp = (size_t)P * ntm * NM * 64;  // f16x8
     const size_t nn_n = (size_t)P * ntn * 32, nn_m = (size_t)P * ntm * 32;
     const size_t bytes =
-        16 * (ap + bp) + 4 * (2 * (nn_n + nn_m) + 9 * (size_t)P + 2 * (size_t)P * (Nmax + Mmax) + 18 * (size_t)P);
+        16 * (ap + bp) + 4 * (3 * (nn_n + nn_m) + 9 * (size_t)P + 2 * (size_t)P * (Nmax + Mmax) + 19 * (size_t)P);
     char *ws = (char *)workspace(2, bytes + 256);
     PCR_REQUIRE(ws, PCR_ERR_NOMEM, "feature_match: %s", pcr_last_error());
     v.Ap = (f16x8 *)ws;
@@ -2406,10 +2557,12 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     v.gnr = v.fnr + nn_n;
     v.fre = v.gnr + nn_m;
     v.gre = v.fre + nn_n;
+    v.fct = v.gre + nn_m;
+    v.gct = v.fct + nn_n;
     // [0,P): max|y|  [P,2P): max|x|  [2P,3P): the scale used  [3P,4P): cnt12  [4P,5P): cnt21
     // [5P,6P): gemax  [6P,7P): femax  [7P,8P): fbc12  [8P,9P): fbc21 (feat_sample clears
     // all but the scale)
-    v.gmax = (unsigned *)(v.gre + nn_m);
+    v.gmax = (unsigned *)(v.gct + nn_m);
     v.fmax = v.gmax + P;
     v.mx = v.gmax + 2 * P;
     v.cnt12 = (int *)(v.gmax + 3 * P);
@@ -2425,6 +2578,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     unsigned *mxp = (unsigned *)(v.fbl21 + (size_t)P * Mmax);  // [P][2][zr] partial maxima (repair)
     unsigned *smax = mxp + 2 * (size_t)P * 8;                     // [P] sample maxima
     int *bad = (int *)(smax + P);                                  // [P] repair flags
+    v.cbias = (float *)(bad + P);                                  // [P] featnn_row9's B
     prof_begin(s, kProfFeatPack);
     hipLaunchKernelGGL(feat_sample, dim3(P), dim3(256), 0, s, F, n_src, Nmax, G, n_tgt, Mmax, D, smax, v.gmax,
                        bad, P);
@@ -2440,12 +2594,15 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
         }
         const int gy = rep ? R : P;
         PackIO io{{F, G}, {n_src, n_tgt}, {Nmax, Mmax}, {ntn, ntm}, {v.Ap, v.Bp}, {v.fnr, v.gnr}, {v.fmax, v.gmax},
-                  {v.femax, v.gemax}, {v.fre, v.gre}};
+                  {v.femax, v.gemax}, {v.fre, v.gre}, {v.fct, v.gct}};
         const dim3 grid(cdiv(std::max(ntn, ntm), 4), gy, 2);
         if (D == 32) hipLaunchKernelGGL(feat_pack5r<32>, grid, dim3(256), 0, s, io, v.sp, pc);  // register-resident
         else hipLaunchKernelGGL(feat_pack5, grid, dim3(256), 0, s, io, D, v.S, v.sp, pc);
         PCR_LAUNCH_CHECK();
     }
+    hipLaunchKernelGGL(feat_colterms, dim3(cdiv(std::max(ntn, ntm) * 32, 256), P, 2), dim3(256), 0, s, v.fct, v.gct,
+                       ntn, ntm, v.fmax, v.gmax, v.cbias);
+    PCR_LAUNCH_CHECK();
     prof_end(s, kProfFeatPack);
     return PCR_OK;
 }
@@ -2786,6 +2943,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
     r.Xr = F; r.sc = v.mx; r.role = 0; r.cs = v.sp.cs;  // featnn_row8 builds its rows from F
     r.cemax = v.gemax; r.nns = nns; r.fbdiag = 0; r.rbmajor = 0;
     r.rre = v.fre; r.bcnt = bcnt; r.blist = blist; r.bcap = cap1; r.rec = rec;
+    r.cct = v.gct; r.rct = v.fct; r.cbias = v.cbias;
     r.csl = 1; r.part = part; r.llist = nullptr; r.lcount = nullptr;
     if (prep_event && prep_at == 2) {
         PCR_HIP_CHECK(hipEventRecord(prep_event, s));
@@ -2883,7 +3041,7 @@ static int feature_corres_v5(const float *F, const float *G, int P, int Nmax, in
             r2b.rlist = v.fbl21; r2b.rcount = v.fbc21; r2b.list = nullptr; r2b.count = nullptr; r2b.fbdiag = 2;
             r2b.rbmajor = 1; r2b.csl = fsl;
             if (use9) {
-                r2.rre = v.gre; r2.bcap = cap2;
+                r2.rre = v.gre; r2.bcap = cap2; r2.cct = v.fct; r2.rct = v.gct;
                 PCR_HIP_CHECK(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)P * nst2, s));
                 if ((rc = launch_row9<false>(r2, v.S, s)) != PCR_OK) return rc;
                 prof_end(s, kProfFeatScreen2);
