@@ -1135,7 +1135,12 @@ def measure_s8d_job(batch, params, pair_ids, world, total_pairs, warmup=3, runs=
     from pointcloudregistration_amd.multigpu import gather_records
     from pointcloudregistration_amd.pipeline import PairPipeline
     P = batch.src.shape[0]
-    C = chunks or (4 if P >= 128 else (2 if P >= 32 else 1))
+    # 5 chunks at 256 pairs: a chunk pipeline costs ~0.94 ms + ~17.5 us per pair
+    # against ~41 us per pair of copy, so chunks of ~41+ pairs keep up with
+    # their copies and the smaller last chunk shortens the tail (measured, one
+    # box: C = 4 19,919-20,075, 5 20,224-20,496, 6 20,344-20,527, 7 19,485
+    # pairs/s; gpurun_out/s8d)
+    C = chunks or (5 if P >= 128 else (2 if P >= 32 else 1))
     C = max(1, min(C, P))
     L = max(1, min(lanes or 1, C, 4))
     bounds = [P * c // C for c in range(C + 1)]

@@ -1432,6 +1432,10 @@ __global__ __launch_bounds__(512) void featnn_row7(RowArgs5 a) {
 // ---------------------------------------------------------------------------
 constexpr int kRow8Head = 24;  // epilogue VALU in front of phase A's first MFMA (the B reads' latency)
 constexpr int kRow8G = 8;      // column tiles per LDS group (16: the whole LDS, measured no faster)
+#ifndef PCR_ROW9_G
+#define PCR_ROW9_G 16  // 8: pass 1 1.12 vs 1.09 ms, pass 2 0.76 vs 0.74 (C4, featnn_bench)
+#endif
+constexpr int kRow9G = PCR_ROW9_G;  // featnn_row9's
 // B: pass 1 1.0 (row k = 6) x 2^15 (G's column image, k = 6); pass 2 (featnn_row8
 // <.., false>, the J rows of G against F's image) 1.0 (row k = 7) x 2^15 (F's
 // image, k = 7).  dual7 pairs F's image with G's: 0 x 2^15 at both slots.
@@ -1973,7 +1977,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     constexpr int NB = S;                 // executed chunks: the f16 segment
     constexpr int kT = G * NB * 64;       // f16x8 of a B buffer's fragments
     constexpr int kB = kT + G * 8;        // + the group's column terms (G x 32 floats)
-    static_assert(G % 2 == 0 && S <= 2 && G * 8 <= 64, "column tiles in pairs; one DMA for the terms");
+    static_assert(G % 8 == 0 && S <= 2, "column tiles in pairs; the terms in whole 1 KB DMA pieces");
+    constexpr int kTC = G / 8;            // the group's terms: 1 KB pieces
     __shared__ __attribute__((aligned(16))) f16x8 Bs[2 * kB];
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
     const int ppx = (a.P + 7) >> 3;
@@ -2002,12 +2007,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     const f16x8 *bsrc = a.Bp + (size_t)p * a.ntc * NM * 64 + l;
     const float *csrc = a.cct + (size_t)p * a.ntc * 32 + 4 * l;
     auto issue = [&](int grp, int bufi) {
-        for (int c = wid; c < G * NB + 1; c += W) {
-            if (c == G * NB) {  // the group's column terms: G x 128 B, one 16-B piece per lane
-                if (l < G * 8)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void *)(csrc + (size_t)grp * G * 32),
-                        (__attribute__((address_space(3))) void *)(Bs + bufi * kB + kT), 16, 0, 0);
+        for (int c = wid; c < G * NB + kTC; c += W) {
+            if (c >= G * NB) {  // the group's column terms: G x 128 B, 16 B per lane and piece
+                const int tc = c - G * NB;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(csrc + (size_t)grp * G * 32 + tc * 256),
+                    (__attribute__((address_space(3))) void *)(Bs + bufi * kB + kT + tc * 64), 16, 0, 0);
                 continue;
             }
             const int g = c / NB, cc = c - g * NB;
@@ -2540,7 +2545,7 @@ static int v5_prepare(const float *F, const float *G, int P, int Nmax, int Mmax,
     // row tiles, padded to whole blocks of the dual screen (8 tiles) and of the
     // row screens (8 waves x row_tiles(S) tiles; the sentinel rows are valid encodings)
     v.ntn = cdiv(cdiv(Nmax, 32), 16) * 16;
-    v.ntm = cdiv(cdiv(Mmax, 32), kRow8G) * kRow8G;  // column tiles, padded to whole groups (G | 8)
+    v.ntm = cdiv(cdiv(Mmax, 32), std::max(kRow8G, kRow9G)) * std::max(kRow8G, kRow9G);  // column tiles, whole groups
     v.ctbits = 1;
     while ((1 << v.ctbits) < std::max(v.ntm, v.ntn)) ++v.ctbits;
     PCR_REQUIRE(v.ctbits <= 16, PCR_ERR_ARG, "feature_match: N=%d / M=%d too large", Nmax, Mmax);
@@ -2769,8 +2774,8 @@ static int launch_row9(const RowArgs5 &r0, int S, hipStream_t s) {
     r.nrb = cdiv(cdiv(r.Rmax, 32), 8 * 2);  // 8 waves x 2 row tiles per workgroup
     const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
-    if (S == 1) hipLaunchKernelGGL((featnn_row9<1, kRow8G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
-    else hipLaunchKernelGGL((featnn_row9<2, kRow8G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    if (S == 1) hipLaunchKernelGGL((featnn_row9<1, kRow9G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    else hipLaunchKernelGGL((featnn_row9<2, kRow9G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
