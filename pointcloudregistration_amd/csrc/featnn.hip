@@ -1435,7 +1435,11 @@ constexpr int kRow8G = 8;      // column tiles per LDS group (16: the whole LDS,
 #ifndef PCR_ROW9_G
 #define PCR_ROW9_G 16  // 8: pass 1 1.12 vs 1.09 ms, pass 2 0.76 vs 0.74 (C4, featnn_bench)
 #endif
-constexpr int kRow9G = PCR_ROW9_G;  // featnn_row9's
+#ifndef PCR_ROW9_G1
+#define PCR_ROW9_G1 PCR_ROW9_G
+#endif
+constexpr int kRow9G = PCR_ROW9_G;     // featnn_row9's: pass 2 (and the padding)
+constexpr int kRow9G1 = PCR_ROW9_G1;   // pass 1 (<= kRow9G)
 // B: pass 1 1.0 (row k = 6) x 2^15 (G's column image, k = 6); pass 2 (featnn_row8
 // <.., false>, the J rows of G against F's image) 1.0 (row k = 7) x 2^15 (F's
 // image, k = 7).  dual7 pairs F's image with G's: 0 x 2^15 at both slots.
@@ -2774,8 +2778,9 @@ static int launch_row9(const RowArgs5 &r0, int S, hipStream_t s) {
     r.nrb = cdiv(cdiv(r.Rmax, 32), 8 * 2);  // 8 waves x 2 row tiles per workgroup
     const long long nblk = 8LL * r.nrb * cdiv(r.P, 8);  // XCD-aware 1-D grid
     PCR_REQUIRE(nblk < (1LL << 31), PCR_ERR_ARG, "feature_corres: grid too large");
-    if (S == 1) hipLaunchKernelGGL((featnn_row9<1, kRow9G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
-    else hipLaunchKernelGGL((featnn_row9<2, kRow9G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    constexpr int G = kIdx ? kRow9G1 : kRow9G;
+    if (S == 1) hipLaunchKernelGGL((featnn_row9<1, G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
+    else hipLaunchKernelGGL((featnn_row9<2, G, kIdx>), dim3((unsigned)nblk), dim3(512), 0, s, r);
     PCR_LAUNCH_CHECK();
     return PCR_OK;
 }
