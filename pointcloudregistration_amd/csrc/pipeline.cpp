@@ -120,6 +120,7 @@ extern "C" int pcr_pipeline_step(const pcr_pipeline_io *io, const pcr_ransac_par
     // its own side stream beside pass 2: 256 pairs at 1 / 2 8.21 / 8.08 ms (one
     // box), 32 pairs 1.59 / 1.57, 64 and 128 pairs 0 / 1 / 2 within 0.03 ms
     int at = (P >= 192 || P <= 48) ? 2 : 0;
+    if (const char *e = getenv("PCR_PREP_AT")) at = atoi(e);  // diagnostic override (0 / 1 / 2)
     if (io->D > 64) at = 0;
     pcr::GridBatch grid_r{}, grid_i{};
     const int32_t *order = nullptr;  // RANSAC's spatial order of the sources, reused by ICP
