@@ -917,20 +917,20 @@ def grid_candidates(src, tgt, T, d, slot_num=2):
 
 
 # Per 32 x 32 tile and wave, the inner loop of the shipped build's screens
-# (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 8
-# column tiles = 16 tiles, D = 32 -> the 1-term screen executes S = 2 k-chunks
+# (tools/isa_loop_mix.py on the gfx950 ISA; one loop trip = 2 row tiles x 16
+# column tiles = 32 tiles, D = 32 -> the 1-term screen executes S = 2 k-chunks
 # of 16, the f16(x) segment, with the columns' |y|^2 + B as the MFMA's C):
-#  featnn_row9<2,8,true> (pass 1): 2 v_mfma_f32_32x32x16_f16, 20.7 VALU per
-#    tile (per 16 tiles: 124 v_min3_u32 + 24 v_min + 8 x (v_max, v_cmp,
-#    v_cndmask) + 128 v_mov_b32_dpp -- the C operand's row broadcasts -- + 23
-#    other), 1.5 LDS reads, 0.5 s_nop;
-#  featnn_row9<2,8,false> (pass 2): the same with the C operand as 4
-#    ds_read_b128 per column tile: 12.6 VALU, 3 LDS reads, 0.4 s_nop.
+#  featnn_row9<2,16,true> (pass 1): 2 v_mfma_f32_32x32x16_f16, 19.8 VALU per
+#    tile (per 32 tiles: 240 v_min3_u32 + 48 v_min + 16 x (v_med3, v_cmp,
+#    v_cndmask) + 256 v_mov_b32_dpp -- the C operand's row broadcasts -- + 41
+#    other), 1.5 LDS reads, 0.3 s_nop;
+#  featnn_row9<2,16,false> (pass 2): the same with the C operand as 4
+#    ds_read_b128 per column tile: 11.8 VALU, 3 LDS reads, 0.25 s_nop.
 # SIMD issue cycles (MI355X guide, 'vector-instruction ISSUE cost'): an MFMA holds
 # vector issue 8 of its 32 cycles, VALU / LDS / s_nop 4 each; the waves of a SIMD
 # share that port.  The MFMA pipe needs 2 x 32 = 64 cycles per tile.
-SCREEN_TILE_ISSUE = {"mfma": 2 * 8, "valu": 331 / 16 * 4, "lds": 24 / 16 * 4, "s_nop": 8 / 16 * 4}
-SCREEN_TILE_ISSUE2 = {"mfma": 2 * 8, "valu": 202 / 16 * 4, "lds": 48 / 16 * 4, "s_nop": 6 / 16 * 4}
+SCREEN_TILE_ISSUE = {"mfma": 2 * 8, "valu": 633 / 32 * 4, "lds": 48 / 32 * 4, "s_nop": 10 / 32 * 4}
+SCREEN_TILE_ISSUE2 = {"mfma": 2 * 8, "valu": 376 / 32 * 4, "lds": 96 / 32 * 4, "s_nop": 8 / 32 * 4}
 SCREEN_TILE_MFMA = 2
 
 
@@ -1383,7 +1383,7 @@ def main():
                      "traffic_source": f"{_traffic_source()} (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this bench; FETCH_SIZE x2 per the "
                                        "gfx950 note)",
-                     "kernel": "featnn_row9<2,8,true> (pass 1: 1-term f16 screen on "
+                     "kernel": "featnn_row9<2,16,true> (pass 1: 1-term f16 screen on "
                                "v_mfma_f32_32x32x16_f16 with the operands transposed -- a lane "
                                "holds one row --, the columns' |y|^2 + B as the MFMA's accumulator "
                                "input (2 MFMAs per tile) and a group-min sweep; featnn_regroup9 "
@@ -1394,7 +1394,7 @@ def main():
                      "executed_frac": executed / PEAK_F16_MFMA_TFLOPS,
                      "vs_f32_mfma_peak": achieved / PEAK_F32_MFMA_TFLOPS,
                      "issue_model": _screen_issue_model(tiles1, per_launch_ms, SCREEN_TILE_ISSUE),
-                     "pass2": {"kernel": "featnn_row9<2,8,false> (target rows J = unique(nn12), "
+                     "pass2": {"kernel": "featnn_row9<2,16,false> (target rows J = unique(nn12), "
                                          "values only)",
                                "kernel_ms_per_launch": per2_ms, "launches": launches2,
                                "j_rows_mean": float(jrows.mean()),

@@ -2040,7 +2040,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     // row tile t's group of step st closed by its second column tile y
     auto close = [&](const f32x16 &y, int t, unsigned st) {
         const unsigned mn = min16(y, pm[t]);
-        const unsigned n2 = umin2(umax2(B1[t], mn), B2[t]);  // 2nd smallest of {B1, B2, mn}
+        // 2nd smallest of {B1, B2, mn}: their median (the full pattern, so it
+        // selects to one v_med3_u32)
+        const unsigned n2 = umax2(umin2(B1[t], B2[t]), umin2(umax2(B1[t], B2[t]), mn));
         I[t] = mn < B1[t] ? st : I[t];
         B1[t] = umin2(B1[t], mn);
         B2[t] = n2;
