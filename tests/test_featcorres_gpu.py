@@ -302,3 +302,34 @@ def test_feature_correspondences_row8_one_term(oracle, monkeypatch, name):
     assert np.array_equal(_np(nn12)[0], e12)
     assert int(_np(nc)[0]) == len(exp)
     assert np.array_equal(_np(co)[0, :len(exp)], exp)
+
+
+def test_colterm_bias_per_pair(oracle):
+    """featnn_row9's column terms ct = f32(|y|^2 + B) with B the pair's power of
+    two above BOTH clouds' max |x|^2 (feat_colterms, csrc/featnn.hip): pairs whose
+    clouds differ by decades in norm (B set by the rows in pass 1, by the columns
+    in pass 2), a single huge-norm row, an all-zero target cloud but one row (B
+    near 1), tiny descriptors (the pair scale lifts them) -- in one batch, every
+    pair equal to the oracle."""
+    P, N, M, D = 6, 600, 550, 32
+    rng = np.random.default_rng(21)
+    code = rng.standard_normal((P, 800, D)).astype(np.float32)
+    fs = np.stack([code[p, rng.permutation(800)[:N]] for p in range(P)]) + \
+        rng.normal(0, 0.6, (P, N, D)).astype(np.float32)
+    ft = np.stack([code[p, rng.permutation(800)[:M]] for p in range(P)]) + \
+        rng.normal(0, 0.6, (P, M, D)).astype(np.float32)
+    fs, ft = fs.astype(np.float32), ft.astype(np.float32)
+    fs[1] *= np.float32(1000.0)
+    ft[2] *= np.float32(1000.0)
+    fs[3, 17] *= np.float32(1e4)
+    ft[4] = 0.0
+    ft[4, 5] = fs[4, 9]
+    fs[5] *= np.float32(1e-20)
+    ft[5] *= np.float32(1e-20)
+    co, nc, nn12 = reg.feature_correspondences(fs, ft)
+    for p in range(P):
+        e12 = oracle.featnn(fs[p], ft[p])
+        exp = oracle.corres(e12, oracle.featnn(ft[p], fs[p]), True, 3)
+        assert np.array_equal(_np(nn12)[p], e12), p
+        assert int(_np(nc)[p]) == len(exp), p
+        assert np.array_equal(_np(co)[p, :len(exp)], exp), p
